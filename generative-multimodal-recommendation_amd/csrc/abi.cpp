@@ -1,0 +1,31 @@
+// C-ABI plumbing of libgmr_hip.so: error reporting and version.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/gmr.h"
+
+namespace gmr {
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fn, const char* msg) { snprintf(g_err, sizeof(g_err), "%s: %s", fn, msg); }
+
+int hip_status(const char* fn, hipError_t e) {
+  snprintf(g_err, sizeof(g_err), "%s: HIP error %d (%s)", fn, (int)e, hipGetErrorString(e));
+  return -(int)e;
+}
+}  // namespace gmr
+
+extern "C" const char* gmr_last_error_string(void) { return gmr::g_err; }
+
+extern "C" int gmr_version(void) { return GMR_ABI_VERSION; }
+
+extern "C" int gmr_device_name(char* buf, int32_t len) {
+  hipDeviceProp_t p;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipGetDeviceProperties(&p, dev);
+  if (e != hipSuccess) return gmr::hip_status(__func__, e);
+  snprintf(buf, (size_t)len, "%s", p.gcnArchName);
+  return GMR_OK;
+}

@@ -1,0 +1,619 @@
+// Fused row-wise kernels of the DiffMM recommendation step (forward + hand-derived backward).
+//
+// Layout in HBM (N = U + I nodes, d = 64):
+//   E0      = [uEmbeds; iEmbeds]            N x 64   (one contiguous parameter slab)
+//   NF      = [norm(imgF) | norm(txtF)]     I x 128
+//   G, H    = adj @ [...] for image|text    N x 128
+//   Q_img   = iadj @ [E0 | S_img]           N x 128  (ris-adj term | contrastive view)
+//   E       = G + H + lambda * [IA | TA]    N x 128  (written over G)
+//   M       = w0 * E_img + w1 * E_txt       N x 64
+//   Emb     = M + adj@M + ris * norm(M)     N x 64   (forward_MM output)
+// Reference: models/diffmm.py:129-258.
+#include "gmr_common.h"
+
+namespace {
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+__device__ __forceinline__ float4 f4(float a, float b, float c, float d) { return make_float4(a, b, c, d); }
+__device__ __forceinline__ float4 sub4(float4 a, float4 b) { return f4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
+__device__ __forceinline__ float4 mul4(float4 a, float4 b) { return f4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w); }
+
+// reduce across the 16 lanes that hold one 64-float row
+__device__ __forceinline__ float row16_sum(float v) {
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+__device__ __forceinline__ void softmax2(const float* mw, float& w0, float& w1) {
+  float a = mw[0], b = mw[1];
+  float mx = fmaxf(a, b);
+  float ea = expf(a - mx), eb = expf(b - mx);
+  float s = ea + eb;
+  w0 = ea / s;
+  w1 = eb / s;
+}
+
+// E = G + H + lam * [Qi[:, :64] | Qt[:, :64]] (in place over G);  M = w0*E_img + w1*E_txt
+__global__ void combine_fwd_kernel(int64_t n, float* __restrict__ G, const float* __restrict__ H,
+                                   const float* __restrict__ Qi, const float* __restrict__ Qt,
+                                   const float* __restrict__ mw, float lam, float* __restrict__ M) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n * 16) return;
+  const int64_t r = gid >> 4;
+  const int c = (gid & 15) * 4;
+  float w0, w1;
+  softmax2(mw, w0, w1);
+  float4 gi = ld4(G + r * 128 + c), gt = ld4(G + r * 128 + 64 + c);
+  float4 hi = ld4(H + r * 128 + c), ht = ld4(H + r * 128 + 64 + c);
+  float4 ai = ld4(Qi + r * 128 + c), at = ld4(Qt + r * 128 + c);
+  float4 ei = gmr::f4_fma(lam, ai, gmr::f4_add(gi, hi));
+  float4 et = gmr::f4_fma(lam, at, gmr::f4_add(gt, ht));
+  st4(G + r * 128 + c, ei);
+  st4(G + r * 128 + 64 + c, et);
+  st4(M + r * 64 + c, gmr::f4_fma(w1, et, gmr::f4_scale(w0, ei)));
+}
+
+// Emb = M + L + ris * M / max(|M|, 1e-12); nrm[r] = max(|M_r|, 1e-12)
+__global__ void final_fwd_kernel(int64_t n, const float* __restrict__ M, const float* __restrict__ L, float ris,
+                                 float* __restrict__ Emb, float* __restrict__ nrm) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = gid >> 4;
+  const bool ok = r < n;
+  const int c = (gid & 15) * 4;
+  float4 m = ok ? ld4(M + r * 64 + c) : f4(0, 0, 0, 0);
+  float ss = row16_sum(dot4(m, m));
+  if (!ok) return;
+  float nv = fmaxf(sqrtf(ss), 1e-12f);
+  float4 l = ld4(L + r * 64 + c);
+  st4(Emb + r * 64 + c, gmr::f4_fma(ris / nv, m, gmr::f4_add(m, l)));
+  if ((gid & 15) == 0) nrm[r] = nv;
+}
+
+// contrastive views: K = C + K2 (C = Q[:, 64:]); CLN = normalize(K + 1e-8) for image|text -> N x 128
+__global__ void cl_fwd_kernel(int64_t n, const float* __restrict__ Qi, const float* __restrict__ Qt,
+                              const float* __restrict__ K2, float* __restrict__ CLN, float* __restrict__ nrm) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = gid >> 5;  // 32 threads per row: 16 image + 16 text
+  const bool ok = r < n;
+  const int half = (gid >> 4) & 1;
+  const int c = (gid & 15) * 4;
+  const float* Q = half ? Qt : Qi;
+  float4 k = ok ? gmr::f4_add(ld4(Q + r * 128 + 64 + c), ld4(K2 + r * 128 + half * 64 + c)) : f4(0, 0, 0, 0);
+  k = f4(k.x + 1e-8f, k.y + 1e-8f, k.z + 1e-8f, k.w + 1e-8f);
+  float ss = row16_sum(dot4(k, k));
+  if (!ok) return;
+  float nv = fmaxf(sqrtf(ss), 1e-12f);
+  st4(CLN + r * 128 + half * 64 + c, gmr::f4_scale(1.f / nv, k));
+  if ((gid & 15) == 0) nrm[half * n + r] = nv;  // [img norms | txt norms]
+}
+
+// Row L2-normalisation of a column block: y = x / max(|x|, eps). 16 lanes per 64 columns.
+__global__ void normalize_rows_kernel(int64_t n, int cols, const float* __restrict__ x, int64_t ldx, float* __restrict__ y,
+                                      int64_t ldy, float* __restrict__ nrm) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = gid >> 4;
+  const bool ok = r < n;
+  const int l = gid & 15;
+  float ss = 0.f;
+  if (ok)
+    for (int c = l * 4; c < cols; c += 64) {
+      float4 v = ld4(x + r * ldx + c);
+      ss += dot4(v, v);
+    }
+  ss = row16_sum(ss);
+  if (!ok) return;
+  float nv = fmaxf(sqrtf(ss), 1e-12f);
+  for (int c = l * 4; c < cols; c += 64) st4(y + r * ldy + c, gmr::f4_scale(1.f / nv, ld4(x + r * ldx + c)));
+  if (l == 0 && nrm) nrm[r] = nv;
+}
+
+// normalize backward: dx = (dy - y <y,dy>) / nrm   (y = output, nrm = clamped norm);
+// if nrm was clamped (== eps) the projection term vanishes.  Optional leaky-ReLU backward
+// on the pre-normalised input (sign(x) == sign(y)).  dx may alias dy.
+__global__ void normalize_bwd_kernel(int64_t n, int cols, const float* __restrict__ y, int64_t ldy,
+                                     const float* __restrict__ nrm, const float* dy, int64_t lddy, float* dx,
+                                     int64_t lddx, float slope, int accumulate) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = gid >> 4;
+  const bool ok = r < n;
+  const int l = gid & 15;
+  float dp = 0.f;
+  if (ok)
+    for (int c = l * 4; c < cols; c += 64) dp += dot4(ld4(y + r * ldy + c), ld4(dy + r * lddy + c));
+  dp = row16_sum(dp);
+  if (!ok) return;
+  const float nv = nrm[r];
+  if (nv <= 1e-12f) dp = 0.f;
+  const float inv = 1.f / nv;
+  for (int c = l * 4; c < cols; c += 64) {
+    float4 yy = ld4(y + r * ldy + c);
+    float4 g = gmr::f4_scale(inv, sub4(ld4(dy + r * lddy + c), gmr::f4_scale(dp, yy)));
+    if (slope != 1.f) {
+      g.x *= yy.x > 0.f ? 1.f : slope;
+      g.y *= yy.y > 0.f ? 1.f : slope;
+      g.z *= yy.z > 0.f ? 1.f : slope;
+      g.w *= yy.w > 0.f ? 1.f : slope;
+    }
+    float* o = dx + r * lddx + c;
+    if (accumulate) g = gmr::f4_add(g, ld4(o));
+    st4(o, g);
+  }
+}
+
+// BPR with gathers: x = <a,p> - <a,n>;  loss_b = -log(1e-10 + sigmoid(x));
+// contributions (scaled by 1/B): slot b -> d a, slot B+b -> d p, slot 2B+b -> d n.
+__global__ void bpr_kernel(int B, int64_t U, const float* __restrict__ Emb, const int* __restrict__ users,
+                           const int* __restrict__ pos, const int* __restrict__ neg, float* __restrict__ loss,
+                           float* __restrict__ contrib) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = gid >> 4;
+  const bool ok = b < B;
+  const int c = (gid & 15) * 4;
+  float4 a = f4(0, 0, 0, 0), p = a, q = a;
+  if (ok) {
+    a = ld4(Emb + (int64_t)users[b] * 64 + c);
+    p = ld4(Emb + (U + pos[b]) * 64 + c);
+    q = ld4(Emb + (U + neg[b]) * 64 + c);
+  }
+  float x = row16_sum(dot4(a, p) - dot4(a, q));
+  if (!ok) return;
+  float s = 1.f / (1.f + expf(-x));
+  float gx = -(s * (1.f - s)) / (1e-10f + s) / (float)B;
+  if ((gid & 15) == 0) loss[b] = -logf(1e-10f + s);
+  st4(contrib + (int64_t)b * 64 + c, gmr::f4_scale(gx, sub4(p, q)));
+  st4(contrib + ((int64_t)B + b) * 64 + c, gmr::f4_scale(gx, a));
+  st4(contrib + (2 * (int64_t)B + b) * 64 + c, gmr::f4_scale(-gx, a));
+}
+
+// Row softmax of contrastive logits L (already divided by temp), in place:
+//   S_b = sum_j exp(L_bj)   (no max subtraction, as the reference; |L| <= 1/temp)
+//   P_bj = coef * exp(L_bj) / S_b ;  lse[b] = log S_b
+__global__ void __launch_bounds__(256) row_softmax_kernel(int64_t rows, int64_t cols, float* __restrict__ L, int64_t ld,
+                                                          float coef, float* __restrict__ lse) {
+  const int64_t r = blockIdx.x;
+  if (r >= rows) return;
+  float* p = L + r * ld;
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int64_t j = threadIdx.x; j < cols; j += 256) s += expf(p[j]);
+  s = gmr::wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const float S = (red[0] + red[1]) + (red[2] + red[3]);
+  const float k = coef / S;
+  for (int64_t j = threadIdx.x; j < cols; j += 256) p[j] = k * expf(p[j]);
+  if (threadIdx.x == 0) lse[r] = logf(S);
+}
+
+// contrastive per-row terms for a gathered batch.  For row b with node t_b:
+//   loss_b = lse_b - <p1_b, p2_b>/temp     (p1 = CLN[t_b, 0:64], p2 = CLN[t_b, 64:128])
+//   contrib (128 wide): [ -coef/temp * p2_b | -coef/temp * p1_b ]  (dp1 dense part added by GEMM)
+__global__ void contrast_rows_kernel(int B, const float* __restrict__ CLN, const int* __restrict__ nodes, int64_t node_off,
+                                     const float* __restrict__ lse, float inv_temp, float coef, float* __restrict__ loss,
+                                     float* __restrict__ contrib, int64_t ld_contrib) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = gid >> 4;
+  const bool ok = b < B;
+  const int c = (gid & 15) * 4;
+  float4 p1 = f4(0, 0, 0, 0), p2 = p1;
+  if (ok) {
+    const int64_t t = node_off + nodes[b];
+    p1 = ld4(CLN + t * 128 + c);
+    p2 = ld4(CLN + t * 128 + 64 + c);
+  }
+  float d = row16_sum(dot4(p1, p2));
+  if (!ok) return;
+  if ((gid & 15) == 0) loss[b] = lse[b] - d * inv_temp;
+  const float k = -coef * inv_temp;
+  float* o = contrib + (int64_t)b * ld_contrib;
+  st4(o + c, gmr::f4_fma(k, p2, ld4(o + c)));  // adds to dp1 produced by P @ table (already in contrib)
+  st4(o + 64 + c, gmr::f4_scale(k, p1));
+}
+
+// gather rows: out[b] = src[off + idx[b]] (cols % 4 == 0)
+__global__ void gather_rows_kernel(int B, int cols, const float* __restrict__ src, int64_t lds, const int* __restrict__ idx,
+                                   int64_t off, float* __restrict__ out, int64_t ldo) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c4 = cols / 4;
+  const int64_t b = gid / c4;
+  if (b >= B) return;
+  const int c = (int)(gid % c4) * 4;
+  st4(out + b * ldo + c, ld4(src + (off + idx[b]) * lds + c));
+}
+
+// Deterministic scatter-add of contribution rows through a sorted (key << 32 | slot) plan:
+// each run of equal keys is summed in slot order and added to dst[key] (one 16-lane group per
+// run start; runs are disjoint so there is no write race).
+__global__ void scatter_sorted_kernel(int n, int cols, const unsigned long long* __restrict__ plan,
+                                      const float* __restrict__ contrib, int64_t ldc, float* __restrict__ dst,
+                                      int64_t ldd) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lanes = cols / 4;
+  const int64_t i = gid / lanes;
+  if (i >= n) return;
+  const int c = (int)(gid % lanes) * 4;
+  const unsigned long long e = plan[i];
+  const unsigned key = (unsigned)(e >> 32);
+  if (key == 0xFFFFFFFFu) return;
+  if (i > 0 && (unsigned)(plan[i - 1] >> 32) == key) return;
+  float4 s = f4(0, 0, 0, 0);
+  for (int64_t j = i; j < n; ++j) {
+    const unsigned long long ej = plan[j];
+    if ((unsigned)(ej >> 32) != key) break;
+    s = gmr::f4_add(s, ld4(contrib + (int64_t)(unsigned)(ej & 0xFFFFFFFFull) * ldc + c));
+  }
+  float* o = dst + (int64_t)key * ldd + c;
+  st4(o, gmr::f4_add(ld4(o), s));
+}
+
+// final backward: dM = dEmb + T1 + ris * nbwd(M, dEmb);  dE = [w0 dM | w1 dM];
+// per-block partial sums of <E_img, dM>, <E_txt, dM> for the modal-weight gradient.
+__global__ void __launch_bounds__(256) final_bwd_kernel(int64_t n, const float* __restrict__ dEmb,
+                                                        const float* __restrict__ T1, const float* __restrict__ M,
+                                                        const float* __restrict__ nrmM, float ris,
+                                                        const float* __restrict__ E, const float* __restrict__ mw,
+                                                        float* __restrict__ dE, float* __restrict__ part) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = gid >> 4;
+  const bool ok = r < n;
+  const int c = (gid & 15) * 4;
+  float w0, w1;
+  softmax2(mw, w0, w1);
+  float4 g = f4(0, 0, 0, 0), m = g, t = g;
+  float nv = 1.f;
+  if (ok) {
+    g = ld4(dEmb + r * 64 + c);
+    m = ld4(M + r * 64 + c);
+    t = ld4(T1 + r * 64 + c);
+    nv = nrmM[r];
+  }
+  float4 y = gmr::f4_scale(1.f / nv, m);
+  float dp = row16_sum(dot4(y, g));
+  if (nv <= 1e-12f) dp = 0.f;
+  float4 dm = gmr::f4_add(gmr::f4_add(g, t), gmr::f4_scale(ris / nv, sub4(g, gmr::f4_scale(dp, y))));
+  float si = 0.f, st = 0.f;
+  if (ok) {
+    float4 ei = ld4(E + r * 128 + c), et = ld4(E + r * 128 + 64 + c);
+    si = dot4(ei, dm);
+    st = dot4(et, dm);
+    st4(dE + r * 128 + c, gmr::f4_scale(w0, dm));
+    st4(dE + r * 128 + 64 + c, gmr::f4_scale(w1, dm));
+  }
+  __shared__ float red[2][4];
+  si = gmr::wave_sum(si);
+  st = gmr::wave_sum(st);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = si;
+    red[1][threadIdx.x >> 6] = st;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[blockIdx.x * 2 + 0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    part[blockIdx.x * 2 + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+}
+
+// modal-weight gradient: dw_i = sum of partials; dmw = w .* (dw - <w, dw>)  (softmax backward)
+__global__ void mw_grad_kernel(int nparts, const float* __restrict__ part, const float* __restrict__ mw,
+                               float* __restrict__ dmw, int accumulate) {
+  __shared__ float red[2][4];
+  float a = 0.f, b = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) {
+    a += part[2 * i];
+    b += part[2 * i + 1];
+  }
+  a = gmr::wave_sum(a);
+  b = gmr::wave_sum(b);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = a;
+    red[1][threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float da = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    float db = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    float w0, w1;
+    softmax2(mw, w0, w1);
+    float s = w0 * da + w1 * db;
+    float g0 = w0 * (da - s), g1 = w1 * (db - s);
+    dmw[0] = accumulate ? dmw[0] + g0 : g0;
+    dmw[1] = accumulate ? dmw[1] + g1 : g1;
+  }
+}
+
+// dG = dE + [T2[:U]; 0]   (N x 128)
+__global__ void dg_kernel(int64_t n, int64_t U, const float* __restrict__ dE, const float* __restrict__ T2,
+                          float* __restrict__ dG) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n * 32) return;
+  const int64_t r = gid >> 5;
+  const int c = (int)(gid & 31) * 4;
+  float4 v = ld4(dE + r * 128 + c);
+  if (r < U) v = gmr::f4_add(v, ld4(T2 + r * 128 + c));
+  st4(dG + r * 128 + c, v);
+}
+
+// contrastive backward through "K = C + adj@C":  dC = dK + T  (in place over T); also
+// build the iadj/tadj backward sources  Rsrc_img = [lam*dE_img | dC_img], Rsrc_txt likewise.
+__global__ void cl_bwd_kernel(int64_t n, const float* __restrict__ dK, const float* __restrict__ T,
+                              const float* __restrict__ dE, float lam, float* __restrict__ Ri,
+                              float* __restrict__ Rt) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n * 16) return;
+  const int64_t r = gid >> 4;
+  const int c = (int)(gid & 15) * 4;
+  float4 dci = gmr::f4_add(ld4(dK + r * 128 + c), ld4(T + r * 128 + c));
+  float4 dct = gmr::f4_add(ld4(dK + r * 128 + 64 + c), ld4(T + r * 128 + 64 + c));
+  st4(Ri + r * 128 + c, gmr::f4_scale(lam, ld4(dE + r * 128 + c)));
+  st4(Ri + r * 128 + 64 + c, dci);
+  st4(Rt + r * 128 + c, gmr::f4_scale(lam, ld4(dE + r * 128 + 64 + c)));
+  st4(Rt + r * 128 + 64 + c, dct);
+}
+
+// gradient assembly:
+//   dE0[:U]  += T3u_img + T3u_txt + Ri[:U, :64] + Ri[:U, 64:] + Rt[:U, :64] + Rt[:U, 64:] + 2 reg uE
+//   dE0[U:]  += T2i_img + T2i_txt + Ri[U:, :64] + Rt[U:, :64] + 2 reg iE
+//   dNF[:, :64] = T3[U:, :64] + Ri[U:, 64:] ;  dNF[:, 64:] = T3[U:, 64:] + Rt[U:, 64:]
+// T2 = adj@dE (its item rows feed diE), T3 = adj@dG.
+__global__ void assemble_kernel(int64_t n, int64_t U, const float* __restrict__ T2, const float* __restrict__ T3,
+                                const float* __restrict__ Ri, const float* __restrict__ Rt,
+                                const float* __restrict__ E0, float reg2, float* __restrict__ dE0,
+                                float* __restrict__ dNF) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n * 16) return;
+  const int64_t r = gid >> 4;
+  const int c = (int)(gid & 15) * 4;
+  const int64_t o = r * 128 + c;
+  float4 g;
+  if (r < U) {
+    g = gmr::f4_add(ld4(T3 + o), ld4(T3 + o + 64));
+    g = gmr::f4_add(g, gmr::f4_add(ld4(Ri + o), ld4(Ri + o + 64)));
+    g = gmr::f4_add(g, gmr::f4_add(ld4(Rt + o), ld4(Rt + o + 64)));
+  } else {
+    g = gmr::f4_add(ld4(T2 + o), ld4(T2 + o + 64));
+    g = gmr::f4_add(g, gmr::f4_add(ld4(Ri + o), ld4(Rt + o)));
+    const int64_t ri = r - U;
+    st4(dNF + ri * 128 + c, gmr::f4_add(ld4(T3 + o), ld4(Ri + o + 64)));
+    st4(dNF + ri * 128 + 64 + c, gmr::f4_add(ld4(T3 + o + 64), ld4(Rt + o + 64)));
+  }
+  g = gmr::f4_fma(reg2, ld4(E0 + r * 64 + c), g);
+  float* d = dE0 + r * 64 + c;
+  st4(d, gmr::f4_add(ld4(d), g));
+}
+
+// sum of a float vector into out[0] (single block, deterministic); optional scale and accumulation
+__global__ void sum_kernel(int64_t n, const float* __restrict__ x, float scale, float* __restrict__ out, int accumulate) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) s += (double)x[i];
+  s = gmr::wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = (float)(((red[0] + red[1]) + (red[2] + red[3])) * (double)scale);
+    out[0] = accumulate ? out[0] + v : v;
+  }
+}
+
+// squared Frobenius norm -> single value (deterministic, one block of 1024)
+__global__ void sqnorm_kernel(int64_t n, const float* __restrict__ x, float scale, float* __restrict__ out, int accumulate) {
+  __shared__ double red[16];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) {
+    double v = x[i];
+    s += v * v;
+  }
+  s = gmr::wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0;
+    for (int i = 0; i < 16; ++i) t += red[i];
+    float v = (float)(t * (double)scale);
+    out[0] = accumulate ? out[0] + v : v;
+  }
+}
+
+// bitonic sort of one keyset per block: pairs (key << 32 | slot), size padded to pow2 <= 8192
+__global__ void __launch_bounds__(1024) sort_keys_kernel(const int* __restrict__ keys, const int64_t* __restrict__ offs,
+                                                         const int* __restrict__ key_add, int n_keysets_per_batch,
+                                                         int64_t key_stride, unsigned long long* __restrict__ out,
+                                                         int64_t out_stride, int pow2) {
+  __shared__ unsigned long long s[8192];
+  // block = (batch, keyset); keyset k covers slots [k*len, (k+1)*len) of the batch's key list
+  const int64_t batch = blockIdx.x;
+  const int64_t beg = offs[batch], end = offs[batch + 1];
+  const int len = (int)(end - beg);
+  const int nk = n_keysets_per_batch;
+  const int total = len * nk;
+  for (int i = threadIdx.x; i < pow2; i += 1024) {
+    unsigned long long v = ~0ull;
+    if (i < total) {
+      const int k = i / len, j = i % len;
+      const unsigned key = (unsigned)(keys[k * key_stride + beg + j] + key_add[k]);
+      v = ((unsigned long long)key << 32) | (unsigned)i;
+    }
+    s[i] = v;
+  }
+  __syncthreads();
+  for (int size = 2; size <= pow2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < pow2 / 2; i += 1024) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = ((lo & size) == 0);
+        unsigned long long a = s[lo], b = s[hi];
+        if ((a > b) == up) {
+          s[lo] = b;
+          s[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < pow2; i += 1024) out[batch * out_stride + i] = s[i];
+}
+
+}  // namespace
+
+#define ROWS16(n) dim3(gmr::grid_for((n) * 16, 256)), dim3(256)
+
+extern "C" int gmr_dmm_combine_fwd(int64_t n, float* G, const float* H, const float* Qi, const float* Qt,
+                                   const float* mw, float lam, float* M, void* stream) {
+  GMR_ARG(G && H && Qi && Qt && mw && M && n > 0, "bad args");
+  hipLaunchKernelGGL(combine_fwd_kernel, ROWS16(n), 0, (hipStream_t)stream, n, G, H, Qi, Qt, mw, lam, M);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dmm_final_fwd(int64_t n, const float* M, const float* L, float ris, float* Emb, float* nrm,
+                                 void* stream) {
+  GMR_ARG(M && L && Emb && nrm && n > 0, "bad args");
+  hipLaunchKernelGGL(final_fwd_kernel, ROWS16(n), 0, (hipStream_t)stream, n, M, L, ris, Emb, nrm);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dmm_cl_fwd(int64_t n, const float* Qi, const float* Qt, const float* K2, float* CLN, float* nrm,
+                              void* stream) {
+  GMR_ARG(Qi && Qt && K2 && CLN && nrm && n > 0, "bad args");
+  hipLaunchKernelGGL(cl_fwd_kernel, dim3(gmr::grid_for(n * 32, 256)), dim3(256), 0, (hipStream_t)stream, n, Qi, Qt, K2,
+                     CLN, nrm);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_normalize_rows_f32(int64_t n, int32_t cols, const float* x, int64_t ldx, float* y, int64_t ldy,
+                                      float* nrm, void* stream) {
+  GMR_ARG(x && y && n > 0 && cols > 0 && cols % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0, "bad args");
+  hipLaunchKernelGGL(normalize_rows_kernel, ROWS16(n), 0, (hipStream_t)stream, n, cols, x, ldx, y, ldy, nrm);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_normalize_rows_bwd_f32(int64_t n, int32_t cols, const float* y, int64_t ldy, const float* nrm,
+                                          const float* dy, int64_t lddy, float* dx, int64_t lddx, float slope,
+                                          int32_t accumulate, void* stream) {
+  GMR_ARG(y && nrm && dy && dx && n > 0 && cols % 4 == 0, "bad args");
+  hipLaunchKernelGGL(normalize_bwd_kernel, ROWS16(n), 0, (hipStream_t)stream, n, cols, y, ldy, nrm, dy, lddy, dx, lddx,
+                     slope, accumulate);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_bpr_fwd_bwd(int32_t B, int64_t U, const float* Emb, const int32_t* users, const int32_t* pos,
+                               const int32_t* neg, float* loss, float* contrib, void* stream) {
+  GMR_ARG(Emb && users && pos && neg && loss && contrib && B > 0, "bad args");
+  hipLaunchKernelGGL(bpr_kernel, ROWS16((int64_t)B), 0, (hipStream_t)stream, B, U, Emb, users, pos, neg, loss, contrib);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_row_softmax_f32(int64_t rows, int64_t cols, float* L, int64_t ld, float coef, float* lse,
+                                   void* stream) {
+  GMR_ARG(L && lse && rows > 0 && cols > 0, "bad args");
+  hipLaunchKernelGGL(row_softmax_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, rows, cols, L, ld, coef,
+                     lse);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_contrast_rows(int32_t B, const float* CLN, const int32_t* nodes, int64_t node_off, const float* lse,
+                                 float inv_temp, float coef, float* loss, float* contrib, int64_t ld_contrib,
+                                 void* stream) {
+  GMR_ARG(CLN && nodes && lse && loss && contrib && B > 0 && ld_contrib >= 128, "bad args");
+  hipLaunchKernelGGL(contrast_rows_kernel, ROWS16((int64_t)B), 0, (hipStream_t)stream, B, CLN, nodes, node_off, lse,
+                     inv_temp, coef, loss, contrib, ld_contrib);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_gather_rows_f32(int32_t B, int32_t cols, const float* src, int64_t lds, const int32_t* idx,
+                                   int64_t off, float* out, int64_t ldo, void* stream) {
+  GMR_ARG(src && idx && out && B > 0 && cols % 4 == 0, "bad args");
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(gmr::grid_for((int64_t)B * cols / 4, 256)), dim3(256), 0,
+                     (hipStream_t)stream, B, cols, src, lds, idx, off, out, ldo);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_scatter_sorted_f32(int32_t n, int32_t cols, const uint64_t* plan, const float* contrib, int64_t ldc,
+                                      float* dst, int64_t ldd, void* stream) {
+  GMR_ARG(plan && contrib && dst && n > 0 && cols % 4 == 0, "bad args");
+  hipLaunchKernelGGL(scatter_sorted_kernel, dim3(gmr::grid_for((int64_t)n * cols / 4, 256)), dim3(256), 0,
+                     (hipStream_t)stream, n, cols, (const unsigned long long*)plan, contrib, ldc, dst, ldd);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dmm_final_bwd(int64_t n, const float* dEmb, const float* T1, const float* M, const float* nrmM,
+                                 float ris, const float* E, const float* mw, float* dE, float* partials,
+                                 void* stream) {
+  GMR_ARG(dEmb && T1 && M && nrmM && E && mw && dE && partials && n > 0, "bad args");
+  hipLaunchKernelGGL(final_bwd_kernel, ROWS16(n), 0, (hipStream_t)stream, n, dEmb, T1, M, nrmM, ris, E, mw, dE,
+                     partials);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int64_t gmr_dmm_final_bwd_partials(int64_t n) { return 2 * (int64_t)gmr::grid_for(n * 16, 256); }
+
+extern "C" int gmr_dmm_mw_grad(int64_t nparts, const float* partials, const float* mw, float* dmw, int32_t accumulate,
+                               void* stream) {
+  GMR_ARG(partials && mw && dmw, "bad args");
+  hipLaunchKernelGGL(mw_grad_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, (int)nparts, partials, mw, dmw,
+                     accumulate);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dmm_dg(int64_t n, int64_t U, const float* dE, const float* T2, float* dG, void* stream) {
+  GMR_ARG(dE && T2 && dG && n > 0, "bad args");
+  hipLaunchKernelGGL(dg_kernel, dim3(gmr::grid_for(n * 32, 256)), dim3(256), 0, (hipStream_t)stream, n, U, dE, T2, dG);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dmm_cl_bwd(int64_t n, const float* dK, const float* T, const float* dE, float lam, float* Ri,
+                              float* Rt, void* stream) {
+  GMR_ARG(dK && T && dE && Ri && Rt && n > 0, "bad args");
+  hipLaunchKernelGGL(cl_bwd_kernel, ROWS16(n), 0, (hipStream_t)stream, n, dK, T, dE, lam, Ri, Rt);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dmm_assemble(int64_t n, int64_t U, const float* T2, const float* T3, const float* Ri,
+                                const float* Rt, const float* E0, float reg2, float* dE0, float* dNF, void* stream) {
+  GMR_ARG(T2 && T3 && Ri && Rt && E0 && dE0 && dNF && n > 0, "bad args");
+  hipLaunchKernelGGL(assemble_kernel, ROWS16(n), 0, (hipStream_t)stream, n, U, T2, T3, Ri, Rt, E0, reg2, dE0, dNF);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_sum_f32(int64_t n, const float* x, float scale, float* out, int32_t accumulate, void* stream) {
+  GMR_ARG(x && out && n >= 0, "bad args");
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n, x, scale, out, accumulate);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_sqnorm_f32(int64_t n, const float* x, float scale, float* out, int32_t accumulate, void* stream) {
+  GMR_ARG(x && out && n >= 0, "bad args");
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, n, x, scale, out, accumulate);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_sort_batch_keys(int64_t n_batches, const int32_t* keys, const int64_t* offsets,
+                                   const int32_t* key_add, int32_t n_keysets, int64_t key_stride, uint64_t* out,
+                                   int64_t out_stride, int32_t pow2, void* stream) {
+  GMR_ARG(keys && offsets && key_add && out && n_batches > 0, "bad args");
+  GMR_ARG(pow2 >= 2 && pow2 <= 8192 && (pow2 & (pow2 - 1)) == 0, "pow2 must be a power of two <= 8192");
+  hipLaunchKernelGGL(sort_keys_kernel, dim3((unsigned)n_batches), dim3(1024), 0, (hipStream_t)stream, keys, offsets,
+                     key_add, n_keysets, key_stride, (unsigned long long*)out, out_stride, pow2);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}

@@ -1,0 +1,378 @@
+// K5 / K6 — Gaussian diffusion over per-user interaction vectors (gfx950).
+//
+// Reference: GaussianDiffusion.q_sample / training_losses / p_sample and Denoise.forward
+// (models/diffmm.py:340-484; models/diffrec.py:75-310).  The denoiser GEMMs themselves
+// run in gemm.hip; this file holds the row-wise pieces around them:
+//   * q_sample fused with the x0 densification (from the train CSR), N(0,1) noise and the
+//     p = 0.5 input dropout of Denoise (train mode), written straight into the GEMM input.
+//     Noise / keep mask / timesteps come from Philox (or caller buffers for parity tests).
+//   * per-timestep input bias EB[t] = emb_layer(temb(t)) @ W1[:, I:]^T + b1: the time
+//     embedding only takes T distinct values, so the concat([x, emb]) columns of the first
+//     Linear collapse into a T x H bias table indexed by t in the GEMM epilogue.
+//   * the loss rows (mse with SNR weight, gc loss) and the first dout term.
+#include "gmr_common.h"
+
+namespace {
+
+__device__ __forceinline__ bool in_row(const int* __restrict__ items, int beg, int end, int v) {
+  int lo = beg, hi = end;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (items[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < end && items[lo] == v;
+}
+
+struct Draw4 {
+  float eps[4];
+  float keep[4];
+};
+
+// noise and keep-mask of the 4 columns [c4*4, c4*4+4) of row b, step `step`
+__device__ __forceinline__ Draw4 draw4(uint64_t seed, uint64_t step, int64_t b, int64_t c4, float keep_prob) {
+  Draw4 d;
+  const uint64_t off = ((uint64_t)b << 24) ^ (uint64_t)c4;
+  uint4 r = gmr::Philox::gen(seed, step * 2 + 0, off);
+  float2 n0 = gmr::box_muller(r.x, r.y), n1 = gmr::box_muller(r.z, r.w);
+  d.eps[0] = n0.x;
+  d.eps[1] = n0.y;
+  d.eps[2] = n1.x;
+  d.eps[3] = n1.y;
+  uint4 q = gmr::Philox::gen(seed, step * 2 + 1, off);
+  d.keep[0] = gmr::u32_to_unit(q.x) <= keep_prob ? 1.f : 0.f;
+  d.keep[1] = gmr::u32_to_unit(q.y) <= keep_prob ? 1.f : 0.f;
+  d.keep[2] = gmr::u32_to_unit(q.z) <= keep_prob ? 1.f : 0.f;
+  d.keep[3] = gmr::u32_to_unit(q.w) <= keep_prob ? 1.f : 0.f;
+  return d;
+}
+
+__global__ void sample_t_kernel(int B, int T, uint64_t seed, uint64_t step, int* __restrict__ t) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  uint4 r = gmr::Philox::gen(seed ^ 0xA5A5A5A5ull, step, (uint64_t)b);
+  t[b] = (int)(((uint64_t)r.x * (uint64_t)T) >> 32);
+}
+
+// dense part: x0 = 0 everywhere -> x_in = (s1[t] * eps) * keep/kp ; sparse part fixes the ones
+__global__ void qsample_dense_kernel(int B, int I, const int* __restrict__ t, const float* __restrict__ sa,
+                                     const float* __restrict__ s1, const float* __restrict__ noise, int64_t ld_noise,
+                                     const float* __restrict__ keep, int64_t ld_keep, float keep_prob, int dropout,
+                                     uint64_t seed, uint64_t step, float* __restrict__ x, int64_t ldx) {
+  const int64_t c4n = (I + 3) / 4;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)B * c4n) return;
+  const int64_t b = gid / c4n, c4 = gid % c4n;
+  const int tb = t[b];
+  const float s1v = s1[tb];
+  Draw4 d;
+  if (!noise || (dropout && !keep)) d = draw4(seed, step, b, c4, keep_prob);
+  const float kscale = 1.f / keep_prob;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t c = c4 * 4 + j;
+    if (c >= I) break;
+    const float e = noise ? noise[b * ld_noise + c] : d.eps[j];
+    float v = s1v * e;
+    if (dropout) v = v * ((keep ? keep[b * ld_keep + c] : d.keep[j]) * kscale);
+    x[b * ldx + c] = v;
+  }
+}
+
+__global__ void qsample_sparse_kernel(int B, const int* __restrict__ users, const int* __restrict__ uptr,
+                                      const int* __restrict__ uitems, const int* __restrict__ t,
+                                      const float* __restrict__ sa, const float* __restrict__ s1,
+                                      const float* __restrict__ noise, int64_t ld_noise, const float* __restrict__ keep,
+                                      int64_t ld_keep, float keep_prob, int dropout, uint64_t seed, uint64_t step,
+                                      float* __restrict__ x, int64_t ldx) {
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int u = users[b];
+  const int tb = t[b];
+  const float sav = sa[tb], s1v = s1[tb];
+  const float kscale = 1.f / keep_prob;
+  for (int e = uptr[u] + threadIdx.x; e < uptr[u + 1]; e += blockDim.x) {
+    const int64_t c = uitems[e];
+    const int64_t c4 = c >> 2;
+    Draw4 d;
+    if (!noise || (dropout && !keep)) d = draw4(seed, step, b, c4, keep_prob);
+    const float eps = noise ? noise[b * ld_noise + c] : d.eps[c & 3];
+    float v = sav * 1.0f + s1v * eps;
+    if (dropout) v = v * ((keep ? keep[b * ld_keep + c] : d.keep[c & 3]) * kscale);
+    x[b * ldx + c] = v;
+  }
+}
+
+// x0 rows: zero then ones at the user's train items
+__global__ void densify_zero_kernel(int B, int I, float* __restrict__ x, int64_t ldx) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)B * I) return;
+  x[(gid / I) * ldx + gid % I] = 0.f;
+}
+
+__global__ void densify_ones_kernel(int B, const int* __restrict__ users, const int* __restrict__ uptr,
+                                    const int* __restrict__ uitems, float* __restrict__ x, int64_t ldx) {
+  const int b = blockIdx.x;
+  const int u = users ? users[b] : b;
+  for (int e = uptr[u] + threadIdx.x; e < uptr[u + 1]; e += blockDim.x) x[(int64_t)b * ldx + uitems[e]] = 1.f;
+}
+
+// EB[t][h] = sum_j emb[t][j] * W1[h][off + j] + b1[h],  emb[t] = emb_W @ temb(t) + emb_b
+__global__ void time_bias_kernel(int T, int E, const float* __restrict__ embW, const float* __restrict__ embB,
+                                 const float* __restrict__ W1, int64_t ldw, int64_t off, const float* __restrict__ b1,
+                                 int H, float* __restrict__ EB, float* __restrict__ temb_out, float* __restrict__ emb_out) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)T * H) return;
+  const int t = (int)(gid / H), h = (int)(gid % H);
+  float te[64], em[64];
+  const int half = E / 2;
+  for (int j = 0; j < half; ++j) {
+    float fr = expf(-9.210340371976184f * (float)j / (float)half);  // ln(10000)
+    float a = (float)t * fr;
+    te[j] = cosf(a);
+    te[half + j] = sinf(a);
+  }
+  if (E & 1) te[E - 1] = 0.f;
+  for (int i = 0; i < E; ++i) {
+    float s = 0.f;
+    for (int j = 0; j < E; ++j) s = fmaf(embW[i * E + j], te[j], s);
+    em[i] = s + embB[i];
+  }
+  float acc = 0.f;
+  for (int j = 0; j < E; ++j) acc = fmaf(em[j], W1[(int64_t)h * ldw + off + j], acc);
+  EB[(int64_t)t * H + h] = acc + b1[h];
+  if (h == 0) {
+    for (int j = 0; j < E; ++j) {
+      if (temb_out) temb_out[t * E + j] = te[j];
+      if (emb_out) emb_out[t * E + j] = em[j];
+    }
+  }
+}
+
+// One block per row: d = out - x0 ; mse_b = mean(d^2);  out <- ca_b * d  (first dout term)
+// diff_b = w[t_b] * mse_b (double).  ca_b = w[t_b] * 2 / (I * B) * scale.
+__global__ void __launch_bounds__(256) loss_rows_kernel(int B, int I, const int* __restrict__ users,
+                                                        const int* __restrict__ uptr, const int* __restrict__ uitems,
+                                                        const int* __restrict__ t, const double* __restrict__ wtab,
+                                                        float* __restrict__ out, int64_t ld, float grad_scale,
+                                                        double* __restrict__ mse_out, double* __restrict__ diff_out,
+                                                        int write_grad) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
+  const int b = blockIdx.x;
+  const int u = users[b];
+  const int nw = (I + 31) / 32;
+  for (int i = threadIdx.x; i < nw; i += 256) bits[i] = 0u;
+  __syncthreads();
+  for (int e = uptr[u] + threadIdx.x; e < uptr[u + 1]; e += 256) {
+    const int c = uitems[e];
+    atomicOr(&bits[c >> 5], 1u << (c & 31));
+  }
+  __syncthreads();
+  const double w = wtab[t[b]];
+  const float ca = (float)(w * 2.0 / (double)I) * grad_scale;
+  float* row = out + (int64_t)b * ld;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < I; i += 256) {
+    const float x0 = (bits[i >> 5] >> (i & 31)) & 1u ? 1.f : 0.f;
+    const float d = row[i] - x0;
+    s = fmaf(d, d, s);
+    if (write_grad) row[i] = ca * d;
+  }
+  __shared__ float red[4];
+  s = gmr::wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double mse = (double)((red[0] + red[1]) + (red[2] + red[3])) / (double)I;
+    mse_out[b] = mse;
+    diff_out[b] = w * mse;
+  }
+}
+
+// gc term: Y = x0 @ iE (sum of the user's item rows), D = Z - Y;  gc_b = mean(D^2) ;
+// G = gscale * D  (B x 64, feeds dout += G @ feats^T).  One 64-lane wave per row.
+__global__ void gc_rows_kernel(int B, const int* __restrict__ users, const int* __restrict__ uptr,
+                               const int* __restrict__ uitems, const float* __restrict__ iE, int64_t ld_ie,
+                               const float* __restrict__ Z, int64_t ldz, float gscale, float* __restrict__ G,
+                               int64_t ldg, double* __restrict__ gc_out) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  const int u = users[b];
+  float y = 0.f;
+  for (int e = uptr[u]; e < uptr[u + 1]; ++e) y += iE[(int64_t)uitems[e] * ld_ie + lane];
+  const float d = Z[(int64_t)b * ldz + lane] - y;
+  const float s = gmr::wave_sum(d * d);
+  if (G) G[(int64_t)b * ldg + lane] = gscale * d;
+  if (lane == 0) gc_out[b] = (double)s / 64.0;
+}
+
+// deterministic column sums: out[c] (+)= sum_r x[r][c]; 64 columns per block, rows split over 4 waves
+__global__ void __launch_bounds__(256) colsum_kernel(int64_t rows, int64_t cols, const float* __restrict__ x, int64_t ld,
+                                                     const int* __restrict__ group, int n_groups,
+                                                     float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int64_t c = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;
+  const int g = blockIdx.y;
+  float s = 0.f;
+  if (c < cols)
+    for (int64_t r = w; r < rows; r += 4)
+      if (!group || group[r] == g) s += x[r * ld + c];
+  red[w][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    float v = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    float* o = out + (int64_t)g * cols + c;
+    *o = accumulate ? *o + v : v;
+  }
+}
+
+// time-embedding backward from S[t][h] = sum_{b: t_b = t} dpre[b][h]:
+//   dW1[h][off + j] (+)= sum_t S[t][h] emb[t][j] ; db1[h] (+)= sum_t S[t][h]
+//   demb[t][j] = sum_h S[t][h] W1[h][off + j] ; d emb_W[i][j] = sum_t demb[t][i] temb[t][j] ; d emb_b[i] = sum_t demb[t][i]
+__global__ void time_bwd_h_kernel(int T, int E, int H, const float* __restrict__ S, const float* __restrict__ emb,
+                                  float* __restrict__ dW1, int64_t ldw, int64_t off, float* __restrict__ db1,
+                                  int accumulate) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H) return;
+  float sb = 0.f;
+  for (int t = 0; t < T; ++t) sb += S[(int64_t)t * H + h];
+  db1[h] = accumulate ? db1[h] + sb : sb;
+  for (int j = 0; j < E; ++j) {
+    float a = 0.f;
+    for (int t = 0; t < T; ++t) a = fmaf(S[(int64_t)t * H + h], emb[t * E + j], a);
+    float* o = dW1 + (int64_t)h * ldw + off + j;
+    *o = accumulate ? *o + a : a;
+  }
+}
+
+__global__ void time_bwd_e_kernel(int T, int E, int H, const float* __restrict__ S, const float* __restrict__ W1,
+                                  int64_t ldw, int64_t off, const float* __restrict__ temb, float* __restrict__ dembW,
+                                  float* __restrict__ dembB, int accumulate) {
+  // single block of 64 threads: thread i handles output row i of emb_W
+  __shared__ float demb[64][64];  // [t][j], T <= 64 handled in chunks of 64 timesteps
+  const int i = threadIdx.x;
+  float accW[64];
+  for (int j = 0; j < E; ++j) accW[j] = 0.f;
+  float accB = 0.f;
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int tn = min(64, T - t0);
+    // demb[t][j] for the chunk: thread i computes column j = i for every t
+    if (i < E)
+      for (int tt = 0; tt < tn; ++tt) {
+        float a = 0.f;
+        for (int h = 0; h < H; ++h) a = fmaf(S[(int64_t)(t0 + tt) * H + h], W1[(int64_t)h * ldw + off + i], a);
+        demb[tt][i] = a;
+      }
+    __syncthreads();
+    if (i < E)
+      for (int tt = 0; tt < tn; ++tt) {
+        const float d = demb[tt][i];
+        accB += d;
+        for (int j = 0; j < E; ++j) accW[j] = fmaf(d, temb[(t0 + tt) * E + j], accW[j]);
+      }
+    __syncthreads();
+  }
+  if (i < E) {
+    for (int j = 0; j < E; ++j) dembW[i * E + j] = accumulate ? dembW[i * E + j] + accW[j] : accW[j];
+    dembB[i] = accumulate ? dembB[i] + accB : accB;
+  }
+}
+
+}  // namespace
+
+extern "C" int gmr_diff_sample_t(int32_t B, int32_t T, uint64_t seed, uint64_t step, int32_t* t, void* stream) {
+  GMR_ARG(t && B > 0 && T > 0, "bad args");
+  hipLaunchKernelGGL(sample_t_kernel, dim3(gmr::grid_for(B, 256)), dim3(256), 0, (hipStream_t)stream, B, T, seed, step, t);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_diff_qsample(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr,
+                                const int32_t* user_items, const int32_t* t, const float* sqrt_ac,
+                                const float* sqrt_1mac, const float* noise, int64_t ld_noise, const float* keep,
+                                int64_t ld_keep, float keep_prob, int32_t dropout, uint64_t seed, uint64_t step,
+                                float* x, int64_t ldx, void* stream) {
+  GMR_ARG(users && user_ptr && user_items && t && sqrt_ac && sqrt_1mac && x && B > 0 && I > 0, "bad args");
+  GMR_ARG(keep_prob > 0.f && keep_prob <= 1.f, "keep_prob must be in (0, 1]");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t c4n = (I + 3) / 4;
+  hipLaunchKernelGGL(qsample_dense_kernel, dim3(gmr::grid_for((int64_t)B * c4n, 256)), dim3(256), 0, st, B, I, t,
+                     sqrt_ac, sqrt_1mac, noise, ld_noise, keep, ld_keep, keep_prob, dropout, seed, step, x, ldx);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(qsample_sparse_kernel, dim3(B), dim3(64), 0, st, B, users, user_ptr, user_items, t, sqrt_ac,
+                     sqrt_1mac, noise, ld_noise, keep, ld_keep, keep_prob, dropout, seed, step, x, ldx);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_diff_densify(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr,
+                                const int32_t* user_items, float* x, int64_t ldx, void* stream) {
+  GMR_ARG(user_ptr && user_items && x && B > 0 && I > 0, "bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(densify_zero_kernel, dim3(gmr::grid_for((int64_t)B * I, 256)), dim3(256), 0, st, B, I, x, ldx);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(densify_ones_kernel, dim3(B), dim3(64), 0, st, B, users, user_ptr, user_items, x, ldx);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_diff_time_bias(int32_t T, int32_t E, const float* emb_W, const float* emb_b, const float* W1,
+                                  int64_t ld_w1, int64_t col_off, const float* b1, int32_t H, float* EB,
+                                  float* temb_out, float* emb_out, void* stream) {
+  GMR_ARG(emb_W && emb_b && W1 && b1 && EB && T > 0 && H > 0, "bad args");
+  GMR_ARG(E >= 1 && E <= 64, "time embedding size must be 1..64");
+  hipLaunchKernelGGL(time_bias_kernel, dim3(gmr::grid_for((int64_t)T * H, 128)), dim3(128), 0, (hipStream_t)stream, T, E,
+                     emb_W, emb_b, W1, ld_w1, col_off, b1, H, EB, temb_out, emb_out);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_diff_loss_rows(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr,
+                                  const int32_t* user_items, const int32_t* t, const double* wtab, float* out,
+                                  int64_t ld, float grad_scale, double* mse_out, double* diff_out, int32_t write_grad,
+                                  void* stream) {
+  GMR_ARG(users && user_ptr && user_items && t && wtab && out && mse_out && diff_out && B > 0 && I > 0, "bad args");
+  const size_t dyn = sizeof(uint32_t) * (size_t)((I + 31) / 32);
+  GMR_ARG(dyn <= 60000, "item count too large for the LDS bitmap");
+  hipLaunchKernelGGL(loss_rows_kernel, dim3(B), dim3(256), dyn, (hipStream_t)stream, B, I, users, user_ptr, user_items,
+                     t, wtab, out, ld, grad_scale, mse_out, diff_out, write_grad);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_diff_gc_rows(int32_t B, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
+                                const float* item_embeds, int64_t ld_ie, const float* Z, int64_t ldz, float gscale,
+                                float* G, int64_t ldg, double* gc_out, void* stream) {
+  GMR_ARG(users && user_ptr && user_items && item_embeds && Z && gc_out && B > 0, "bad args");
+  hipLaunchKernelGGL(gc_rows_kernel, dim3(gmr::grid_for(B, 4)), dim3(256), 0, (hipStream_t)stream, B, users, user_ptr,
+                     user_items, item_embeds, ld_ie, Z, ldz, gscale, G, ldg, gc_out);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_colsum_f32(int64_t rows, int64_t cols, const float* x, int64_t ld, const int32_t* group,
+                              int32_t n_groups, float* out, int32_t accumulate, void* stream) {
+  GMR_ARG(x && out && rows > 0 && cols > 0 && n_groups >= 1, "bad args");
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)n_groups);
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, x, ld, group, n_groups, out,
+                     accumulate);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_diff_time_bwd(int32_t T, int32_t E, int32_t H, const float* S, const float* temb, const float* emb,
+                                 const float* W1, int64_t ld_w1, int64_t col_off, float* dW1, float* db1,
+                                 float* d_emb_W, float* d_emb_b, int32_t accumulate, void* stream) {
+  GMR_ARG(S && temb && emb && W1 && dW1 && db1 && d_emb_W && d_emb_b && T > 0 && H > 0, "bad args");
+  GMR_ARG(E >= 1 && E <= 64, "time embedding size must be 1..64");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(time_bwd_h_kernel, dim3(gmr::grid_for(H, 256)), dim3(256), 0, st, T, E, H, S, emb, dW1, ld_w1,
+                     col_off, db1, accumulate);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(time_bwd_e_kernel, dim3(1), dim3(64), 0, st, T, E, H, S, W1, ld_w1, col_off, temb, d_emb_W, d_emb_b,
+                     accumulate);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}

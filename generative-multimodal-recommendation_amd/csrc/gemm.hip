@@ -1,0 +1,343 @@
+// K3/K4/K6/K9 — fp32 GEMM on the gfx950 f32-input matrix cores (v_mfma_f32_32x32x2_f32).
+//
+// C[M,N] = epilogue(alpha * op(A)[M,K] * op(B)[K,N], ...), all row-major.
+//   op(A): trans_a = 0 -> A stored M x K (lda >= K);  trans_a = 1 -> A stored K x M.
+//   op(B): trans_b = 0 -> B stored K x N (ldb >= N);  trans_b = 1 -> B stored N x K.
+// Replaces nn.Linear / torch.mm / matmul on the hot path: Denoise layers
+// (models/diffmm.py:352-358), modal projections (:117,124), gc loss GEMMs (:472-473),
+// full-catalog scoring (:277) and their backward products.
+//
+// Block: 256 threads = 4 waves in a 2x2 grid; tile BM x BN x 32; each wave owns
+// (BM/64) x (BN/64) 32x32 accumulators.  The k order inside a 32-deep tile is
+// permuted (MFMA step s, lane half h -> k = 16h + s) so a lane's A/B fragments for
+// consecutive steps are contiguous in a k-contiguous LDS row: 4 x ds_read_b128 per
+// tile per 16 MFMAs.  m/n-contiguous operands keep an [k][m] LDS image read with
+// conflict-free ds_read_b32.  Register-staged double buffer, one barrier per k-tile.
+// Split-K (grid.z) writes fp32 partial slabs that a second pass sums in slab order
+// (deterministic) and then applies the epilogue.
+#include "gmr_common.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int BK = 32;
+
+struct Epi {
+  int kind;
+  float alpha, beta, slope;
+  const float* bias;
+  const int* bias_row;
+  int64_t ld_bias;
+  const float* aux;
+  int64_t ld_aux;
+  const float* rv1;
+  const float* rv2;
+};
+
+__device__ __forceinline__ float epi_apply(const Epi& e, float acc, int64_t m, int64_t n, float* cp) {
+  float v = e.alpha * acc;
+  float b = 0.f;
+  if (e.bias) b = e.bias[(e.bias_row ? (int64_t)e.bias_row[m] : 0) * e.ld_bias + n];
+  switch (e.kind) {
+    case GMR_EPI_NONE:
+      return e.beta != 0.f ? fmaf(e.beta, *cp, v) : v;
+    case GMR_EPI_BIAS:
+      v += b;
+      return e.beta != 0.f ? fmaf(e.beta, *cp, v) : v;
+    case GMR_EPI_BIAS_TANH:
+      return tanhf(v + b);
+    case GMR_EPI_LEAKY:
+      v += b;
+      return v > 0.f ? v : v * e.slope;
+    case GMR_EPI_POSTERIOR:  // scalar coefficients (slope, beta) when the row vectors are absent
+      return (e.rv1 ? e.rv1[m] : e.slope) * (v + b) + (e.rv2 ? e.rv2[m] : e.beta) * e.aux[m * e.ld_aux + n];
+    case GMR_EPI_DTANH: {
+      float h = e.aux[m * e.ld_aux + n];
+      return v * (1.f - h * h);
+    }
+    case GMR_EPI_ROWSCALE_AUX:
+      return v + b + e.rv1[m] * e.aux[m * e.ld_aux + n];
+    default:
+      return v;
+  }
+}
+
+// Loads a BK-deep tile slice of an operand into registers (float4 granules).
+// KC: operand stored [rows][k] (k contiguous), tile = R rows x BK.
+// MC: operand stored [k][rows] (rows contiguous), tile = BK x R.
+template <int R, bool KC, bool VEC>
+struct Stage {
+  static constexpr int N4 = R * BK / 4 / 256;  // float4 per thread
+  float4 r[N4];
+
+  __device__ __forceinline__ void load(const float* __restrict__ p, int64_t ld, int64_t r0, int64_t nrows,
+                                       int64_t k0, int64_t K) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < N4; ++i) {
+      const int idx = t + 256 * i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (KC) {
+        const int rr = idx / (BK / 4), k4 = (idx % (BK / 4)) * 4;
+        const int64_t row = r0 + rr, k = k0 + k4;
+        if (row < nrows) {
+          const float* q = p + row * ld + k;
+          if (VEC && k + 3 < K) {
+            v = *reinterpret_cast<const float4*>(q);
+          } else {
+            if (k < K) v.x = q[0];
+            if (k + 1 < K) v.y = q[1];
+            if (k + 2 < K) v.z = q[2];
+            if (k + 3 < K) v.w = q[3];
+          }
+        }
+      } else {
+        const int kk = idx / (R / 4), m4 = (idx % (R / 4)) * 4;
+        const int64_t k = k0 + kk, row = r0 + m4;
+        if (k < K) {
+          const float* q = p + k * ld + row;
+          if (VEC && row + 3 < nrows) {
+            v = *reinterpret_cast<const float4*>(q);
+          } else {
+            if (row < nrows) v.x = q[0];
+            if (row + 1 < nrows) v.y = q[1];
+            if (row + 2 < nrows) v.z = q[2];
+            if (row + 3 < nrows) v.w = q[3];
+          }
+        }
+      }
+      r[i] = v;
+    }
+  }
+
+  // LDS images: KC -> [R][BK + 4] ; MC -> [BK][R + 4]
+  static constexpr int LD = KC ? BK + 4 : R + 4;
+  static constexpr int WORDS = KC ? R * (BK + 4) : BK * (R + 4);
+
+  __device__ __forceinline__ void store(float* s) const {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < N4; ++i) {
+      const int idx = t + 256 * i;
+      if (KC) {
+        const int rr = idx / (BK / 4), k4 = (idx % (BK / 4)) * 4;
+        *reinterpret_cast<float4*>(s + rr * LD + k4) = r[i];
+      } else {
+        const int kk = idx / (R / 4), m4 = (idx % (R / 4)) * 4;
+        *reinterpret_cast<float4*>(s + kk * LD + m4) = r[i];
+      }
+    }
+  }
+};
+
+// fragment for rows [row] and k = 16h + 4q .. +3 (four consecutive MFMA steps)
+template <bool KC, int LD>
+__device__ __forceinline__ float4 frag4(const float* s, int row, int h, int q) {
+  if (KC) {
+    return *reinterpret_cast<const float4*>(s + row * LD + h * 16 + q * 4);
+  } else {
+    const int k = h * 16 + q * 4;
+    return make_float4(s[(k + 0) * LD + row], s[(k + 1) * LD + row], s[(k + 2) * LD + row], s[(k + 3) * LD + row]);
+  }
+}
+
+template <int BM, int BN, bool AKC, bool BKC, bool VEC>
+__global__ void __launch_bounds__(256) gemm_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
+                                                   int64_t lda, const float* __restrict__ B, int64_t ldb,
+                                                   float* __restrict__ C, int64_t ldc, Epi epi, int tiles_n,
+                                                   int64_t k_per_split, float* __restrict__ ws) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  using SA = Stage<BM, AKC, VEC>;
+  using SB = Stage<BN, BKC, VEC>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (SA::WORDS + SB::WORDS)];
+  constexpr int STAGE_WORDS = SA::WORDS + SB::WORDS;
+
+  // XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous tile range.
+  const int nwg = gridDim.x;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  const int64_t m0 = (int64_t)(tile / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(tile % tiles_n) * BN;
+  const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
+  const int64_t kend = min(K, kbeg + k_per_split);
+
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int h = lane >> 5, l32 = lane & 31;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  SA ra;
+  SB rb;
+  int cur = 0;
+  if (kbeg < kend) {
+    ra.load(A, lda, m0, M, kbeg, kend);
+    rb.load(B, ldb, n0, N, kbeg, kend);
+    ra.store(smem);
+    rb.store(smem + SA::WORDS);
+  }
+  __syncthreads();
+  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+    const bool more = k0 + BK < kend;
+    if (more) {
+      ra.load(A, lda, m0, M, k0 + BK, kend);
+      rb.load(B, ldb, n0, N, k0 + BK, kend);
+    }
+    const float* a_s = smem + cur * STAGE_WORDS;
+    const float* b_s = a_s + SA::WORDS;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      float4 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = frag4<AKC, SA::LD>(a_s, wm * (BM / 2) + i * 32 + l32, h, qq);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = frag4<BKC, SB::LD>(b_s, wn * (BN / 2) + j * 32 + l32, h, qq);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].x, fb[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].y, fb[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].z, fb[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+    if (more) {
+      ra.store(smem + (cur ^ 1) * STAGE_WORDS);
+      rb.store(smem + (cur ^ 1) * STAGE_WORDS + SA::WORDS);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // epilogue: acc element e of lane -> row (e&3) + 8(e>>2) + 4h, col l32
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t n = n0 + wn * (BN / 2) + j * 32 + l32;
+      if (n >= N) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t m = m0 + wm * (BM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (m >= M) continue;
+        if (ws) {
+          ws[((int64_t)blockIdx.z * M + m) * N + n] = acc[i][j][e];
+        } else {
+          float* cp = C + m * ldc + n;
+          *cp = epi_apply(epi, acc[i][j][e], m, n, cp);
+        }
+      }
+    }
+}
+
+__global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const float* __restrict__ ws,
+                                     float* __restrict__ C, int64_t ldc, Epi epi) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * N) return;
+  const int64_t m = idx / N, n = idx % N;
+  float s = 0.f;
+  for (int z = 0; z < splits; ++z) s += ws[(int64_t)z * M * N + idx];
+  float* cp = C + m * ldc + n;
+  *cp = epi_apply(epi, s, m, n, cp);
+}
+
+template <int BM, int BN, bool AKC, bool BKC>
+void launch_t(bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+              const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n, int64_t kps,
+              float* ws) {
+  if (vec)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AKC, BKC, true>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc,
+                       epi, tiles_n, kps, ws);
+  else
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AKC, BKC, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc,
+                       epi, tiles_n, kps, ws);
+}
+
+template <int BM, int BN>
+void launch_tile(int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A,
+                 int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n,
+                 int64_t kps, float* ws) {
+  // AKC = A is k-contiguous (not transposed); BKC = B is k-contiguous (transposed)
+  if (!ta && tb) launch_t<BM, BN, true, true>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+  else if (!ta && !tb) launch_t<BM, BN, true, false>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+  else if (ta && !tb) launch_t<BM, BN, false, false>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+  else launch_t<BM, BN, false, true>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+}
+
+}  // namespace
+
+extern "C" int64_t gmr_gemm_workspace_floats(int64_t M, int64_t N, int64_t K) {
+  // upper bound used by gmr_gemm_f32's split-K path
+  (void)K;
+  return 16 * M * N;
+}
+
+extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, float alpha,
+                            const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
+                            int64_t ldc, int32_t epilogue, const float* bias, const int32_t* bias_row, int64_t ld_bias,
+                            const float* aux, int64_t ld_aux, const float* rowvec1, const float* rowvec2, float slope,
+                            int32_t tile, int32_t split_k, float* workspace, int64_t workspace_floats, void* stream) {
+  GMR_ARG(A && B && C, "null operand");
+  GMR_ARG(M > 0 && N > 0 && K > 0, "empty GEMM");
+  GMR_ARG(lda >= (trans_a ? M : K) && ldb >= (trans_b ? K : N) && ldc >= N, "leading dimension too small");
+  GMR_ARG(epilogue >= GMR_EPI_NONE && epilogue <= GMR_EPI_ROWSCALE_AUX, "bad epilogue");
+  GMR_ARG(!(epilogue == GMR_EPI_POSTERIOR || epilogue == GMR_EPI_DTANH || epilogue == GMR_EPI_ROWSCALE_AUX) || aux,
+          "epilogue needs aux");
+  GMR_ARG(epilogue != GMR_EPI_ROWSCALE_AUX || rowvec1, "epilogue needs rowvec1");
+  GMR_ARG(tile == 0 || tile == 64 || tile == 128, "tile must be 0 (auto), 64 or 128");
+  Epi e;
+  e.kind = epilogue;
+  e.alpha = alpha;
+  e.beta = beta;
+  e.slope = slope;
+  e.bias = bias;
+  e.bias_row = bias_row;
+  e.ld_bias = ld_bias;
+  e.aux = aux;
+  e.ld_aux = ld_aux;
+  e.rv1 = rowvec1;
+  e.rv2 = rowvec2;
+  const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
+  if (tile == 0) {
+    int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128);
+    tile = (t128 >= 512) ? 128 : 64;
+  }
+  const int64_t tm = (M + tile - 1) / tile, tn = (N + tile - 1) / tile;
+  GMR_ARG(tm * tn < (1ll << 31), "too many tiles");
+  int splits = split_k;
+  if (splits <= 0) {  // auto: aim for >= 512 workgroups on 256 CUs
+    splits = 1;
+    while (tm * tn * splits < 512 && K / (splits * 2) >= 256 && splits < 16) splits *= 2;
+  }
+  int64_t kps = (K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = (int)((K + kps - 1) / kps);
+  float* ws = nullptr;
+  if (splits > 1) {
+    GMR_ARG(workspace && workspace_floats >= (int64_t)splits * M * N, "split-K needs workspace of splits*M*N floats");
+    ws = workspace;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)(tm * tn), 1, (unsigned)splits);
+  if (tile == 128)
+    launch_tile<128, 128>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+  else
+    launch_tile<64, 64>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+  GMR_LAUNCHED();
+  if (ws) {
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gmr::grid_for(M * N, 256)), dim3(256), 0, st, M, N, splits, ws, C,
+                       ldc, e);
+    GMR_LAUNCHED();
+  }
+  return GMR_OK;
+}

@@ -1,0 +1,187 @@
+// K11 — device construction of the symmetric-normalised bipartite adjacency in CSR.
+//
+//   rows 0..U-1      user u : [u (self loop, optional)] + [U + item for its items, ascending]
+//   rows U..U+I-1    item i : [users that hold i, ascending] + [U + i (self loop, optional)]
+//   val(r, c) = float( (deg_r + eps)^-1/2 * (deg_c + eps)^-1/2 )   computed in fp64
+//
+// Serves both reference builders:
+//   DiffMM.get_norm_adj_mat   models/diffmm.py:88-107   (no self loops, eps = 1e-7)
+//   DiffMMTrainer.buildUIMatrix + normalizeAdj   common/trainer.py:464-485  (self loops, eps = 0)
+// Columns are sorted inside each row, so the CSR equals the reference's coalesced COO.
+// Item rows are filled in user order by a single workgroup (rounds of 1024 entries with
+// an in-round stable rank), so the build is deterministic without a device sort.
+#include "gmr_common.h"
+
+namespace {
+
+__global__ void count_items_kernel(int64_t nnz, const int* __restrict__ items, int* __restrict__ cnt) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < nnz) atomicAdd(&cnt[items[e]], 1);
+}
+
+// rowptr for all N+1 rows (single block, chunked serial + LDS scan over 1024 chunk sums)
+__global__ void __launch_bounds__(1024) rowptr_kernel(int U, int I, const int* __restrict__ uptr,
+                                                      const int* __restrict__ cnt, int sl, int* __restrict__ rowptr) {
+  __shared__ int s[1024];
+  const int t = threadIdx.x;
+  const int N = U + I;
+  const int chunk = (N + 1023) / 1024;
+  const int r0 = t * chunk, r1 = min(N, r0 + chunk);
+  int sum = 0;
+  for (int r = r0; r < r1; ++r) sum += (r < U ? uptr[r + 1] - uptr[r] : cnt[r - U]) + sl;
+  s[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    int v = t >= off ? s[t - off] : 0;
+    __syncthreads();
+    s[t] += v;
+    __syncthreads();
+  }
+  int o = s[t] - sum;
+  for (int r = r0; r < r1; ++r) {
+    rowptr[r] = o;
+    o += (r < U ? uptr[r + 1] - uptr[r] : cnt[r - U]) + sl;
+  }
+  if (t == 1023) rowptr[N] = s[1023];
+}
+
+__global__ void user_rows_kernel(int U, const int* __restrict__ uptr, const int* __restrict__ uitems, int sl,
+                                 const int* __restrict__ rowptr, int* __restrict__ col) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  int o = rowptr[u];
+  if (sl) col[o++] = u;
+  for (int e = uptr[u]; e < uptr[u + 1]; ++e) col[o++] = U + uitems[e];
+}
+
+__device__ __forceinline__ int user_of(const int* __restrict__ uptr, int U, int e) {
+  int lo = 0, hi = U;  // largest u with uptr[u] <= e
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (uptr[mid] <= e) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(1024) item_rows_kernel(int U, int nnz, const int* __restrict__ uptr,
+                                                         const int* __restrict__ uitems, const int* __restrict__ rowptr,
+                                                         int* __restrict__ col, int sl, int I) {
+  __shared__ int key[1024];
+  extern __shared__ __attribute__((aligned(16))) int running[];  // I ints
+  const int t = threadIdx.x;
+  for (int i = t; i < I; i += 1024) running[i] = 0;
+  __syncthreads();
+  for (int base = 0; base < nnz; base += 1024) {
+    const int e = base + t;
+    const int it = e < nnz ? uitems[e] : -1 - t;
+    key[t] = it;
+    __syncthreads();
+    int rank = 0;
+    bool last = true;
+    for (int j = 0; j < 1024; ++j) {
+      const int kj = key[j];
+      rank += (j < t) & (kj == it);
+      last &= !((j > t) & (kj == it));
+    }
+    if (e < nnz) {
+      const int u = user_of(uptr, U, e);
+      col[rowptr[U + it] + running[it] + rank] = u;
+    }
+    __syncthreads();
+    if (e < nnz && last) running[it] += rank + 1;
+    __syncthreads();
+  }
+  if (sl)
+    for (int i = t; i < I; i += 1024) col[rowptr[U + i + 1] - 1] = U + i;
+}
+
+// one wave per row: values in fp64, rounded once to fp32
+__global__ void values_kernel(int N, const int* __restrict__ rowptr, const int* __restrict__ col, double eps,
+                              float* __restrict__ val) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= N) return;
+  const int lane = threadIdx.x & 63;
+  const int beg = rowptr[r], end = rowptr[r + 1];
+  const double dr = pow((double)(end - beg) + eps, -0.5);
+  for (int e = beg + lane; e < end; e += 64) {
+    const int c = col[e];
+    const double dc = pow((double)(rowptr[c + 1] - rowptr[c]) + eps, -0.5);
+    val[e] = (float)(dr * dc);
+  }
+}
+
+// sort the k items of each user (insertion sort, k <= 64) and write uptr = u*k
+__global__ void topk_to_user_csr_kernel(int U, int k, const int* __restrict__ topk, int64_t ld, int* __restrict__ uptr,
+                                        int* __restrict__ uitems) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u > U) return;
+  uptr[u] = u * k;
+  if (u == U) return;
+  int v[64];
+  for (int j = 0; j < k; ++j) {
+    int x = topk[(int64_t)u * ld + j];
+    int p = j;
+    while (p > 0 && v[p - 1] > x) {
+      v[p] = v[p - 1];
+      --p;
+    }
+    v[p] = x;
+  }
+  for (int j = 0; j < k; ++j) uitems[u * k + j] = v[j];
+}
+
+}  // namespace
+
+extern "C" int64_t gmr_bipartite_nnz(int64_t n_users, int64_t n_items, int64_t n_user_items, int32_t self_loops) {
+  return 2 * n_user_items + (self_loops ? n_users + n_items : 0);
+}
+
+extern "C" int64_t gmr_bipartite_workspace_ints(int64_t n_users, int64_t n_items) { return 2 * n_items; }
+
+extern "C" int gmr_bipartite_symnorm_build(int64_t n_users, int64_t n_items, const int32_t* user_ptr,
+                                           const int32_t* user_items, int64_t n_user_items, int32_t self_loops,
+                                           double deg_eps, int32_t* workspace, int32_t* rowptr, int32_t* col,
+                                           float* val, void* stream) {
+  GMR_ARG(user_ptr && user_items && workspace && rowptr && col && val, "null pointer");
+  GMR_ARG(n_users > 0 && n_items > 0 && n_users + n_items < (1ll << 30), "bad size");
+  GMR_ARG(2 * n_user_items + n_users + n_items < (1ll << 31), "too many entries");
+  hipStream_t st = (hipStream_t)stream;
+  const int U = (int)n_users, I = (int)n_items, N = U + I;
+  const int sl = self_loops ? 1 : 0;
+  GMR_ARG(n_items <= 36000, "n_items above the LDS budget of the item-row builder");
+  int* cnt = workspace;
+  hipError_t e = hipMemsetAsync(workspace, 0, sizeof(int) * 2 * (size_t)I, st);
+  if (e != hipSuccess) return gmr::hip_status(__func__, e);
+  if (n_user_items > 0) {
+    hipLaunchKernelGGL(count_items_kernel, dim3(gmr::grid_for(n_user_items, 256)), dim3(256), 0, st, n_user_items,
+                       user_items, cnt);
+    GMR_LAUNCHED();
+  }
+  hipLaunchKernelGGL(rowptr_kernel, dim3(1), dim3(1024), 0, st, U, I, user_ptr, cnt, sl, rowptr);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(user_rows_kernel, dim3(gmr::grid_for(U, 256)), dim3(256), 0, st, U, user_ptr, user_items, sl, rowptr,
+                     col);
+  GMR_LAUNCHED();
+  const size_t dyn = sizeof(int) * (size_t)I;
+  if (dyn > 65536) {
+    e = hipFuncSetAttribute((const void*)item_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    if (e != hipSuccess) return gmr::hip_status(__func__, e);
+  }
+  hipLaunchKernelGGL(item_rows_kernel, dim3(1), dim3(1024), dyn, st, U, (int)n_user_items, user_ptr,
+                     user_items, rowptr, col, sl, I);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(values_kernel, dim3(gmr::grid_for(N, 4)), dim3(256), 0, st, N, rowptr, col, deg_eps, val);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_topk_to_user_csr(int64_t n_users, int32_t k, const int32_t* topk, int64_t ld, int32_t* user_ptr,
+                                    int32_t* user_items, void* stream) {
+  GMR_ARG(topk && user_ptr && user_items && n_users > 0, "bad args");
+  GMR_ARG(k >= 1 && k <= 64, "k must be 1..64");
+  hipLaunchKernelGGL(topk_to_user_csr_kernel, dim3(gmr::grid_for(n_users + 1, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (int)n_users, k, topk, ld, user_ptr, user_items);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}

@@ -1,0 +1,278 @@
+// K1 — CSR SpMM for the LightGCN-style graph convolution (gfx950).
+//
+// Replaces torch.spmm / torch.sparse.mm on the normalised user-item adjacency
+// (reference models/diffmm.py:136-191, 285).  Y = alpha * A * X + beta * Y with
+//   * X given as up to 4 column blocks of 64 floats, each block a "split source":
+//     source row s < split reads lo[b] + s*ld_lo[b], else hi[b] + (s-split)*ld_hi[b]
+//     (this removes the torch.concat([uEmbeds, feats]) copies of the reference);
+//   * nnz-balanced work: a plan cuts every row into segments of <= seg_nnz entries.
+//     One wave64 owns one segment; a 64-float row block is 16 lanes x float4, so a
+//     wave gathers 64/(16*nb) neighbour rows per instruction.  Single-segment rows
+//     are written directly; hub rows (popular items) write per-segment partials that
+//     a second pass adds in segment order, so results are deterministic.
+#include "gmr_common.h"
+
+namespace {
+
+constexpr int kPlanHdr = 4;  // n_seg, n_fix, n_partial, pad
+
+struct PlanView {
+  int* hdr;
+  int* seg_row;
+  int* seg_beg;
+  int* seg_end;
+  int* seg_slot;
+  int* fix_row;
+  int* fix_first;
+  int* fix_cnt;
+};
+
+__host__ __device__ inline int64_t plan_max_seg(int64_t n_rows, int64_t nnz, int seg_nnz) {
+  return n_rows + (nnz + seg_nnz - 1) / seg_nnz + 1;
+}
+__host__ __device__ inline int64_t plan_max_fix(int64_t n_rows, int64_t nnz, int seg_nnz) {
+  int64_t f = (nnz + seg_nnz - 1) / seg_nnz + 1;
+  return f < n_rows ? f : n_rows;
+}
+
+__host__ __device__ inline PlanView plan_view(int32_t* p, int64_t n_rows, int64_t nnz, int seg_nnz) {
+  int64_t ms = plan_max_seg(n_rows, nnz, seg_nnz), mf = plan_max_fix(n_rows, nnz, seg_nnz);
+  PlanView v;
+  v.hdr = p;
+  v.seg_row = p + kPlanHdr;
+  v.seg_beg = v.seg_row + ms;
+  v.seg_end = v.seg_beg + ms;
+  v.seg_slot = v.seg_end + ms;
+  v.fix_row = v.seg_slot + ms;
+  v.fix_first = v.fix_row + mf;
+  v.fix_cnt = v.fix_first + mf;
+  return v;
+}
+
+// Single-workgroup plan builder: three exclusive scans over rows (segments, fix rows,
+// partial slots) done as chunked serial sums + an LDS scan of the 1024 chunk totals.
+__global__ void __launch_bounds__(1024) plan_build_kernel(const int* __restrict__ rowptr, int n_rows, int seg_nnz,
+                                                          PlanView pv) {
+  __shared__ int s_seg[1024], s_fix[1024], s_part[1024];
+  const int t = threadIdx.x;
+  const int chunk = (n_rows + 1023) / 1024;
+  const int r0 = t * chunk, r1 = min(n_rows, r0 + chunk);
+  int ns = 0, nf = 0, np_ = 0;
+  for (int r = r0; r < r1; ++r) {
+    int deg = rowptr[r + 1] - rowptr[r];
+    int k = deg <= seg_nnz ? 1 : (deg + seg_nnz - 1) / seg_nnz;
+    ns += k;
+    if (k > 1) {
+      nf += 1;
+      np_ += k;
+    }
+  }
+  s_seg[t] = ns;
+  s_fix[t] = nf;
+  s_part[t] = np_;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    int a = t >= off ? s_seg[t - off] : 0;
+    int b = t >= off ? s_fix[t - off] : 0;
+    int c = t >= off ? s_part[t - off] : 0;
+    __syncthreads();
+    s_seg[t] += a;
+    s_fix[t] += b;
+    s_part[t] += c;
+    __syncthreads();
+  }
+  int so = s_seg[t] - ns, fo = s_fix[t] - nf, po = s_part[t] - np_;
+  for (int r = r0; r < r1; ++r) {
+    int beg = rowptr[r], end = rowptr[r + 1];
+    int deg = end - beg;
+    int k = deg <= seg_nnz ? 1 : (deg + seg_nnz - 1) / seg_nnz;
+    if (k == 1) {
+      pv.seg_row[so] = r;
+      pv.seg_beg[so] = beg;
+      pv.seg_end[so] = end;
+      pv.seg_slot[so] = -1;
+      ++so;
+    } else {
+      pv.fix_row[fo] = r;
+      pv.fix_first[fo] = po;
+      pv.fix_cnt[fo] = k;
+      ++fo;
+      for (int j = 0; j < k; ++j) {
+        pv.seg_row[so] = r;
+        pv.seg_beg[so] = beg + j * seg_nnz;
+        pv.seg_end[so] = min(end, beg + (j + 1) * seg_nnz);
+        pv.seg_slot[so] = po++;
+        ++so;
+      }
+    }
+  }
+  if (t == 1023) {
+    pv.hdr[0] = s_seg[1023];
+    pv.hdr[1] = s_fix[1023];
+    pv.hdr[2] = s_part[1023];
+    pv.hdr[3] = 0;
+  }
+}
+
+struct Src {
+  const float* lo[4];
+  const float* hi[4];
+  int64_t ld_lo[4];
+  int64_t ld_hi[4];
+  int64_t split;
+};
+
+// NB = number of 64-column blocks (d = 64 * NB).  LPR = lanes per neighbour row.
+template <int NB>
+__global__ void __launch_bounds__(256) spmm_seg_kernel(const int* __restrict__ col, const float* __restrict__ val,
+                                                       PlanView pv, Src src, float alpha, float beta,
+                                                       float* __restrict__ y, int64_t ldy,
+                                                       float* __restrict__ partial) {
+  constexpr int LPR = 16 * NB;
+  constexpr int G = 64 / LPR;  // neighbour rows gathered per wave instruction
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n_seg = pv.hdr[0];
+  if (seg >= n_seg) return;
+  const int row = pv.seg_row[seg];
+  const int beg = pv.seg_beg[seg], end = pv.seg_end[seg];
+  const int slot = pv.seg_slot[seg];
+  const int g = lane / LPR;
+  const int sub = lane % LPR;
+  const int blk = sub >> 4;
+  const int c4 = (sub & 15) * 4;
+  const float* lo = src.lo[blk];
+  const float* hi = src.hi[blk];
+  const int64_t ldl = src.ld_lo[blk], ldh = src.ld_hi[blk];
+  const int64_t split = src.split;
+
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int base = beg; base < end; base += 64) {
+    const int e = base + lane;
+    int my_c = 0;
+    float my_v = 0.f;
+    if (e < end) {
+      my_c = col[e];
+      my_v = val[e];
+    }
+    const int cnt = min(64, end - base);
+    for (int j = 0; j < 64; j += G) {
+      if (j >= cnt) break;
+      const int k = j + g;
+      const int c = __shfl(my_c, k);
+      const float v = __shfl(my_v, k);
+      if (k < cnt) {
+        const float* p = c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh;
+        const float4 x = *reinterpret_cast<const float4*>(p + c4);
+        acc = gmr::f4_fma(v, x, acc);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = LPR; m < 64; m <<= 1) acc = gmr::f4_add(acc, gmr::shfl_xor_f4(acc, m));
+  if (g != 0) return;
+  const int cc = blk * 64 + c4;
+  if (slot < 0) {
+    float* yp = y + (int64_t)row * ldy + cc;
+    float4 o = gmr::f4_scale(alpha, acc);
+    if (beta != 0.f) {
+      float4 old = *reinterpret_cast<const float4*>(yp);
+      o = gmr::f4_fma(beta, old, o);
+    }
+    *reinterpret_cast<float4*>(yp) = o;
+  } else {
+    *reinterpret_cast<float4*>(partial + (int64_t)slot * (64 * NB) + cc) = acc;
+  }
+}
+
+template <int NB>
+__global__ void __launch_bounds__(256) spmm_fix_kernel(PlanView pv, float alpha, float beta, float* __restrict__ y,
+                                                       int64_t ldy, const float* __restrict__ partial) {
+  constexpr int D = 64 * NB;
+  constexpr int TPR = D / 4;  // threads per fix row
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t f = gid / TPR;
+  if (f >= pv.hdr[1]) return;
+  const int c = (int)(gid % TPR) * 4;
+  const int row = pv.fix_row[f], first = pv.fix_first[f], cnt = pv.fix_cnt[f];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j = 0; j < cnt; ++j) acc = gmr::f4_add(acc, *reinterpret_cast<const float4*>(partial + (int64_t)(first + j) * D + c));
+  float* yp = y + (int64_t)row * ldy + c;
+  float4 o = gmr::f4_scale(alpha, acc);
+  if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
+  *reinterpret_cast<float4*>(yp) = o;
+}
+
+}  // namespace
+
+extern "C" int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_nnz) {
+  if (seg_nnz <= 0) return -1;
+  return kPlanHdr + 4 * plan_max_seg(n_rows, nnz, seg_nnz) + 3 * plan_max_fix(n_rows, nnz, seg_nnz);
+}
+
+extern "C" int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t seg_nnz) {
+  if (seg_nnz <= 0) return -1;
+  return 2 * ((nnz + seg_nnz - 1) / seg_nnz) + 2;
+}
+
+extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t seg_nnz,
+                                   int32_t* plan, void* stream) {
+  GMR_ARG(rowptr && plan, "null pointer");
+  GMR_ARG(n_rows > 0 && n_rows < (1ll << 31) && nnz >= 0 && nnz < (1ll << 31), "bad size");
+  GMR_ARG(seg_nnz >= 64 && seg_nnz % 64 == 0, "seg_nnz must be a positive multiple of 64");
+  PlanView pv = plan_view(plan, n_rows, nnz, seg_nnz);
+  hipLaunchKernelGGL(plan_build_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, (int)n_rows, seg_nnz,
+                     pv);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
+                                int64_t nnz, const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,
+                                const float* const* x_lo, const int64_t* ld_lo, const float* const* x_hi,
+                                const int64_t* ld_hi, int64_t split, float alpha, float beta, float* y, int64_t ldy,
+                                void* stream) {
+  GMR_ARG(rowptr && col && val && plan && y && x_lo && ld_lo, "null pointer");
+  GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "n_blocks must be 1, 2 or 4");
+  GMR_ARG(n_rows > 0 && nnz >= 0 && ldy >= 64 * n_blocks && ldy % 4 == 0, "bad shape");
+  GMR_ARG(((uintptr_t)y & 15) == 0, "y must be 16-byte aligned");
+  Src s;
+  s.split = split;
+  for (int b = 0; b < 4; ++b) {
+    int bb = b < n_blocks ? b : 0;
+    s.lo[b] = x_lo[bb];
+    s.ld_lo[b] = ld_lo[bb];
+    s.hi[b] = (split < n_rows && x_hi) ? x_hi[bb] : x_lo[bb];
+    s.ld_hi[b] = (split < n_rows && ld_hi) ? ld_hi[bb] : ld_lo[bb];
+    GMR_ARG(s.lo[b] && s.hi[b], "null source block");
+    GMR_ARG(((uintptr_t)s.lo[b] & 15) == 0 && ((uintptr_t)s.hi[b] & 15) == 0, "sources must be 16-byte aligned");
+    GMR_ARG(s.ld_lo[b] % 4 == 0 && s.ld_hi[b] % 4 == 0, "source ld must be a multiple of 4");
+  }
+  PlanView pv = plan_view(const_cast<int32_t*>(plan), n_rows, nnz, seg_nnz);
+  const int64_t max_seg = plan_max_seg(n_rows, nnz, seg_nnz);
+  const int grid = gmr::grid_for(max_seg, 4);
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t max_fix = plan_max_fix(n_rows, nnz, seg_nnz);
+  switch (n_blocks) {
+    case 1:
+      hipLaunchKernelGGL(spmm_seg_kernel<1>, dim3(grid), dim3(256), 0, st, col, val, pv, s, alpha, beta, y, ldy, partial);
+      GMR_LAUNCHED();
+      hipLaunchKernelGGL(spmm_fix_kernel<1>, dim3(gmr::grid_for(max_fix * 16, 256)), dim3(256), 0, st, pv, alpha, beta,
+                         y, ldy, partial);
+      break;
+    case 2:
+      hipLaunchKernelGGL(spmm_seg_kernel<2>, dim3(grid), dim3(256), 0, st, col, val, pv, s, alpha, beta, y, ldy, partial);
+      GMR_LAUNCHED();
+      hipLaunchKernelGGL(spmm_fix_kernel<2>, dim3(gmr::grid_for(max_fix * 32, 256)), dim3(256), 0, st, pv, alpha, beta,
+                         y, ldy, partial);
+      break;
+    default:
+      hipLaunchKernelGGL(spmm_seg_kernel<4>, dim3(grid), dim3(256), 0, st, col, val, pv, s, alpha, beta, y, ldy, partial);
+      GMR_LAUNCHED();
+      hipLaunchKernelGGL(spmm_fix_kernel<4>, dim3(gmr::grid_for(max_fix * 64, 256)), dim3(256), 0, st, pv, alpha, beta,
+                         y, ldy, partial);
+      break;
+  }
+  GMR_LAUNCHED();
+  return GMR_OK;
+}

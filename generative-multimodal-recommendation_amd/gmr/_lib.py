@@ -1,0 +1,110 @@
+"""ctypes binding of libgmr_hip.so (the C-ABI declared in include/gmr.h).
+
+The HIP library is the ONLY compute path of this package: when it is missing or cannot be
+loaded, every op raises immediately — there is no CPU or eager-PyTorch fallback.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GMR_HIP_LIB", os.path.join(_HERE, "libgmr_hip.so"))
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+U64 = ctypes.c_uint64
+F32 = ctypes.c_float
+F64 = ctypes.c_double
+CP = ctypes.c_char_p
+
+# name: (restype, argtypes) — must match include/gmr.h
+SIGNATURES = {
+    "gmr_last_error_string": (CP, []),
+    "gmr_version": (I32, []),
+    "gmr_device_name": (I32, [P, I32]),
+    "gmr_zero": (I32, [P, I64, P]),
+    "gmr_spmm_plan_words": (I64, [I64, I64, I32]),
+    "gmr_spmm_partial_rows": (I64, [I64, I64, I32]),
+    "gmr_spmm_plan_build": (I32, [P, I64, I64, I32, P, P]),
+    "gmr_spmm_csr_f32": (I32, [P, P, P, I64, I64, P, I32, P, I32, P, P, P, P, I64, F32, F32, P, I64, P]),
+    "gmr_bipartite_nnz": (I64, [I64, I64, I64, I32]),
+    "gmr_bipartite_workspace_ints": (I64, [I64, I64]),
+    "gmr_bipartite_symnorm_build": (I32, [I64, I64, P, P, I64, I32, F64, P, P, P, P, P]),
+    "gmr_topk_to_user_csr": (I32, [I64, I32, P, I64, P, P, P]),
+    "gmr_gemm_workspace_floats": (I64, [I64, I64, I64]),
+    "gmr_gemm_f32": (I32, [I32, I32, I64, I64, I64, F32, P, I64, P, I64, F32, P, I64, I32, P, P, I64, P, I64, P, P,
+                           F32, I32, I32, P, I64, P]),
+    "gmr_dmm_combine_fwd": (I32, [I64, P, P, P, P, P, F32, P, P]),
+    "gmr_dmm_final_fwd": (I32, [I64, P, P, F32, P, P, P]),
+    "gmr_dmm_cl_fwd": (I32, [I64, P, P, P, P, P, P]),
+    "gmr_dmm_final_bwd": (I32, [I64, P, P, P, P, F32, P, P, P, P, P]),
+    "gmr_dmm_final_bwd_partials": (I64, [I64]),
+    "gmr_dmm_mw_grad": (I32, [I64, P, P, P, I32, P]),
+    "gmr_dmm_dg": (I32, [I64, I64, P, P, P, P]),
+    "gmr_dmm_cl_bwd": (I32, [I64, P, P, P, F32, P, P, P]),
+    "gmr_dmm_assemble": (I32, [I64, I64, P, P, P, P, P, F32, P, P, P]),
+    "gmr_normalize_rows_f32": (I32, [I64, I32, P, I64, P, I64, P, P]),
+    "gmr_normalize_rows_bwd_f32": (I32, [I64, I32, P, I64, P, P, I64, P, I64, F32, I32, P]),
+    "gmr_bpr_fwd_bwd": (I32, [I32, I64, P, P, P, P, P, P, P]),
+    "gmr_row_softmax_f32": (I32, [I64, I64, P, I64, F32, P, P]),
+    "gmr_contrast_rows": (I32, [I32, P, P, I64, P, F32, F32, P, P, I64, P]),
+    "gmr_gather_rows_f32": (I32, [I32, I32, P, I64, P, I64, P, I64, P]),
+    "gmr_scatter_sorted_f32": (I32, [I32, I32, P, P, I64, P, I64, P]),
+    "gmr_sort_batch_keys": (I32, [I64, P, P, P, I32, I64, P, I64, I32, P]),
+    "gmr_sum_f32": (I32, [I64, P, F32, P, I32, P]),
+    "gmr_sqnorm_f32": (I32, [I64, P, F32, P, I32, P]),
+    "gmr_colsum_f32": (I32, [I64, I64, P, I64, P, I32, P, I32, P]),
+    "gmr_sample_epoch": (I32, [I64, P, P, P, P, P, I64, U64, U64, P, P, P, P]),
+    "gmr_permutation": (I32, [I64, U64, U64, P, P]),
+    "gmr_diff_sample_t": (I32, [I32, I32, U64, U64, P, P]),
+    "gmr_diff_qsample": (I32, [I32, I32, P, P, P, P, P, P, P, I64, P, I64, F32, I32, U64, U64, P, I64, P]),
+    "gmr_diff_densify": (I32, [I32, I32, P, P, P, P, I64, P]),
+    "gmr_diff_time_bias": (I32, [I32, I32, P, P, P, I64, I64, P, I32, P, P, P, P]),
+    "gmr_diff_loss_rows": (I32, [I32, I32, P, P, P, P, P, P, I64, F32, P, P, I32, P]),
+    "gmr_diff_gc_rows": (I32, [I32, P, P, P, P, I64, P, I64, F32, P, I64, P, P]),
+    "gmr_diff_time_bwd": (I32, [I32, I32, I32, P, P, P, P, I64, I64, P, P, P, P, I32, P]),
+    "gmr_mask_scores_f32": (I32, [I64, P, P, P, I64, F32, P]),
+    "gmr_topk_rows_f32": (I32, [I64, I64, P, I64, I32, P, I64, P, P]),
+    "gmr_eval_metrics_partials": (I64, [I64]),
+    "gmr_eval_metrics": (I32, [I64, P, I64, I32, P, P, I32, P, P, P, P]),
+    "gmr_adam_f32": (I32, [I64, P, P, P, P, F32, F32, F32, F32, F32, F32, P]),
+}
+
+_lib = None
+
+
+class HipLibraryMissing(RuntimeError):
+    pass
+
+
+def load():
+    """Load libgmr_hip.so (after torch, so the process shares torch's HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (loads torch's libamdhip64 first; our .so binds to it by SONAME)
+
+    if not os.path.exists(LIB_PATH):
+        raise HipLibraryMissing(
+            f"libgmr_hip.so not found at {LIB_PATH}; build it with `make -C generative-multimodal-recommendation_amd`"
+            " or __graft_entry__.build(). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, name="gmr"):
+    if rc != 0:
+        msg = load().gmr_last_error_string()
+        raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc
+
+
+def call(name, *args):
+    """Call an int-returning entry point and raise on a non-zero status."""
+    fn = getattr(load(), name)
+    return check(fn(*args), name)

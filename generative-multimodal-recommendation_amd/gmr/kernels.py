@@ -1,0 +1,192 @@
+"""Thin tensor-level wrappers over the C-ABI (include/gmr.h).
+
+Every function takes torch tensors that already live on the GPU, passes raw device
+pointers + the current torch HIP stream to libgmr_hip.so, and raises on error.  Torch is
+used here only for memory and streams.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+EPI_NONE, EPI_BIAS, EPI_BIAS_TANH, EPI_LEAKY, EPI_POSTERIOR, EPI_DTANH, EPI_ROWSCALE_AUX = range(7)
+
+_ws = {}
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("gmr kernels take device tensors only (no CPU fallback)")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _ld(t):
+    if t.dim() == 1:
+        return t.shape[0]
+    if t.stride(-1) != 1:
+        raise ValueError("inner dimension must be contiguous")
+    return t.stride(0)
+
+
+def workspace(nfloats, device, tag="gemm"):
+    key = (tag, device)
+    w = _ws.get(key)
+    if w is None or w.numel() < nfloats:
+        w = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
+        _ws[key] = w
+    return w
+
+
+def zero_(t):
+    _lib.call("gmr_zero", ptr(t), t.numel() * t.element_size(), stream())
+    return t
+
+
+# ----------------------------------------------------------------------------- GEMM
+def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NONE, bias=None, bias_row=None,
+         ld_bias=0, aux=None, rv1=None, rv2=None, slope=0.0, tile=0, split_k=0):
+    """C = epi(alpha * op(A) @ op(B) ...), see include/gmr.h gmr_gemm_f32."""
+    M, N = C.shape
+    K = A.shape[0] if trans_a else A.shape[1]
+    if (A.shape[1] if trans_a else A.shape[0]) != M:
+        raise ValueError(f"A shape {tuple(A.shape)} does not give M={M}")
+    if (B.shape[1] if trans_b else B.shape[0]) != K or (B.shape[0] if trans_b else B.shape[1]) != N:
+        raise ValueError(f"B shape {tuple(B.shape)} does not match K={K}, N={N}")
+    for t in (A, B, C):
+        if t.dtype != torch.float32:
+            raise TypeError("gemm is fp32")
+    ws = workspace(16 * M * N, C.device)
+    _lib.call("gmr_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), ptr(A), _ld(A), ptr(B), _ld(B),
+              float(beta), ptr(C), _ld(C), epi, ptr(bias), ptr(bias_row), ld_bias, ptr(aux),
+              _ld(aux) if aux is not None else 0, ptr(rv1), ptr(rv2), float(slope), tile, split_k, ptr(ws), ws.numel(),
+              stream())
+    return C
+
+
+# ----------------------------------------------------------------------------- SpMM
+class CSR:
+    """Device CSR (int32 rowptr/col, fp32 val) of an n x n matrix with its SpMM work plan."""
+
+    def __init__(self, rowptr, col, val, n_cols=None, seg_nnz=256, symmetric=True):
+        self.rowptr, self.col, self.val = rowptr, col, val
+        self.n_rows = rowptr.numel() - 1
+        self.n_cols = self.n_rows if n_cols is None else n_cols
+        self.nnz = col.numel()
+        self.seg_nnz = seg_nnz
+        self.symmetric = symmetric
+        dev = rowptr.device
+        words = _lib.load().gmr_spmm_plan_words(self.n_rows, self.nnz, seg_nnz)
+        self.plan = torch.empty(words, dtype=torch.int32, device=dev)
+        prow = _lib.load().gmr_spmm_partial_rows(self.n_rows, self.nnz, seg_nnz)
+        self.partial = torch.empty((prow, 256), dtype=torch.float32, device=dev)
+        _lib.call("gmr_spmm_plan_build", ptr(rowptr), self.n_rows, self.nnz, seg_nnz, ptr(self.plan), stream())
+
+    def spmm(self, out, blocks, split=None, alpha=1.0, beta=0.0):
+        """out = alpha * A @ X + beta * out; X = column blocks [(lo, hi), ...] of 64 columns each.
+
+        Source row s of a block reads lo[s] if s < split else hi[s - split] (hi may be None
+        when split is None, i.e. lo covers all rows)."""
+        nb = len(blocks)
+        if nb not in (1, 2, 4):
+            raise ValueError("1, 2 or 4 blocks of 64 columns")
+        if out.shape[0] != self.n_rows or out.shape[1] != 64 * nb:
+            raise ValueError(f"out shape {tuple(out.shape)} != ({self.n_rows}, {64 * nb})")
+        PArr = ctypes.c_void_p * 4
+        LArr = ctypes.c_int64 * 4
+        lo = PArr(*[b[0].data_ptr() for b in blocks] + [0] * (4 - nb))
+        ldl = LArr(*[_ld(b[0]) for b in blocks] + [0] * (4 - nb))
+        if split is None:
+            split = self.n_cols
+            hi, ldh = lo, ldl
+        else:
+            hi = PArr(*[b[1].data_ptr() for b in blocks] + [0] * (4 - nb))
+            ldh = LArr(*[_ld(b[1]) for b in blocks] + [0] * (4 - nb))
+        for b in blocks:
+            if b[0].shape[1] != 64 or (split != self.n_cols and b[1].shape[1] != 64):
+                raise ValueError("each block is 64 columns wide")
+        _lib.call("gmr_spmm_csr_f32", ptr(self.rowptr), ptr(self.col), ptr(self.val), self.n_rows, self.nnz,
+                  ptr(self.plan), self.seg_nnz, ptr(self.partial), nb, lo, ldl, hi, ldh, split, float(alpha),
+                  float(beta), ptr(out), _ld(out), stream())
+        return out
+
+
+def bipartite_symnorm(n_users, n_items, user_ptr, user_items, self_loops, deg_eps, seg_nnz=256):
+    """Build the normalised (U+I)^2 bipartite adjacency on the device (graph.hip)."""
+    lib = _lib.load()
+    dev = user_ptr.device
+    n_ui = user_items.numel()
+    nnz = lib.gmr_bipartite_nnz(n_users, n_items, n_ui, int(self_loops))
+    N = n_users + n_items
+    rowptr = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    val = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    ws = torch.empty(lib.gmr_bipartite_workspace_ints(n_users, n_items), dtype=torch.int32, device=dev)
+    _lib.call("gmr_bipartite_symnorm_build", n_users, n_items, ptr(user_ptr), ptr(user_items), n_ui,
+              int(self_loops), float(deg_eps), ptr(ws), ptr(rowptr), ptr(col), ptr(val), stream())
+    return CSR(rowptr, col[:nnz], val[:nnz], seg_nnz=seg_nnz)
+
+
+def topk_to_user_csr(topk, user_ptr, user_items):
+    U, k = topk.shape
+    _lib.call("gmr_topk_to_user_csr", U, k, ptr(topk), _ld(topk), ptr(user_ptr), ptr(user_items), stream())
+
+
+# ----------------------------------------------------------------------------- rows / reductions
+def normalize_rows(x, y, nrm=None):
+    n, cols = x.shape
+    _lib.call("gmr_normalize_rows_f32", n, cols, ptr(x), _ld(x), ptr(y), _ld(y), ptr(nrm), stream())
+    return y
+
+
+def normalize_rows_bwd(y, nrm, dy, dx, slope=1.0, accumulate=False):
+    n, cols = y.shape
+    _lib.call("gmr_normalize_rows_bwd_f32", n, cols, ptr(y), _ld(y), ptr(nrm), ptr(dy), _ld(dy), ptr(dx), _ld(dx),
+              float(slope), int(accumulate), stream())
+    return dx
+
+
+def topk_rows(scores, k, out_idx, out_val=None):
+    n, m = scores.shape
+    _lib.call("gmr_topk_rows_f32", n, m, ptr(scores), _ld(scores), int(k), ptr(out_idx), _ld(out_idx), ptr(out_val),
+              stream())
+    return out_idx
+
+
+def mask_scores(scores, rows, cols, fill=-1e10):
+    _lib.call("gmr_mask_scores_f32", rows.numel(), ptr(rows), ptr(cols), ptr(scores), _ld(scores), float(fill),
+              stream())
+
+
+def colsum(x, out, group=None, n_groups=1, accumulate=False):
+    rows, cols = x.shape
+    _lib.call("gmr_colsum_f32", rows, cols, ptr(x), _ld(x), ptr(group), n_groups, ptr(out), int(accumulate),
+              stream())
+    return out
+
+
+def gather_rows(src, idx, out, off=0):
+    B = idx.numel()
+    _lib.call("gmr_gather_rows_f32", B, out.shape[1], ptr(src), _ld(src), ptr(idx), off, ptr(out), _ld(out),
+              stream())
+    return out
+
+
+def adam(param, grad, m, v, lr, beta1, beta2, eps, weight_decay, step):
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    _lib.call("gmr_adam_f32", param.numel(), ptr(param), ptr(grad), ptr(m), ptr(v), float(beta1), float(beta2),
+              float(eps), float(weight_decay), float(lr / bc1), float(bc2 ** 0.5), stream())
+
+
+def eval_metrics(topk, pos_ptr, pos_items, ks, partials, out_sums):
+    n, K = topk.shape
+    ks_t = ks
+    _lib.call("gmr_eval_metrics", n, ptr(topk), _ld(topk), K, ptr(pos_ptr), ptr(pos_items), ks_t.numel(), ptr(ks_t),
+              ptr(partials), ptr(out_sums), stream())

@@ -1,0 +1,191 @@
+/* libgmr_hip.so — C-ABI of the MI355X-native GenMMRec hot path (gfx950).
+ *
+ * The reference (orangeai-research/Generative-Multimodal-Recommendation, GenMMRec/src) is pure
+ * PyTorch: its hot path has no FFI.  The boundary it exposes is the Python module API
+ * (GeneralRecommender.calculate_loss / full_sort_predict, the trainers' diffusion hooks);
+ * every entry point below replaces the torch/ATen call sites named in its comment, and the
+ * Python package `gmr` (generative-multimodal-recommendation_amd/gmr) binds them with ctypes.
+ *
+ * Conventions
+ *   - all pointers are DEVICE pointers unless the comment says "host"; the caller owns every
+ *     buffer (no allocation inside); workspaces are sized by the *_words and *_floats helpers;
+ *   - matrices are row-major with an explicit leading dimension (elements);
+ *   - every call is asynchronous on `stream` (a hipStream_t; NULL = legacy default stream);
+ *   - return 0 on success, GMR_ERR_ARG for a rejected argument, or -(hipError_t);
+ *     gmr_last_error_string() describes the last failure of the calling thread;
+ *   - calls are stateless and re-entrant (safe from several threads on different streams).
+ */
+#ifndef GMR_H_
+#define GMR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GMR_ABI_VERSION 1
+#define GMR_OK 0
+#define GMR_ERR_ARG (-1000)
+
+/* GEMM epilogues (gmr_gemm_f32) */
+#define GMR_EPI_NONE 0         /* C = alpha*acc + beta*C                                  */
+#define GMR_EPI_BIAS 1         /* C = alpha*acc + bias + beta*C                           */
+#define GMR_EPI_BIAS_TANH 2    /* C = tanh(alpha*acc + bias)            Denoise in_layers */
+#define GMR_EPI_LEAKY 3        /* C = leaky_relu(alpha*acc + bias, slope)  modal projection */
+#define GMR_EPI_POSTERIOR 4    /* C = c1*(alpha*acc + bias) + c2*aux[m,n], c1 = rv1 ? rv1[m] : slope,
+                                  c2 = rv2 ? rv2[m] : beta            p_sample posterior mean */
+#define GMR_EPI_DTANH 5        /* C = alpha*acc * (1 - aux[m,n]^2)      tanh backward      */
+#define GMR_EPI_ROWSCALE_AUX 6 /* C = alpha*acc + bias + rv1[m]*aux[m,n]                  */
+
+const char* gmr_last_error_string(void);
+int gmr_version(void);
+int gmr_device_name(char* buf /* host */, int32_t len);
+int gmr_zero(void* ptr, int64_t bytes, void* stream);
+
+/* ---------------------------------------------------------------- K1 graph convolution
+ * Y = alpha * A * X + beta * Y for CSR A (int32 rowptr/col, fp32 val).
+ * Replaces torch.spmm / torch.sparse.mm: models/diffmm.py:136,139,142,146,149,152,176,179,285;
+ * lightgcn.py:120.  X is n_blocks (1,2,4) column blocks of 64 floats; block b reads source
+ * row s from x_lo[b] + s*ld_lo[b] when s < split, else x_hi[b] + (s-split)*ld_hi[b]
+ * (x_lo/x_hi/ld_* are HOST arrays of device pointers / strides).  A plan (built once per
+ * matrix by gmr_spmm_plan_build) cuts rows into <= seg_nnz segments for load balance;
+ * `partial` holds gmr_spmm_partial_rows(...) x (64*n_blocks) floats for hub rows. */
+int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_nnz);
+int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t seg_nnz);
+int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t seg_nnz, int32_t* plan,
+                        void* stream);
+int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
+                     const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,
+                     const float* const* x_lo, const int64_t* ld_lo, const float* const* x_hi, const int64_t* ld_hi,
+                     int64_t split, float alpha, float beta, float* y, int64_t ldy, void* stream);
+
+/* ---------------------------------------------------------------- K11 graph construction
+ * Symmetric-normalised bipartite adjacency (N = U + I) in CSR from a user->items CSR
+ * (items ascending and distinct per user).  Replaces DiffMM.get_norm_adj_mat
+ * (models/diffmm.py:88-107: self_loops=0, deg_eps=1e-7) and DiffMMTrainer.buildUIMatrix +
+ * normalizeAdj (common/trainer.py:464-485: self_loops=1, deg_eps=0).  rowptr: N+1, col/val:
+ * gmr_bipartite_nnz(...) entries, workspace: gmr_bipartite_workspace_ints(...) ints. */
+int64_t gmr_bipartite_nnz(int64_t n_users, int64_t n_items, int64_t n_user_items, int32_t self_loops);
+int64_t gmr_bipartite_workspace_ints(int64_t n_users, int64_t n_items);
+int gmr_bipartite_symnorm_build(int64_t n_users, int64_t n_items, const int32_t* user_ptr, const int32_t* user_items,
+                                int64_t n_user_items, int32_t self_loops, double deg_eps, int32_t* workspace,
+                                int32_t* rowptr, int32_t* col, float* val, void* stream);
+/* per-user top-k item lists (n_users x k, ld) -> user CSR with items sorted (trainer.py:545-562) */
+int gmr_topk_to_user_csr(int64_t n_users, int32_t k, const int32_t* topk, int64_t ld, int32_t* user_ptr,
+                         int32_t* user_items, void* stream);
+
+/* ---------------------------------------------------------------- K3/K4/K6/K9 dense GEMM (fp32 MFMA)
+ * C[M,N] = epilogue(alpha * op(A) op(B)); op(A) = A (M x K, lda) or A^T (A stored K x M);
+ * op(B) = B (K x N, ldb) or B^T (B stored N x K).  bias[(bias_row ? bias_row[m] : 0)*ld_bias + n].
+ * Replaces nn.Linear / torch.mm / matmul: diffmm.py:117,124,277,352-358,472-473; vbpr.py:70,105.
+ * tile: 0 auto, 64 or 128; split_k: 0 auto, else >= 1 (needs workspace >= splits*M*N floats). */
+int64_t gmr_gemm_workspace_floats(int64_t M, int64_t N, int64_t K);
+int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+                 int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc, int32_t epilogue,
+                 const float* bias, const int32_t* bias_row, int64_t ld_bias, const float* aux, int64_t ld_aux,
+                 const float* rowvec1, const float* rowvec2, float slope, int32_t tile, int32_t split_k,
+                 float* workspace, int64_t workspace_floats, void* stream);
+
+/* ---------------------------------------------------------------- DiffMM rec step (diffmm.py:129-258)
+ * Fused row kernels of forward_MM / forward_cl_MM / calculate_loss and their backward
+ * (layouts in csrc/diffmm.hip). */
+int gmr_dmm_combine_fwd(int64_t n, float* G, const float* H, const float* Qi, const float* Qt, const float* mw,
+                        float lam, float* M, void* stream);
+int gmr_dmm_final_fwd(int64_t n, const float* M, const float* L, float ris, float* Emb, float* nrm, void* stream);
+int gmr_dmm_cl_fwd(int64_t n, const float* Qi, const float* Qt, const float* K2, float* CLN, float* nrm,
+                   void* stream);
+int gmr_dmm_final_bwd(int64_t n, const float* dEmb, const float* T1, const float* M, const float* nrmM, float ris,
+                      const float* E, const float* mw, float* dE, float* partials, void* stream);
+int64_t gmr_dmm_final_bwd_partials(int64_t n);
+int gmr_dmm_mw_grad(int64_t nparts, const float* partials, const float* mw, float* dmw, int32_t accumulate,
+                    void* stream);
+int gmr_dmm_dg(int64_t n, int64_t U, const float* dE, const float* T2, float* dG, void* stream);
+int gmr_dmm_cl_bwd(int64_t n, const float* dK, const float* T, const float* dE, float lam, float* Ri, float* Rt,
+                   void* stream);
+int gmr_dmm_assemble(int64_t n, int64_t U, const float* T2, const float* T3, const float* Ri, const float* Rt,
+                     const float* E0, float reg2, float* dE0, float* dNF, void* stream);
+
+/* F.normalize (p=2, eps=1e-12) over rows and its backward (optionally fused with leaky-ReLU backward) */
+int gmr_normalize_rows_f32(int64_t n, int32_t cols, const float* x, int64_t ldx, float* y, int64_t ldy, float* nrm,
+                           void* stream);
+int gmr_normalize_rows_bwd_f32(int64_t n, int32_t cols, const float* y, int64_t ldy, const float* nrm, const float* dy,
+                               int64_t lddy, float* dx, int64_t lddx, float slope, int32_t accumulate, void* stream);
+
+/* K7 BPR: -log(1e-10 + sigmoid(<a,p> - <a,n>)) with gathers; per-row loss + 3B contribution rows
+ * (diffmm.py:220-227, common/loss.py:33-37) */
+int gmr_bpr_fwd_bwd(int32_t B, int64_t U, const float* Emb, const int32_t* users, const int32_t* pos,
+                    const int32_t* neg, float* loss, float* contrib, void* stream);
+/* K8 InfoNCE pieces (diffmm.py:251-258): in-place row softmax of logits with log-sum-exp out,
+ * and the per-row terms of the gathered batch */
+int gmr_row_softmax_f32(int64_t rows, int64_t cols, float* L, int64_t ld, float coef, float* lse, void* stream);
+int gmr_contrast_rows(int32_t B, const float* CLN, const int32_t* nodes, int64_t node_off, const float* lse,
+                      float inv_temp, float coef, float* loss, float* contrib, int64_t ld_contrib, void* stream);
+/* K2 gather / deterministic scatter-add through a sorted (key << 32 | slot) plan */
+int gmr_gather_rows_f32(int32_t B, int32_t cols, const float* src, int64_t lds, const int32_t* idx, int64_t off,
+                        float* out, int64_t ldo, void* stream);
+int gmr_scatter_sorted_f32(int32_t n, int32_t cols, const uint64_t* plan, const float* contrib, int64_t ldc,
+                           float* dst, int64_t ldd, void* stream);
+int gmr_sort_batch_keys(int64_t n_batches, const int32_t* keys, const int64_t* offsets, const int32_t* key_add,
+                        int32_t n_keysets, int64_t key_stride, uint64_t* out, int64_t out_stride, int32_t pow2,
+                        void* stream);
+/* deterministic reductions */
+int gmr_sum_f32(int64_t n, const float* x, float scale, float* out, int32_t accumulate, void* stream);
+int gmr_sqnorm_f32(int64_t n, const float* x, float scale, float* out, int32_t accumulate, void* stream);
+int gmr_colsum_f32(int64_t rows, int64_t cols, const float* x, int64_t ld, const int32_t* group, int32_t n_groups,
+                   float* out, int32_t accumulate, void* stream);
+
+/* ---------------------------------------------------------------- BPR epoch sampler (dataloader.py:218-275)
+ * shuffled interactions + one rejection-sampled negative from `all_items` per interaction */
+int gmr_sample_epoch(int64_t n_inter, const int32_t* inter_user, const int32_t* inter_item, const int32_t* user_rowptr,
+                     const int32_t* user_items, const int32_t* all_items, int64_t n_all_items, uint64_t seed,
+                     uint64_t epoch, int32_t* out_users, int32_t* out_pos, int32_t* out_neg, void* stream);
+/* random permutation of [0, n) (DataLoader(shuffle=True) over users, trainer.py:462) */
+int gmr_permutation(int64_t n, uint64_t seed, uint64_t epoch, int32_t* out, void* stream);
+
+/* ---------------------------------------------------------------- K5/K6 diffusion (diffmm.py:408-484, diffrec.py:182-310)
+ * x_t = sqrt_ac[t]*x0 + sqrt_1mac[t]*eps, times the Denoise input dropout keep/keep_prob when
+ * dropout != 0; x0 rows come from the user's train items.  noise/keep may be NULL (Philox). */
+int gmr_diff_sample_t(int32_t B, int32_t T, uint64_t seed, uint64_t step, int32_t* t, void* stream);
+int gmr_diff_qsample(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
+                     const int32_t* t, const float* sqrt_ac, const float* sqrt_1mac, const float* noise,
+                     int64_t ld_noise, const float* keep, int64_t ld_keep, float keep_prob, int32_t dropout,
+                     uint64_t seed, uint64_t step, float* x, int64_t ldx, void* stream);
+int gmr_diff_densify(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
+                     float* x, int64_t ldx, void* stream);
+int gmr_diff_time_bias(int32_t T, int32_t E, const float* emb_W, const float* emb_b, const float* W1, int64_t ld_w1,
+                       int64_t col_off, const float* b1, int32_t H, float* EB, float* temb_out, float* emb_out,
+                       void* stream);
+int gmr_diff_loss_rows(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
+                       const int32_t* t, const double* wtab, float* out, int64_t ld, float grad_scale,
+                       double* mse_out, double* diff_out, int32_t write_grad, void* stream);
+int gmr_diff_gc_rows(int32_t B, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
+                     const float* item_embeds, int64_t ld_ie, const float* Z, int64_t ldz, float gscale, float* G,
+                     int64_t ldg, double* gc_out, void* stream);
+int gmr_diff_time_bwd(int32_t T, int32_t E, int32_t H, const float* S, const float* temb, const float* emb,
+                      const float* W1, int64_t ld_w1, int64_t col_off, float* dW1, float* db1, float* d_emb_W,
+                      float* d_emb_b, int32_t accumulate, void* stream);
+
+/* ---------------------------------------------------------------- K10/K12 eval tail (trainer.py:369-388)
+ * ties -> lowest index; k <= 64 */
+int gmr_mask_scores_f32(int64_t n, const int32_t* rows, const int32_t* cols, float* scores, int64_t ld, float fill,
+                        void* stream);
+int gmr_topk_rows_f32(int64_t n_rows, int64_t n_cols, const float* scores, int64_t ld, int32_t k, int32_t* out_idx,
+                      int64_t ld_idx, float* out_val, void* stream);
+/* Recall/NDCG/Precision/MAP sums over users at ks (topk_evaluator.py:107-120, metrics.py):
+ * out_sums[metric*8 + j], metric 0 recall 1 ndcg 2 precision 3 map, j < n_ks (fp64). */
+int64_t gmr_eval_metrics_partials(int64_t n_users);
+int gmr_eval_metrics(int64_t n_users, const int32_t* topk, int64_t ld_topk, int32_t K, const int64_t* pos_ptr,
+                     const int32_t* pos_items, int32_t n_ks, const int32_t* ks, double* partials, double* out_sums,
+                     void* stream);
+
+/* ---------------------------------------------------------------- optimizer (torch.optim.Adam, trainer.py:125-142)
+ * flat fp32 slabs; step_size = lr / (1 - b1^t), bias_correction2_sqrt = sqrt(1 - b2^t) */
+int gmr_adam_f32(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float beta1,
+                 float beta2, float eps, float weight_decay, float step_size, float bias_correction2_sqrt,
+                 void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GMR_H_ */

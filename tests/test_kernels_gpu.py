@@ -1,0 +1,225 @@
+"""HIP kernels vs the CPU oracle / torch-fp32 references, through the C-ABI (GPU only)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import eval_ref, graph_ref, model_ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def K():
+    from gmr import kernels, _lib
+    _lib.load()
+    return kernels
+
+
+def _rng(s=0):
+    return np.random.default_rng(s)
+
+
+def _user_csr(U, I, rows, cols):
+    key = np.unique(rows.astype(np.int64) * I + cols)
+    u, i = key // I, key % I
+    ptr = np.zeros(U + 1, np.int64)
+    np.add.at(ptr, u + 1, 1)
+    return np.cumsum(ptr).astype(np.int32), i.astype(np.int32)
+
+
+def _dev(a, dt=None):
+    t = torch.as_tensor(np.ascontiguousarray(a))
+    if dt is not None:
+        t = t.to(dt)
+    return t.to(DEV)
+
+
+@pytest.mark.parametrize("self_loops,eps", [(0, 1e-7), (1, 0.0)])
+def test_bipartite_build_bit_exact(K, golden, self_loops, eps):
+    g = golden("diffmm_tiny")
+    U, I = int(g["U"]), int(g["I"])
+    if self_loops:
+        rows, cols = np.repeat(np.arange(U), 3), g["ui_k3_items"].reshape(-1)
+        want = graph_ref.ui_adj_csr(U, I, rows, cols)
+    else:
+        rows, cols = g["train_rows"], g["train_cols"]
+        want = graph_ref.norm_adj_csr(U, I, rows, cols)
+    uptr, uitems = _user_csr(U, I, rows, cols)
+    csr = K.bipartite_symnorm(U, I, _dev(uptr), _dev(uitems), self_loops, eps)
+    torch.cuda.synchronize()
+    assert np.array_equal(csr.rowptr.cpu().numpy(), want[0])
+    assert np.array_equal(csr.col.cpu().numpy(), want[1])
+    assert np.array_equal(csr.val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
+
+
+def test_bipartite_build_large_hubs(K):
+    rng = _rng(1)
+    U, I = 3000, 500
+    rows = np.repeat(np.arange(U), 7)
+    p = 1.0 / np.arange(1, I + 1) ** 1.2
+    cols = rng.choice(I, size=rows.size, p=p / p.sum())
+    want = graph_ref.norm_adj_csr(U, I, rows, cols)
+    uptr, uitems = _user_csr(U, I, rows, cols)
+    csr = K.bipartite_symnorm(U, I, _dev(uptr), _dev(uitems), 0, 1e-7)
+    assert np.array_equal(csr.col.cpu().numpy(), want[1])
+    assert np.array_equal(csr.val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
+
+
+@pytest.mark.parametrize("nb", [1, 2, 4])
+def test_spmm_vs_oracle(K, nb):
+    rng = _rng(2)
+    U, I = 2500, 900
+    rows = np.repeat(np.arange(U), rng.integers(1, 20, size=U))
+    p = 1.0 / np.arange(1, I + 1) ** 1.1
+    cols = rng.choice(I, size=rows.size, p=p / p.sum())  # hub items -> multi-segment rows
+    rp, col, val = graph_ref.norm_adj_csr(U, I, rows, cols)
+    N = U + I
+    csr = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=64)
+    X = rng.standard_normal((N, 64 * nb)).astype(np.float32)
+    Y0 = rng.standard_normal((N, 64 * nb)).astype(np.float32)
+    Xd, Yd = _dev(X), _dev(Y0)
+    blocks = [(Xd[:, 64 * b:64 * (b + 1)],) for b in range(nb)]
+    K.CSR.spmm(csr, Yd, blocks, alpha=0.7, beta=0.3)
+    A = graph_ref.csr_to_dense(rp, col, val).astype(np.float64)
+    want = 0.7 * (A @ X.astype(np.float64)) + 0.3 * Y0
+    np.testing.assert_allclose(Yd.cpu().numpy(), want, rtol=1e-5, atol=1e-5)
+
+
+def test_spmm_split_sources(K):
+    rng = _rng(3)
+    U, I = 300, 200
+    rows = np.repeat(np.arange(U), 6)
+    cols = rng.integers(0, I, size=rows.size)
+    rp, col, val = graph_ref.norm_adj_csr(U, I, rows, cols)
+    csr = K.CSR(_dev(rp), _dev(col), _dev(val))
+    uE = rng.standard_normal((U, 64)).astype(np.float32)
+    F = rng.standard_normal((I, 128)).astype(np.float32)
+    uEd, Fd = _dev(uE), _dev(F)
+    out = torch.empty((U + I, 128), device=DEV)
+    csr.spmm(out, [(uEd, Fd[:, :64]), (uEd, Fd[:, 64:])], split=U)
+    A = graph_ref.csr_to_dense(rp, col, val).astype(np.float64)
+    want0 = A @ np.concatenate([uE, F[:, :64]]).astype(np.float64)
+    want1 = A @ np.concatenate([uE, F[:, 64:]]).astype(np.float64)
+    np.testing.assert_allclose(out.cpu().numpy(), np.concatenate([want0, want1], 1), rtol=1e-5, atol=1e-5)
+
+
+GEMM_CASES = [
+    # (M, N, K, ta, tb)
+    (2048, 1000, 7050, 0, 1), (2048, 7050, 1000, 0, 1), (2048, 1000, 7050, 0, 0), (7050, 1000, 2048, 1, 0),
+    (97, 61, 33, 0, 0), (61, 97, 130, 1, 1), (130, 64, 4096, 0, 0), (4096, 64, 7050, 1, 0), (37, 5, 3, 1, 0),
+]
+
+
+@pytest.mark.parametrize("M,N,Kd,ta,tb", GEMM_CASES)
+def test_gemm_vs_torch_fp32(K, M, N, Kd, ta, tb):
+    torch.manual_seed(0)
+    A = torch.randn(Kd, M) if ta else torch.randn(M, Kd)
+    B = torch.randn(N, Kd) if tb else torch.randn(Kd, N)
+    ref = (A.T if ta else A).double() @ (B.T if tb else B).double()
+    C = torch.empty(M, N, device=DEV)
+    K.gemm(A.to(DEV), B.to(DEV), C, trans_a=bool(ta), trans_b=bool(tb))
+    err = (C.cpu().double() - ref).abs().max().item()
+    scale = ((A.abs().T if ta else A.abs()).double() @ (B.abs().T if tb else B.abs()).double()).max().item()
+    assert err <= 2e-6 * scale, (err, scale)
+
+
+def test_gemm_unaligned_ld(K):
+    torch.manual_seed(1)
+    A = torch.randn(50, 71)[:, :69]  # lda = 71 (not a multiple of 4)
+    B = torch.randn(69, 33)
+    C = torch.empty(50, 33, device=DEV)
+    K.gemm(A.to(DEV), B.to(DEV), C)
+    np.testing.assert_allclose(C.cpu().numpy(), (A @ B).numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_gemm_epilogues(K):
+    torch.manual_seed(2)
+    M, N, Kd, T = 200, 96, 150, 5
+    A, B = torch.randn(M, Kd), torch.randn(N, Kd)
+    acc = A.double() @ B.double().T
+    eb = torch.randn(T, N)
+    t = torch.randint(0, T, (M,), dtype=torch.int32)
+    C = torch.empty(M, N, device=DEV)
+    K.gemm(A.to(DEV), B.to(DEV), C, trans_b=True, epi=K.EPI_BIAS_TANH, bias=eb.to(DEV), bias_row=t.to(DEV), ld_bias=N)
+    np.testing.assert_allclose(C.cpu().numpy(), torch.tanh(acc + eb[t.long()].double()).numpy(), rtol=1e-5, atol=1e-5)
+    aux = torch.randn(M, N)
+    b = torch.randn(N)
+    K.gemm(A.to(DEV), B.to(DEV), C.copy_(aux.to(DEV)), trans_b=True, epi=K.EPI_POSTERIOR, bias=b.to(DEV), aux=C,
+           slope=0.25, beta=0.75)
+    np.testing.assert_allclose(C.cpu().numpy(), (0.25 * (acc + b.double()) + 0.75 * aux.double()).numpy(), rtol=1e-5,
+                               atol=1e-5)
+    K.gemm(A.to(DEV), B.to(DEV), C, trans_b=True, epi=K.EPI_DTANH, aux=aux.to(DEV))
+    np.testing.assert_allclose(C.cpu().numpy(), (acc * (1 - aux.double() ** 2)).numpy(), rtol=1e-5, atol=1e-4)
+    K.gemm(A.to(DEV), B.to(DEV), C, trans_b=True, epi=K.EPI_LEAKY, slope=0.2)
+    np.testing.assert_allclose(C.cpu().numpy(), torch.nn.functional.leaky_relu(acc, 0.2).numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("k", [1, 10, 50])
+def test_topk_rows_vs_oracle(K, k):
+    rng = _rng(4)
+    S = rng.standard_normal((300, 7050)).astype(np.float32)
+    S[:, ::7] = np.float32(0.5)   # many exact ties
+    S[5] = 1.0                     # all-equal row
+    S[6, :100] = -1e10
+    out = torch.empty((300, k), dtype=torch.int32, device=DEV)
+    K.topk_rows(_dev(S), k, out)
+    assert np.array_equal(out.cpu().numpy(), eval_ref.topk_rows(S, k))
+
+
+def test_mask_and_topk_golden(K, golden):
+    g = golden("diffmm_tiny")
+    s = _dev(g["eval_scores_raw"])
+    K.mask_scores(s, _dev(g["eval_mask_rows"], torch.int32), _dev(g["eval_mask_cols"], torch.int32))
+    assert np.array_equal(s.cpu().numpy(), g["eval_scores_masked"])
+    out = torch.empty((s.shape[0], 50), dtype=torch.int32, device=DEV)
+    K.topk_rows(s, 50, out)
+    assert np.array_equal(out.cpu().numpy(), eval_ref.topk_rows(g["eval_scores_masked"], 50))
+
+
+def test_eval_metrics_vs_oracle(K, golden_meta):
+    rng = _rng(5)
+    n, Kk = 1000, 50
+    topk = np.stack([rng.choice(400, size=Kk, replace=False) for _ in range(n)]).astype(np.int32)
+    pos = [np.sort(rng.choice(400, size=int(rng.integers(1, 80)), replace=False)) for _ in range(n)]
+    ptr = np.concatenate([[0], np.cumsum([len(p) for p in pos])]).astype(np.int64)
+    from gmr import _lib
+    parts = torch.empty(_lib.load().gmr_eval_metrics_partials(n), dtype=torch.float64, device=DEV)
+    sums = torch.empty(32, dtype=torch.float64, device=DEV)
+    ks = _dev(np.array([5, 10, 20, 50], np.int32))
+    K.eval_metrics(_dev(topk), _dev(ptr), _dev(np.concatenate(pos).astype(np.int32)), ks, parts, sums)
+    got = sums.cpu().numpy().reshape(4, 8)[:, :4] / n
+    curves = eval_ref.metric_curves(eval_ref.hit_matrix(topk, pos), [len(p) for p in pos])
+    for mi, m in enumerate(["recall", "ndcg", "precision", "map"]):
+        np.testing.assert_allclose(got[mi], curves[m][[4, 9, 19, 49]], rtol=1e-12, atol=1e-14)
+
+
+def test_adam_vs_torch(K):
+    rng = _rng(6)
+    p0 = rng.standard_normal(1000).astype(np.float32)
+    gs = [[rng.standard_normal(1000).astype(np.float32)] for _ in range(4)]
+    want = model_ref.adam_reference([p0], gs, lr=1e-3)[0]
+    p, m, v = _dev(p0), torch.zeros(1000, device=DEV), torch.zeros(1000, device=DEV)
+    for i, g in enumerate(gs):
+        K.adam(p, _dev(g[0]), m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, i + 1)
+    np.testing.assert_allclose(p.cpu().numpy(), want, rtol=0, atol=2e-7)
+
+
+def test_normalize_rows_and_bwd(K):
+    torch.manual_seed(3)
+    x = torch.randn(333, 128)
+    x[7] = 0.0
+    xr = x.clone().requires_grad_(True)
+    y = torch.nn.functional.leaky_relu(xr, 0.2)
+    out = torch.nn.functional.normalize(y[:, :64])
+    dy = torch.randn(333, 64)
+    out.backward(dy)
+    F = torch.nn.functional.leaky_relu(x, 0.2).to(DEV)
+    yd = torch.empty(333, 64, device=DEV)
+    nrm = torch.empty(333, device=DEV)
+    K.normalize_rows(F[:, :64], yd, nrm)
+    np.testing.assert_allclose(yd.cpu().numpy(), out.detach().numpy(), rtol=1e-6, atol=1e-7)
+    dx = torch.empty(333, 64, device=DEV)
+    K.normalize_rows_bwd(yd, nrm, dy.to(DEV), dx, slope=0.2)
+    np.testing.assert_allclose(dx.cpu().numpy(), xr.grad[:, :64].numpy(), rtol=1e-5, atol=1e-6)
