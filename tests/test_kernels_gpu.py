@@ -203,7 +203,7 @@ def test_adam_vs_torch(K):
     p, m, v = _dev(p0), torch.zeros(1000, device=DEV), torch.zeros(1000, device=DEV)
     for i, g in enumerate(gs):
         K.adam(p, _dev(g[0]), m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, i + 1)
-    np.testing.assert_allclose(p.cpu().numpy(), want, rtol=0, atol=2e-7)
+    np.testing.assert_allclose(p.cpu().numpy(), want, rtol=3e-7, atol=1e-7)  # fp32 contraction: <= 1 ulp
 
 
 def test_normalize_rows_and_bwd(K):
