@@ -1,0 +1,241 @@
+"""Benchmark: DiffMM on Amazon-baby-shaped synthetic data, train users/s (+ full-rank eval users/s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
+
+One "step" = one full DiffMM training epoch of the reference's DiffMMTrainer._train_epoch
+(common/trainer.py:487-585): diffusion training of both denoisers over all users, the graph
+rebuild (p_sample + top-1 + normalised UI graphs) and the BPR/contrastive phase over all train
+interactions.  value = users/s = U * steps * N / wall (max over ranks); after the timed epochs one
+full-rank evaluation pass over the valid split is timed as eval users/s.
+Multi-GPU (N > 1): every rank trains its own replica of the baby workload (weak scaling, no
+data-path collective); the barrier + max-over-ranks timing follows the driver contract.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "generative-multimodal-recommendation_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "train users/sec + full-rank eval users/sec, DiffMM Amazon-baby, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0
+FP32_MFMA_PEAK_TFS = 157.3
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def setup(args):
+    from gmr.configurator import Config
+    from gmr.dataloader import EvalDataLoader, TrainDataLoader
+    from gmr.diffmm import DiffMM
+    from gmr.quick_start import popularity_groups
+    from gmr.synthetic import make_dataset
+    from gmr.trainer import DiffMMTrainer
+    from gmr.utils import init_seed
+
+    cfg = Config("DiffMM", "baby", {"synthetic": args.shape, "save_recommended_topk": False, "epochs": 1})
+    init_seed(999)
+    t0 = time.time()
+    ds = make_dataset(cfg, args.shape, seed=0)
+    tr, va, te = ds.split()
+    pop, warm, _, _ = popularity_groups(cfg, tr)
+    cfg["pop_items"], cfg["warm_users"] = pop, warm
+    tl = TrainDataLoader(cfg, tr, batch_size=cfg["train_batch_size"], shuffle=True)
+    vl = EvalDataLoader(cfg, va, additional_dataset=tr, batch_size=cfg["eval_batch_size"])
+    model = DiffMM(cfg, tl)
+    trainer = DiffMMTrainer(cfg, model)
+    torch.cuda.synchronize()
+    log(f"setup {time.time() - t0:.1f}s: U={ds.user_num} I={ds.item_num} train={len(tr)} valid users={vl.pr_end}")
+    return cfg, ds, tr, tl, vl, model, trainer
+
+
+def summarize_probe(p):
+    """Aggregate HIP-event timings per kernel class into roofline objects."""
+    out = {}
+    for tag, recs in p.items():
+        if not recs:
+            continue
+        ms = [s.elapsed_time(e) for s, e, _ in recs]
+        tot_ms = float(np.sum(ms))
+        if tag == "gemm":
+            work = sum(2.0 * M * N * K for M, N, K in (r[2] for r in recs))
+            achieved = work / (tot_ms * 1e-3) / 1e12
+            out[tag] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": round(achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
+                        "launches": len(recs), "avg_us": round(1e3 * tot_ms / len(recs), 2),
+                        "total_ms": round(tot_ms, 3), "algorithmic_per_launch": work / len(recs),
+                        "kernel": "gemm_kernel (fp32 MFMA 32x32x2)"}
+        else:
+            # bytes = 8 nnz + 4 (n_rows+1) + 4 d n_cols (X once) + 4 d n_rows (Y once [+ read if beta])
+            byts = 0.0
+            for nnz, nr, nc, nb, has_beta in (r[2] for r in recs):
+                d = 64 * nb
+                byts += 8.0 * nnz + 4.0 * (nr + 1) + 4.0 * d * nc + 4.0 * d * nr * (2 if has_beta else 1)
+            achieved = byts / (tot_ms * 1e-3) / 1e9
+            out[tag] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "launches": len(recs),
+                        "avg_us": round(1e3 * tot_ms / len(recs), 2), "total_ms": round(tot_ms, 3),
+                        "algorithmic_per_launch": byts / len(recs), "kernel": "spmm_seg_kernel (CSR, wave/segment)"}
+    return out
+
+
+def cpu_baseline(model, tl, budget_s=30.0):
+    """Oracle (torch-CPU restatement) timed on the host: one BPR step, one diffusion batch and one
+    p_sample batch at the baby shape, extrapolated to a full epoch (train users/s)."""
+    from oracle import graph_ref, model_ref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    U, I, B = model.n_users, model.n_items, 2048
+    N = U + I
+    s = model.rec_slab
+    p = {"uEmbeds": s.view("E0")[:U].cpu().clone().requires_grad_(True),
+         "iEmbeds": s.view("E0")[U:].cpu().clone().requires_grad_(True),
+         "image_trans": s.view("image_trans").cpu().clone().requires_grad_(True),
+         "text_trans": s.view("text_trans").cpu().clone().requires_grad_(True),
+         "modal_weight": s.view("modal_weight").cpu().clone().requires_grad_(True)}
+    feats = {"v": model.v_feat.cpu(), "t": model.t_feat.cpu()}
+    rows = np.repeat(np.arange(U), np.diff(tl.uptr_np))
+    adj = model_ref.sparse_from_csr(*graph_ref.norm_adj_csr(U, I, rows, tl.uitems_np), N)
+    rng = np.random.default_rng(0)
+    iadj = model_ref.sparse_from_csr(*graph_ref.ui_adj_csr(U, I, np.arange(U), rng.integers(0, I, U)), N)
+    tadj = model_ref.sparse_from_csr(*graph_ref.ui_adj_csr(U, I, np.arange(U), rng.integers(0, I, U)), N)
+    users = torch.as_tensor(rng.integers(0, U, B))
+    pos = torch.as_tensor(rng.integers(0, I, B))
+    neg = torch.as_tensor(rng.integers(0, I, B))
+    t0 = time.time()
+    loss = model_ref.rec_loss(p, feats, adj, iadj, tadj, users, pos, neg)
+    loss.backward()
+    t_bpr = time.time() - t0
+    den = model.denoise_model_image.slab
+    w = {"emb_W": den.view("emb_W").cpu(), "emb_b": den.view("emb_b").cpu(), "W1": den.view("W1").cpu().contiguous(),
+         "b1": den.view("b1").cpu(), "W2": den.view("W2").cpu().contiguous(), "b2": den.view("b2").cpu()}
+    w = {k: v.clone().requires_grad_(True) for k, v in w.items()}
+    tab = model_ref.diffmm_schedule()
+    x0 = torch.zeros(B, I)
+    for b in range(B):
+        x0[b, tl.uitems_np[tl.uptr_np[b]:tl.uptr_np[b + 1]]] = 1.0
+    ts = rng.integers(0, 5, B)
+    t0 = time.time()
+    diff, gc = model_ref.diffmm_training_losses(w, tab, x0, ts, torch.randn(B, I), (torch.rand(B, I) < 0.5).float(),
+                                                p["iEmbeds"].detach(), torch.randn(I, 64))
+    (diff.mean() + 0.5 * gc.mean()).backward()
+    t_dif = 2 * (time.time() - t0)  # image + text denoisers
+    t0 = time.time()
+    with torch.no_grad():
+        model_ref.diffmm_p_sample({k: v.detach() for k, v in w.items()}, tab, x0)
+    t_ps = 2 * (time.time() - t0)
+    n_bpr = -(-tl.n_inter // B)
+    n_dif = -(-U // B)
+    epoch = t_bpr * n_bpr + t_dif * n_dif + t_ps * n_dif
+    return {"value": round(U / epoch, 2), "unit": "users/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (torch-CPU fp32 restatement): 1 BPR+contrastive step (B=2048, fwd+bwd) = {t_bpr:.2f}s, "
+                      f"1 diffusion batch x2 denoisers = {t_dif:.2f}s, 1 p_sample batch x2 = {t_ps:.2f}s; "
+                      f"extrapolated to {n_bpr} BPR + {n_dif} diffusion + {n_dif} p_sample batches = {epoch:.1f}s/epoch"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--shape", default="baby")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eval-passes", type=int, default=3)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist = world > 1
+
+    def barrier():
+        if dist:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if not dist:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        return float(t.item())
+
+    from gmr import kernels as K
+
+    cfg, ds, tr, tl, vl, model, trainer = setup(args)
+    U = model.n_users
+
+    # warmup (the first warmup epoch is also probed to rank the kernel classes)
+    probe_all = None
+    for i in range(args.warmup):
+        if i == args.warmup - 1:
+            K.probe_begin(["gemm", "spmm"])
+        t0 = time.time()
+        trainer._train_epoch(tl, i)
+        torch.cuda.synchronize()
+        if i == args.warmup - 1:
+            probe_all = summarize_probe(K.probe_end())
+        log(f"warmup epoch {i}: {time.time() - t0:.3f}s")
+    dominant = max(probe_all, key=lambda k: probe_all[k]["total_ms"]) if probe_all else "gemm"
+
+    # timed epochs (live events around the dominant kernel class only)
+    K.probe_begin([dominant])
+    barrier()
+    t0 = time.time()
+    for i in range(args.steps):
+        trainer._train_epoch(tl, args.warmup + i)
+    barrier()
+    dt = max_over_ranks(time.time() - t0)
+    live = summarize_probe(K.probe_end())
+    train_ups = U * args.steps * world / dt
+
+    # full-rank evaluation passes (valid split)
+    trainer.evaluate(vl)
+    barrier()
+    t0 = time.time()
+    for _ in range(args.eval_passes):
+        res = trainer.evaluate(vl)
+    barrier()
+    et = max_over_ranks(time.time() - t0)
+    eval_ups = vl.pr_end * args.eval_passes * world / et
+
+    if rank == 0:
+        roof = live.get(dominant) or probe_all.get(dominant)
+        line = {
+            "metric": METRIC, "value": round(train_ups, 1), "unit": "users/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 2),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (Amazon-baby shape, SURVEY.md 8d recipe; random-init weights)",
+            "config": {"workload": f"DiffMM {args.shape}-shaped synthetic: {U} users x {model.n_items} items, "
+                                   f"{tl.n_inter} train interactions; step = one DiffMMTrainer epoch "
+                                   "(diffusion train + graph rebuild + BPR/contrastive)",
+                       "global_batch": cfg["train_batch_size"], "eval_batch": cfg["eval_batch_size"],
+                       "parallelism": f"replica{world}" if world > 1 else "single"},
+            "eval_users_per_s": round(eval_ups, 1), "eval_recall@20": res.get("recall@20"),
+            "roofline": roof, "roofline_by_kernel": probe_all, "dominant_kernel": dominant,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(model, tl)
+            except Exception as e:  # noqa: BLE001
+                line["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(line), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -617,3 +617,26 @@ extern "C" int gmr_sort_batch_keys(int64_t n_batches, const int32_t* keys, const
   GMR_LAUNCHED();
   return GMR_OK;
 }
+
+namespace {
+__global__ void sum_f64_kernel(int64_t n, const double* __restrict__ x, double scale, double* __restrict__ out,
+                               int accumulate) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) s += x[i];
+  s = gmr::wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double v = ((red[0] + red[1]) + (red[2] + red[3])) * scale;
+    out[0] = accumulate ? out[0] + v : v;
+  }
+}
+}  // namespace
+
+extern "C" int gmr_sum_f64(int64_t n, const double* x, double scale, double* out, int32_t accumulate, void* stream) {
+  GMR_ARG(x && out && n >= 0, "bad args");
+  hipLaunchKernelGGL(sum_f64_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n, x, scale, out, accumulate);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}

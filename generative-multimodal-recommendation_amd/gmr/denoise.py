@@ -1,0 +1,117 @@
+"""MLP denoiser of the Gaussian diffusion over interaction vectors, on flat slabs + HIP GEMMs.
+
+Reference: Denoise (models/diffmm.py:303-360) / DNN (models/diffrec.py:16-91), one hidden
+layer (dims = [H]):  h = tanh([drop(x), emb(t)] @ W1^T + b1);  out = h @ W2^T + b2.
+The time embedding takes only T values, so emb(t) @ W1[:, I:]^T + b1 is precomputed as a
+T x H table (gmr_diff_time_bias) and added by the first GEMM's epilogue.
+State-dict names follow the reference: emb_layer.{weight,bias}, in_layers.0.*, out_layers.0.*.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+from . import kernels as K
+from .kernels import ptr, stream
+from .slab import Slab
+
+
+def _r4(n):
+    return (n + 3) // 4 * 4
+
+
+class _Linear(nn.Module):
+    def __init__(self, weight, bias):
+        super().__init__()
+        self.weight = weight
+        self.bias = bias
+
+
+class Denoiser(nn.Module):
+    def __init__(self, n_items, hidden, emb_size, device, dropout=0.5, norm=False):
+        super().__init__()
+        if norm:
+            raise NotImplementedError("Denoise(norm=True) is not on the configured hot path")
+        I, H, E = n_items, hidden, emb_size
+        self.I, self.H, self.E = I, H, E
+        self.ld_w1 = _r4(I + E)
+        self.keep_prob = 1.0 - dropout
+        self.slab = Slab([("emb_W", (E, E), None), ("emb_b", (E,), None), ("W1", (H, I + E), self.ld_w1),
+                          ("b1", (H,), None), ("W2", (I, H), _r4(H)), ("b2", (I,), None)], device)
+        self.emb_layer = _Linear(self.slab.parameter("emb_W"), self.slab.parameter("emb_b"))
+        self.in_layers = nn.ModuleList([_Linear(self.slab.parameter("W1"), self.slab.parameter("b1"))])
+        self.out_layers = nn.ModuleList([_Linear(self.slab.parameter("W2"), self.slab.parameter("b2"))])
+        self.device = device
+        self._tb = None
+
+    @torch.no_grad()
+    def init_like_reference(self):
+        """Consume the CPU RNG exactly as the reference constructor does (nn.Linear default init,
+        then init_weights' normal_ draws, diffmm.py:311-338) and copy the result in."""
+        I, H, E = self.I, self.H, self.E
+        emb = nn.Linear(E, E)
+        lin_in = nn.Linear(I + E, H)
+        lin_out = nn.Linear(H, I)
+        nn.Dropout(1.0 - self.keep_prob)
+        for lay in (lin_in, lin_out, emb):
+            size = lay.weight.size()
+            lay.weight.data.normal_(0.0, float(np.sqrt(2.0 / (size[0] + size[1]))))
+            lay.bias.data.normal_(0.0, 0.001)
+        self.slab.load("emb_W", emb.weight)
+        self.slab.load("emb_b", emb.bias)
+        self.slab.load("W1", lin_in.weight)
+        self.slab.load("b1", lin_in.bias)
+        self.slab.load("W2", lin_out.weight)
+        self.slab.load("b2", lin_out.bias)
+
+    # ------------------------------------------------------------------ time table
+    def time_bias(self, T):
+        """EB[t] = emb_layer(temb(t)) @ W1[:, I:]^T + b1 for t < T (recomputed after each update)."""
+        if self._tb is None or self._tb[0].shape[0] != T:
+            self._tb = (torch.empty((T, self.H), device=self.device), torch.empty((T, self.E), device=self.device),
+                        torch.empty((T, self.E), device=self.device))
+        EB, temb, emb = self._tb
+        s = self.slab
+        _lib.call("gmr_diff_time_bias", T, self.E, ptr(s.view("emb_W")), ptr(s.view("emb_b")), ptr(s.view("W1")),
+                  self.ld_w1, self.I, ptr(s.view("b1")), self.H, ptr(EB), ptr(temb), ptr(emb), stream())
+        return self._tb
+
+    def W1x(self):
+        return self.slab.view("W1")[:, :self.I]
+
+    # ------------------------------------------------------------------ forward pieces
+    def hidden(self, x, h, EB, t_rows=None, t_const=None):
+        """h = tanh(x @ W1[:, :I]^T + EB[t])."""
+        if t_rows is not None:
+            K.gemm(x, self.W1x(), h, trans_b=True, epi=K.EPI_BIAS_TANH, bias=EB, bias_row=t_rows, ld_bias=self.H)
+        else:
+            K.gemm(x, self.W1x(), h, trans_b=True, epi=K.EPI_BIAS_TANH, bias=EB[t_const], ld_bias=0)
+        return h
+
+    def output(self, h, out):
+        """out = h @ W2^T + b2."""
+        K.gemm(h, self.slab.view("W2"), out, trans_b=True, epi=K.EPI_BIAS, bias=self.slab.view("b2"))
+        return out
+
+    def posterior_step(self, h, x, c1, c2):
+        """x <- c1 * (h @ W2^T + b2) + c2 * x (in place; GaussianDiffusion.p_mean_variance mean)."""
+        K.gemm(h, self.slab.view("W2"), x, trans_b=True, epi=K.EPI_POSTERIOR, bias=self.slab.view("b2"), aux=x,
+               slope=c1, beta=c2)
+        return x
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, x_in, h, dout, dpre, t_rows, T, S):
+        """Parameter gradients (written into the slab's grad buffer) from dout = dL/d out."""
+        s = self.slab
+        I = self.I
+        K.gemm(dout, h, s.gview("W2"), trans_a=True)                      # dW2 = dout^T h
+        K.colsum(dout, s.gview("b2"))                                     # db2
+        K.gemm(dout, s.view("W2"), dpre, epi=K.EPI_DTANH, aux=h)          # dpre = (dout W2) * (1 - h^2)
+        K.gemm(dpre, x_in, s.gview("W1")[:, :I], trans_a=True)             # dW1[:, :I] = dpre^T x_in
+        K.colsum(dpre, S, group=t_rows, n_groups=T)                       # S[t] = sum_{b: t_b = t} dpre[b]
+        EB, temb, emb = self._tb
+        _lib.call("gmr_diff_time_bwd", T, self.E, self.H, ptr(S), ptr(temb), ptr(emb), ptr(s.view("W1")), self.ld_w1,
+                  I, ptr(s.gview("W1")), ptr(s.gview("b1")), ptr(s.gview("emb_W")), ptr(s.gview("emb_b")), 0,
+                  stream())

@@ -14,6 +14,38 @@ EPI_NONE, EPI_BIAS, EPI_BIAS_TANH, EPI_LEAKY, EPI_POSTERIOR, EPI_DTANH, EPI_ROWS
 
 _ws = {}
 
+# ---------------------------------------------------------------- live per-kernel timing (bench.py)
+_probe = None
+
+
+def probe_begin(tags):
+    """Record HIP events around every launch whose tag is in `tags` (on the launching stream)."""
+    global _probe
+    _probe = {t: [] for t in tags}
+
+
+def probe_end():
+    global _probe
+    p, _probe = _probe, None
+    return p
+
+
+class _Probe:
+    def __init__(self, tag, meta):
+        self.rec = _probe.get(tag) if _probe is not None else None
+        self.meta = meta
+
+    def __enter__(self):
+        if self.rec is not None:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.e = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+
+    def __exit__(self, *a):
+        if self.rec is not None:
+            self.e.record()
+            self.rec.append((self.s, self.e, self.meta))
+
 
 def stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -45,6 +77,8 @@ def workspace(nfloats, device, tag="gemm"):
 
 
 def zero_(t):
+    if not t.is_contiguous():
+        raise ValueError("zero_ needs a contiguous tensor")
     _lib.call("gmr_zero", ptr(t), t.numel() * t.element_size(), stream())
     return t
 
@@ -63,10 +97,11 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
         if t.dtype != torch.float32:
             raise TypeError("gemm is fp32")
     ws = workspace(16 * M * N, C.device)
-    _lib.call("gmr_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), ptr(A), _ld(A), ptr(B), _ld(B),
-              float(beta), ptr(C), _ld(C), epi, ptr(bias), ptr(bias_row), ld_bias, ptr(aux),
-              _ld(aux) if aux is not None else 0, ptr(rv1), ptr(rv2), float(slope), tile, split_k, ptr(ws), ws.numel(),
-              stream())
+    with _Probe("gemm", (M, N, K)):
+        _lib.call("gmr_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), ptr(A), _ld(A), ptr(B), _ld(B),
+                  float(beta), ptr(C), _ld(C), epi, ptr(bias), ptr(bias_row), ld_bias, ptr(aux),
+                  _ld(aux) if aux is not None else 0, ptr(rv1), ptr(rv2), float(slope), tile, split_k, ptr(ws),
+                  ws.numel(), stream())
     return C
 
 
@@ -111,9 +146,10 @@ class CSR:
         for b in blocks:
             if b[0].shape[1] != 64 or (split != self.n_cols and b[1].shape[1] != 64):
                 raise ValueError("each block is 64 columns wide")
-        _lib.call("gmr_spmm_csr_f32", ptr(self.rowptr), ptr(self.col), ptr(self.val), self.n_rows, self.nnz,
-                  ptr(self.plan), self.seg_nnz, ptr(self.partial), nb, lo, ldl, hi, ldh, split, float(alpha),
-                  float(beta), ptr(out), _ld(out), stream())
+        with _Probe("spmm", (self.nnz, self.n_rows, self.n_cols, nb, beta != 0.0)):
+            _lib.call("gmr_spmm_csr_f32", ptr(self.rowptr), ptr(self.col), ptr(self.val), self.n_rows, self.nnz,
+                      ptr(self.plan), self.seg_nnz, ptr(self.partial), nb, lo, ldl, hi, ldh, split, float(alpha),
+                      float(beta), ptr(out), _ld(out), stream())
         return out
 
 

@@ -1,0 +1,243 @@
+"""Trainers — mirror common/trainer.py of the reference (Trainer :58-408, DiffMMTrainer :410-585).
+
+Same epoch structure, log lines, early stopping, checkpointing and return values as the
+reference; the per-step work runs through the fused HIP paths of the models:
+  * BPR phase: device-sampled epoch, one fused forward+backward per batch, flat-slab Adam;
+    the epoch loss is accumulated on the device and read once per epoch (the reference syncs
+    on loss.item() every batch; its NaN check therefore happens at epoch end here);
+  * DiffMM diffusion phase + graph rebuild: fused denoiser steps and device p_sample/top-k/CSR;
+  * evaluation: forward once per pass, then per eval batch score -> mask -> top-K on the device
+    and Recall/NDCG/Precision/MAP sums on the device.
+"""
+import itertools
+import os
+from logging import getLogger
+from time import time
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import kernels as K
+from .kernels import ptr, stream
+from .slab import FlatAdam
+from .topk_evaluator import TopKEvaluator
+from .utils import dict2str, early_stopping
+
+
+class Trainer:
+    def __init__(self, config, model, mg=False):
+        self.config = config
+        self.model = model
+        self.logger = getLogger()
+        self.learner = config["learner"]
+        self.learning_rate = config["learning_rate"]
+        self.epochs = config["epochs"]
+        self.eval_step = min(config["eval_step"], self.epochs)
+        self.stopping_step = config["stopping_step"]
+        self.clip_grad_norm = config["clip_grad_norm"]
+        if self.clip_grad_norm:
+            raise NotImplementedError("clip_grad_norm is unset in the hot-path configs")
+        self.valid_metric = config["valid_metric"].lower()
+        self.valid_metric_bigger = config["valid_metric_bigger"]
+        self.test_batch_size = config["eval_batch_size"]
+        self.device = config["device"]
+        wd = config["weight_decay"]
+        self.weight_decay = (eval(wd) if isinstance(wd, str) else wd) if wd is not None else 0.0
+        self.req_training = config["req_training"]
+        self.start_epoch = 0
+        self.cur_step = 0
+        zero = {f"{j.lower()}@{k}": 0.0 for j, k in itertools.product(config["metrics"], config["topk"])}
+        self.best_valid_score = -1
+        self.best_valid_result = zero
+        self.best_test_upon_valid = zero
+        self.train_loss_dict = {}
+        self.optimizer = self._build_optimizer()
+        sched = config["learning_rate_scheduler"] or [1.0, 50]
+        self.lr_factor = lambda e: sched[0] ** (e / sched[1])
+        self._sched_epoch = 0
+        self.evaluator = TopKEvaluator(config)
+        self.mg = mg
+        self._loss_acc = torch.zeros(2, dtype=torch.float32, device=self.device)
+
+    def _build_optimizer(self):
+        if (self.learner or "adam").lower() != "adam":
+            raise NotImplementedError(f"learner {self.learner}: the hot-path configs use adam")
+        return FlatAdam(self.model.optim_slabs(), lr=self.learning_rate, weight_decay=self.weight_decay)
+
+    # ------------------------------------------------------------------ training
+    def _train_epoch(self, train_data, epoch_idx, loss_func=None):
+        if not self.req_training:
+            return 0.0, []
+        self.model.train()
+        d = train_data.epoch()
+        acc = self._loss_acc
+        K.zero_(acc)
+        n = 0
+        for b, u, p, ng, pb, pc in train_data.batches(d):
+            loss = self.model.rec_step(u, p, ng, pb, pc)
+            _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
+            self.optimizer.step()
+            n += 1
+        total = float(acc[0].item())
+        if np.isnan(total):
+            self.logger.info("Loss is nan at epoch: {}. Exiting.".format(epoch_idx))
+            return torch.tensor(float("nan")), []
+        return total, []
+
+    def _generate_train_loss_output(self, epoch_idx, s_time, e_time, losses):
+        out = "epoch %d training [time: %.2fs, " % (epoch_idx, e_time - s_time)
+        if isinstance(losses, tuple):
+            out = ", ".join("train_loss%d: %.4f" % (i + 1, l) for i, l in enumerate(losses))
+        else:
+            out += "train loss: %.4f" % losses
+        return out + "]"
+
+    def _valid_epoch(self, valid_data, is_test=False):
+        res = self.evaluate(valid_data, is_test=is_test)
+        score = res[self.valid_metric] if self.valid_metric else res["NDCG@20"]
+        return score, res
+
+    def fit(self, train_data, valid_data=None, test_data=None, saved=False, verbose=True):
+        for epoch_idx in range(self.start_epoch, self.epochs):
+            t0 = time()
+            self.model.pre_epoch_processing()
+            train_loss, _ = self._train_epoch(train_data, epoch_idx)
+            if torch.is_tensor(train_loss):
+                break
+            self._sched_epoch += 1
+            self.optimizer.set_lr_factor(self.lr_factor(self._sched_epoch))
+            self.train_loss_dict[epoch_idx] = sum(train_loss) if isinstance(train_loss, tuple) else train_loss
+            t1 = time()
+            msg = self._generate_train_loss_output(epoch_idx, t0, t1, train_loss)
+            post = self.model.post_epoch_processing()
+            if verbose:
+                self.logger.info(msg)
+                if post is not None:
+                    self.logger.info(post)
+            if (epoch_idx + 1) % self.eval_step == 0:
+                v0 = time()
+                valid_score, valid_result = self._valid_epoch(valid_data)
+                self.best_valid_score, self.cur_step, stop_flag, update_flag = early_stopping(
+                    valid_score, self.best_valid_score, self.cur_step, max_step=self.stopping_step,
+                    bigger=self.valid_metric_bigger)
+                v1 = time()
+                _, test_result = self._valid_epoch(test_data, is_test=True)
+                if verbose:
+                    self.logger.info("epoch %d evaluating [time: %.2fs, valid_score: %f]" % (epoch_idx, v1 - v0,
+                                                                                            valid_score))
+                    self.logger.info("valid result: \n" + dict2str(valid_result))
+                    self.logger.info("test result: \n" + dict2str(test_result))
+                if update_flag:
+                    if verbose:
+                        self.logger.info("██ " + str(self.config["model"]) + "--Best validation results updated!!!")
+                    self.best_valid_result = valid_result
+                    self.best_test_upon_valid = test_result
+                    if saved:
+                        self._save_checkpoint(epoch_idx)
+                if stop_flag:
+                    if verbose:
+                        self.logger.info("+++++Finished training, best eval result in epoch %d" %
+                                         (epoch_idx - self.cur_step * self.eval_step))
+                    break
+        return self.best_valid_score, self.best_valid_result, self.best_test_upon_valid
+
+    def _save_checkpoint(self, epoch):
+        d = self.config["checkpoint_dir"] or "saved"
+        os.makedirs(d, exist_ok=True)
+        path = os.path.join(d, "{}-{}.pth".format(self.config["model"], self.config["dataset"]))
+        state = {"config": {k: v for k, v in self.config.final_config_dict.items() if k not in ("device",)},
+                 "epoch": epoch, "state_dict": {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
+                 "optimizer": self.optimizer.state_dict(), "best_valid_score": self.best_valid_score}
+        extra = getattr(self.model, "extra_state", None)
+        if callable(extra):
+            state["generated_graphs"] = extra()
+        torch.save(state, path)
+        self.logger.info("Saved best model to {}".format(path))
+
+    # ------------------------------------------------------------------ evaluation
+    @torch.no_grad()
+    def evaluate(self, eval_data, is_test=False, idx=0):
+        self.model.eval()
+        kmax = max(self.config["topk"])
+        topk = self.topk_all(eval_data, kmax)
+        return self.evaluator.evaluate_device(topk, eval_data, is_test=is_test, idx=idx)
+
+    @torch.no_grad()
+    def topk_all(self, eval_data, kmax):
+        """Top-k indices of every eval user (n_eval x k int32, device); reference trainer.py:369-388."""
+        d = eval_data.to_device()
+        n = eval_data.pr_end
+        E = eval_data.step
+        out = getattr(self, "_topk_buf", None)
+        if out is None or out.shape != (n, kmax):
+            out = torch.empty((n, kmax), dtype=torch.int32, device=self.device)
+            self._topk_buf = out
+        m = self.model
+        if hasattr(m, "forward_embeddings"):
+            usr, itm = m.forward_embeddings()  # identical for every batch of the pass (no_grad)
+            sb = getattr(self, "_score_buf", None)
+            if sb is None or sb.shape[0] < min(E, n):
+                sb = torch.empty((min(E, n), (m.n_items + 3) // 4 * 4), dtype=torch.float32, device=self.device)
+                self._score_buf = sb
+        mptr = d["mask_ptr"]
+        for lo in range(0, n, E):
+            hi = min(n, lo + E)
+            users = d["eval_u32"][lo:hi]
+            m0, m1 = int(mptr[lo]), int(mptr[hi])
+            rows = d["mask_rows"][m0:m1] - lo
+            cols = d["mask_cols"][m0:m1]
+            if hasattr(m, "forward_embeddings"):
+                m.topk_from_embeddings(usr, itm, users, rows, cols, kmax, out[lo:hi], sb)
+            else:
+                scores = m.full_sort_predict([users.long()])
+                K.mask_scores(scores, rows, cols)
+                K.topk_rows(scores, kmax, out[lo:hi])
+        return out
+
+
+class DiffMMTrainer(Trainer):
+    def __init__(self, config, model, mg=False):
+        super().__init__(config, model, mg)
+        lr = config["learning_rate"]
+        self.denoise_opt_image = FlatAdam([model.denoise_model_image.slab], lr=lr, weight_decay=0.0)
+        self.denoise_opt_text = FlatAdam([model.denoise_model_text.slab], lr=lr, weight_decay=0.0)
+        self.item_num, self.user_num = model.n_items, model.n_users
+        self._perm = torch.empty(self.user_num, dtype=torch.int32, device=self.device)
+        self._dloss = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self._epoch_ctr = 0
+
+    def diffusion_phase(self, epoch_idx):
+        """trainer.py:487-527 — train both denoisers over all users in shuffled batches."""
+        m = self.model
+        m.train()
+        B = self.config["train_batch_size"]
+        U = self.user_num
+        w = m._work(1)
+        m._project(w)                                         # image/text feats, detached (:501-502)
+        feats_i, feats_t = w["F"][:, :64], w["F"][:, 64:]
+        iE = m.rec_slab.view("E0")[U:]                        # getItemEmbeds().detach() (:496)
+        _lib.call("gmr_permutation", U, m.seed, 1000 + self._epoch_ctr, ptr(self._perm), stream())
+        K.zero_(self._dloss)
+        steps = 0
+        for bi, lo in enumerate(range(0, U, B)):
+            users = self._perm[lo:min(U, lo + B)]
+            nb = users.numel()
+            base = (self._epoch_ctr * 100000 + bi) * 2
+            for j, (den, feats) in enumerate(((m.denoise_model_image, feats_i), (m.denoise_model_text, feats_t))):
+                diff, gc = m.diffusion_step(den, users, feats, iE, base + j)
+                _lib.call("gmr_sum_f64", nb, ptr(diff), 1.0 / nb, ptr(self._dloss[j:j + 1]), 1, stream())
+                _lib.call("gmr_sum_f64", nb, ptr(gc), m.e_loss / nb, ptr(self._dloss[j:j + 1]), 1, stream())
+            self.denoise_opt_image.step()
+            self.denoise_opt_text.step()
+            steps += 1
+        self._epoch_ctr += 1
+        return steps
+
+    def _train_epoch(self, train_data, epoch_idx, loss_func=None):
+        steps = self.diffusion_phase(epoch_idx)
+        self.model.rebuild_ui_graphs()                      # trainer.py:529-576
+        rec_loss, batches = super()._train_epoch(train_data, epoch_idx)
+        dl = self._dloss.cpu().numpy() / max(steps, 1)
+        self.logger.info(f"Diffusion Loss: Image={dl[0]:.4f}, Text={dl[1]:.4f}")
+        return rec_loss, batches
