@@ -102,8 +102,10 @@ def test_diffusion_step_injected(model, golden):
     names = [("emb_W", "emb_layer_weight"), ("emb_b", "emb_layer_bias"), ("W1", "in_layers_0_weight"),
              ("b1", "in_layers_0_bias"), ("W2", "out_layers_0_weight"), ("b2", "out_layers_0_bias")]
     for ours, ref in names:
-        np.testing.assert_allclose(den.slab.gview(ours).cpu().numpy(), g["dif_grad_" + ref], rtol=2e-4, atol=1e-6,
-                                   err_msg=ours)
+        want = g["dif_grad_" + ref]
+        # fp32 sums over the batch: absolute tolerance relative to the tensor's scale
+        np.testing.assert_allclose(den.slab.gview(ours).cpu().numpy(), want, rtol=2e-4,
+                                   atol=2e-6 * max(1.0, float(np.abs(want).max())), err_msg=ours)
 
 
 def test_p_sample_and_top1(model, golden):
