@@ -398,21 +398,31 @@ __global__ void sum_kernel(int64_t n, const float* __restrict__ x, float scale, 
   }
 }
 
-// squared Frobenius norm -> single value (deterministic, one block of 1024)
-__global__ void sqnorm_kernel(int64_t n, const float* __restrict__ x, float scale, float* __restrict__ out, int accumulate) {
-  __shared__ double red[16];
+// squared Frobenius norm: per-block fp64 partials (grid-stride) then one ordered sum
+__global__ void __launch_bounds__(256) sqnorm_part_kernel(int64_t n, const float* __restrict__ x,
+                                                          double* __restrict__ part) {
+  __shared__ double red[4];
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += 1024) {
-    double v = x[i];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double v = x[i];
     s += v * v;
   }
   s = gmr::wave_sum_d(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void sqnorm_fin_kernel(int nparts, const double* __restrict__ part, float scale, float* __restrict__ out,
+                                  int accumulate) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
+  s = gmr::wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    double t = 0;
-    for (int i = 0; i < 16; ++i) t += red[i];
-    float v = (float)(t * (double)scale);
+    const float v = (float)(((red[0] + red[1]) + (red[2] + red[3])) * (double)scale);
     out[0] = accumulate ? out[0] + v : v;
   }
 }
@@ -600,9 +610,14 @@ extern "C" int gmr_sum_f32(int64_t n, const float* x, float scale, float* out, i
   return GMR_OK;
 }
 
-extern "C" int gmr_sqnorm_f32(int64_t n, const float* x, float scale, float* out, int32_t accumulate, void* stream) {
-  GMR_ARG(x && out && n >= 0, "bad args");
-  hipLaunchKernelGGL(sqnorm_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, n, x, scale, out, accumulate);
+extern "C" int gmr_sqnorm_f32(int64_t n, const float* x, float scale, float* out, int32_t accumulate,
+                              double* workspace, void* stream) {
+  GMR_ARG(x && out && workspace && n >= 0, "bad args");
+  const int g = gmr::grid_for(n, 256 * 8, GMR_SQNORM_PARTS);
+  hipLaunchKernelGGL(sqnorm_part_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, n, x, workspace);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(sqnorm_fin_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, g, workspace, scale, out,
+                     accumulate);
   GMR_LAUNCHED();
   return GMR_OK;
 }

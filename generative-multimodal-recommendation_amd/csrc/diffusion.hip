@@ -207,10 +207,43 @@ __global__ void gc_rows_kernel(int B, const int* __restrict__ users, const int* 
   if (lane == 0) gc_out[b] = (double)s / 64.0;
 }
 
-// deterministic column sums: out[c] (+)= sum_r x[r][c]; 64 columns per block, rows split over 4 waves
-__global__ void __launch_bounds__(256) colsum_kernel(int64_t rows, int64_t cols, const float* __restrict__ x, int64_t ld,
-                                                     const int* __restrict__ group, int n_groups,
-                                                     float* __restrict__ out, int accumulate) {
+// deterministic column sums: out[g][c] (+)= sum_{r: group[r] == g} x[r][c].
+// One block = 64 columns x 16 waves; wave w takes rows w, w+16, ...; each lane keeps the sums of
+// up to GMAX groups in registers; waves are combined in a fixed order through LDS.
+template <int GMAX>
+__global__ void __launch_bounds__(1024) colsum_kernel(int64_t rows, int64_t cols, const float* __restrict__ x,
+                                                      int64_t ld, const int* __restrict__ group, int n_groups,
+                                                      float* __restrict__ out, int accumulate) {
+  __shared__ float red[16][GMAX][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  float s[GMAX];
+#pragma unroll
+  for (int q = 0; q < GMAX; ++q) s[q] = 0.f;
+  if (c < cols) {
+#pragma unroll 4
+    for (int64_t r = w; r < rows; r += 16) {
+      const float v = x[r * ld + c];
+      const int gr = group ? group[r] : 0;
+#pragma unroll
+      for (int q = 0; q < GMAX; ++q) s[q] += (gr == q) ? v : 0.f;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < GMAX; ++q) red[w][q][lane] = s[q];
+  __syncthreads();
+  if (w < n_groups && w < GMAX && c < cols) {
+    float v = 0.f;
+    for (int k = 0; k < 16; ++k) v += red[k][w][lane];
+    float* o = out + (int64_t)w * cols + c;
+    *o = accumulate ? *o + v : v;
+  }
+}
+
+// generic fallback (many groups): one group per blockIdx.y
+__global__ void __launch_bounds__(256) colsum_grouped_kernel(int64_t rows, int64_t cols, const float* __restrict__ x,
+                                                             int64_t ld, const int* __restrict__ group,
+                                                             float* __restrict__ out, int accumulate) {
   __shared__ float red[4][64];
   const int64_t c = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
   const int w = threadIdx.x >> 6;
@@ -218,7 +251,7 @@ __global__ void __launch_bounds__(256) colsum_kernel(int64_t rows, int64_t cols,
   float s = 0.f;
   if (c < cols)
     for (int64_t r = w; r < rows; r += 4)
-      if (!group || group[r] == g) s += x[r * ld + c];
+      if (group[r] == g) s += x[r * ld + c];
   red[w][threadIdx.x & 63] = s;
   __syncthreads();
   if (w == 0 && c < cols) {
@@ -247,36 +280,32 @@ __global__ void time_bwd_h_kernel(int T, int E, int H, const float* __restrict__
   }
 }
 
-__global__ void time_bwd_e_kernel(int T, int E, int H, const float* __restrict__ S, const float* __restrict__ W1,
-                                  int64_t ldw, int64_t off, const float* __restrict__ temb, float* __restrict__ dembW,
-                                  float* __restrict__ dembB, int accumulate) {
-  // single block of 64 threads: thread i handles output row i of emb_W
-  __shared__ float demb[64][64];  // [t][j], T <= 64 handled in chunks of 64 timesteps
-  const int i = threadIdx.x;
-  float accW[64];
-  for (int j = 0; j < E; ++j) accW[j] = 0.f;
-  float accB = 0.f;
-  for (int t0 = 0; t0 < T; t0 += 64) {
-    const int tn = min(64, T - t0);
-    // demb[t][j] for the chunk: thread i computes column j = i for every t
-    if (i < E)
-      for (int tt = 0; tt < tn; ++tt) {
-        float a = 0.f;
-        for (int h = 0; h < H; ++h) a = fmaf(S[(int64_t)(t0 + tt) * H + h], W1[(int64_t)h * ldw + off + i], a);
-        demb[tt][i] = a;
-      }
-    __syncthreads();
-    if (i < E)
-      for (int tt = 0; tt < tn; ++tt) {
-        const float d = demb[tt][i];
-        accB += d;
-        for (int j = 0; j < E; ++j) accW[j] = fmaf(d, temb[(t0 + tt) * E + j], accW[j]);
-      }
-    __syncthreads();
+// demb[t][i] = sum_h S[t][h] W1[h][off+i] by 16 waves (one output per wave at a time, lanes over h),
+// then d emb_W[i][j] = sum_t demb[t][i] temb[t][j], d emb_b[i] = sum_t demb[t][i]
+__global__ void __launch_bounds__(1024) time_bwd_e_kernel(int T, int E, int H, const float* __restrict__ S,
+                                                          const float* __restrict__ W1, int64_t ldw, int64_t off,
+                                                          const float* __restrict__ temb, float* __restrict__ dembW,
+                                                          float* __restrict__ dembB, int accumulate) {
+  extern __shared__ __attribute__((aligned(16))) float demb[];  // T * E
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int o = w; o < T * E; o += 16) {
+    const int t = o / E, i = o % E;
+    float a = 0.f;
+    for (int h = lane; h < H; h += 64) a = fmaf(S[(int64_t)t * H + h], W1[(int64_t)h * ldw + off + i], a);
+    a = gmr::wave_sum(a);
+    if (lane == 0) demb[o] = a;
   }
-  if (i < E) {
-    for (int j = 0; j < E; ++j) dembW[i * E + j] = accumulate ? dembW[i * E + j] + accW[j] : accW[j];
-    dembB[i] = accumulate ? dembB[i] + accB : accB;
+  __syncthreads();
+  for (int o = threadIdx.x; o < E * E; o += 1024) {
+    const int i = o / E, j = o % E;
+    float a = 0.f;
+    for (int t = 0; t < T; ++t) a = fmaf(demb[t * E + i], temb[t * E + j], a);
+    dembW[o] = accumulate ? dembW[o] + a : a;
+  }
+  for (int i = threadIdx.x; i < E; i += 1024) {
+    float a = 0.f;
+    for (int t = 0; t < T; ++t) a += demb[t * E + i];
+    dembB[i] = accumulate ? dembB[i] + a : a;
   }
 }
 
@@ -355,9 +384,17 @@ extern "C" int gmr_diff_gc_rows(int32_t B, const int32_t* users, const int32_t* 
 extern "C" int gmr_colsum_f32(int64_t rows, int64_t cols, const float* x, int64_t ld, const int32_t* group,
                               int32_t n_groups, float* out, int32_t accumulate, void* stream) {
   GMR_ARG(x && out && rows > 0 && cols > 0 && n_groups >= 1, "bad args");
-  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)n_groups);
-  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, x, ld, group, n_groups, out,
-                     accumulate);
+  GMR_ARG(n_groups == 1 || group, "groups need a group array");
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned gx = (unsigned)((cols + 63) / 64);
+  if (n_groups == 1)
+    hipLaunchKernelGGL(colsum_kernel<1>, dim3(gx), dim3(1024), 0, st, rows, cols, x, ld, group, 1, out, accumulate);
+  else if (n_groups <= 8)
+    hipLaunchKernelGGL(colsum_kernel<8>, dim3(gx), dim3(1024), 0, st, rows, cols, x, ld, group, n_groups, out,
+                       accumulate);
+  else
+    hipLaunchKernelGGL(colsum_grouped_kernel, dim3(gx, (unsigned)n_groups), dim3(256), 0, st, rows, cols, x, ld, group,
+                       out, accumulate);
   GMR_LAUNCHED();
   return GMR_OK;
 }
@@ -371,8 +408,9 @@ extern "C" int gmr_diff_time_bwd(int32_t T, int32_t E, int32_t H, const float* S
   hipLaunchKernelGGL(time_bwd_h_kernel, dim3(gmr::grid_for(H, 256)), dim3(256), 0, st, T, E, H, S, emb, dW1, ld_w1,
                      col_off, db1, accumulate);
   GMR_LAUNCHED();
-  hipLaunchKernelGGL(time_bwd_e_kernel, dim3(1), dim3(64), 0, st, T, E, H, S, W1, ld_w1, col_off, temb, d_emb_W, d_emb_b,
-                     accumulate);
+  GMR_ARG((size_t)T * E * sizeof(float) <= 60000, "T * E too large for the LDS staging");
+  hipLaunchKernelGGL(time_bwd_e_kernel, dim3(1), dim3(1024), sizeof(float) * (size_t)T * E, st, T, E, H, S, W1, ld_w1,
+                     col_off, temb, d_emb_W, d_emb_b, accumulate);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -146,6 +146,9 @@ __global__ void __launch_bounds__(256) spmm_seg_kernel(const int* __restrict__ c
   const int64_t ldl = src.ld_lo[blk], ldh = src.ld_hi[blk];
   const int64_t split = src.split;
 
+  // UNR neighbour rows per lane group in flight: the loads of one batch are independent and
+  // issued back to back (masked entries read row 0 with weight 0: always a valid address).
+  constexpr int UNR = 8;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int base = beg; base < end; base += 64) {
     const int e = base + lane;
@@ -156,16 +159,22 @@ __global__ void __launch_bounds__(256) spmm_seg_kernel(const int* __restrict__ c
       my_v = val[e];
     }
     const int cnt = min(64, end - base);
-    for (int j = 0; j < 64; j += G) {
-      if (j >= cnt) break;
-      const int k = j + g;
-      const int c = __shfl(my_c, k);
-      const float v = __shfl(my_v, k);
-      if (k < cnt) {
-        const float* p = c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh;
-        const float4 x = *reinterpret_cast<const float4*>(p + c4);
-        acc = gmr::f4_fma(v, x, acc);
+    for (int j = 0; j < cnt; j += UNR * G) {
+      float4 xs[UNR];
+      float vs[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int k = j + u * G + g;
+        const int c = __shfl(my_c, k & 63);
+        const float v = __shfl(my_v, k & 63);
+        const bool ok = k < cnt;
+        const int cc = ok ? c : 0;
+        const float* p = cc < split ? lo + (int64_t)cc * ldl : hi + (int64_t)(cc - split) * ldh;
+        xs[u] = *reinterpret_cast<const float4*>(p + c4);
+        vs[u] = ok ? v : 0.f;
       }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) acc = gmr::f4_fma(vs[u], xs[u], acc);
     }
   }
 #pragma unroll
@@ -196,7 +205,15 @@ __global__ void __launch_bounds__(256) spmm_fix_kernel(PlanView pv, float alpha,
   const int c = (int)(gid % TPR) * 4;
   const int row = pv.fix_row[f], first = pv.fix_first[f], cnt = pv.fix_cnt[f];
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int j = 0; j < cnt; ++j) acc = gmr::f4_add(acc, *reinterpret_cast<const float4*>(partial + (int64_t)(first + j) * D + c));
+  int j = 0;
+  for (; j + 8 <= cnt; j += 8) {  // 8 independent partial rows in flight, summed in segment order
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(partial + (int64_t)(first + j + u) * D + c);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = gmr::f4_add(acc, v[u]);
+  }
+  for (; j < cnt; ++j) acc = gmr::f4_add(acc, *reinterpret_cast<const float4*>(partial + (int64_t)(first + j) * D + c));
   float* yp = y + (int64_t)row * ldy + c;
   float4 o = gmr::f4_scale(alpha, acc);
   if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);

@@ -127,6 +127,34 @@ __global__ void __launch_bounds__(TK_THREADS) topk_rows_kernel(int64_t n_rows, i
   }
 }
 
+// k == 1: single pass arg-max per row, ties -> lowest index
+__global__ void __launch_bounds__(256) argmax_rows_kernel(int64_t n_rows, int64_t n_cols, const float* __restrict__ S,
+                                                          int64_t ld, int* __restrict__ out_idx, int64_t ld_idx,
+                                                          float* __restrict__ out_val) {
+  __shared__ unsigned long long red[4];
+  const int64_t row = blockIdx.x;
+  const float* p = S + row * ld;
+  unsigned long long best = ~0ull;  // ascending order on (~key, idx)
+  for (int64_t j = threadIdx.x; j < n_cols; j += 256) {
+    const unsigned long long e = ((unsigned long long)(~fkey(p[j])) << 32) | (uint32_t)j;
+    best = e < best ? e : best;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    unsigned long long o = __shfl_xor(best, m);
+    best = o < best ? o : best;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = red[0];
+    for (int i = 1; i < 4; ++i) b = red[i] < b ? red[i] : b;
+    const int j = (int)(uint32_t)(b & 0xFFFFFFFFull);
+    out_idx[row * ld_idx] = j;
+    if (out_val) out_val[row * ld_idx] = p[j];
+  }
+}
+
 // One thread per user.  ks = {5, 10, 20, 50} (any ascending list <= K, up to 8).
 // sums layout: [metric][k] with metric 0 recall, 1 ndcg, 2 precision, 3 map; per-block partials.
 __global__ void __launch_bounds__(256) metrics_kernel(int64_t n_users, const int* __restrict__ topk, int64_t ld_topk,
@@ -213,8 +241,12 @@ extern "C" int gmr_topk_rows_f32(int64_t n_rows, int64_t n_cols, const float* sc
   GMR_ARG(k >= 1 && k <= 64 && k <= n_cols, "k must be in [1, min(64, n_cols)]");
   GMR_ARG((n_cols + TK_THREADS - 1) / TK_THREADS < 32768, "n_cols too large");
   GMR_ARG(n_rows < (1ll << 31), "too many rows");
-  hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)n_rows), dim3(TK_THREADS), 0, (hipStream_t)stream, n_rows, n_cols,
-                     scores, ld, k, out_idx, ld_idx, out_val);
+  if (k == 1)
+    hipLaunchKernelGGL(argmax_rows_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, n_rows, n_cols,
+                       scores, ld, out_idx, ld_idx, out_val);
+  else
+    hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)n_rows), dim3(TK_THREADS), 0, (hipStream_t)stream, n_rows,
+                       n_cols, scores, ld, k, out_idx, ld_idx, out_val);
   GMR_LAUNCHED();
   return GMR_OK;
 }

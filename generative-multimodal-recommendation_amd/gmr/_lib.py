@@ -52,7 +52,7 @@ SIGNATURES = {
     "gmr_scatter_sorted_f32": (I32, [I32, I32, P, P, I64, P, I64, P]),
     "gmr_sort_batch_keys": (I32, [I64, P, P, P, I32, I64, P, I64, I32, P]),
     "gmr_sum_f32": (I32, [I64, P, F32, P, I32, P]),
-    "gmr_sqnorm_f32": (I32, [I64, P, F32, P, I32, P]),
+    "gmr_sqnorm_f32": (I32, [I64, P, F32, P, I32, P, P]),
     "gmr_sum_f64": (I32, [I64, P, F64, P, I32, P]),
     "gmr_colsum_f32": (I32, [I64, I64, P, I64, P, I32, P, I32, P]),
     "gmr_sample_epoch": (I32, [I64, P, P, P, P, P, I64, U64, U64, P, P, P, P]),

@@ -159,7 +159,8 @@ class DiffMM(GeneralRecommender):
              "partials": f(int(_lib.load().gmr_dmm_final_bwd_partials(N))),
              "logits": f(B, (nt + 3) // 4 * 4), "lse": f(B), "P1": f(B, 64),
              "contrib_bpr": f(3 * B, 64), "contrib_cl": f(2 * B, 128),
-             "loss_bpr": f(B), "loss_cu": f(B), "loss_ci": f(B), "loss": f(4)}
+             "loss_bpr": f(B), "loss_cu": f(B), "loss_ci": f(B), "loss": f(4),
+             "sqws": torch.empty(1024, dtype=torch.float64, device=dev)}
         self._w = w
         return w
 
@@ -241,7 +242,7 @@ class DiffMM(GeneralRecommender):
         self._contrast(w, pos, U, I, B, w["loss_ci"], B)
         loss = w["loss"][:1]
         _lib.call("gmr_sum_f32", B, ptr(w["loss_bpr"]), 1.0 / B, ptr(loss), 0, stream())
-        _lib.call("gmr_sqnorm_f32", N * 64, ptr(E0), self.reg_weight, ptr(loss), 1, stream())
+        _lib.call("gmr_sqnorm_f32", N * 64, ptr(E0), self.reg_weight, ptr(loss), 1, ptr(w["sqws"]), stream())
         _lib.call("gmr_sum_f32", B, ptr(w["loss_cu"]), self.ssl_reg / B, ptr(loss), 1, stream())
         _lib.call("gmr_sum_f32", B, ptr(w["loss_ci"]), self.ssl_reg / B, ptr(loss), 1, stream())
         # --- backward

@@ -109,7 +109,7 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
 class CSR:
     """Device CSR (int32 rowptr/col, fp32 val) of an n x n matrix with its SpMM work plan."""
 
-    def __init__(self, rowptr, col, val, n_cols=None, seg_nnz=256, symmetric=True):
+    def __init__(self, rowptr, col, val, n_cols=None, seg_nnz=128, symmetric=True):
         self.rowptr, self.col, self.val = rowptr, col, val
         self.n_rows = rowptr.numel() - 1
         self.n_cols = self.n_rows if n_cols is None else n_cols
@@ -153,7 +153,7 @@ class CSR:
         return out
 
 
-def bipartite_symnorm(n_users, n_items, user_ptr, user_items, self_loops, deg_eps, seg_nnz=256):
+def bipartite_symnorm(n_users, n_items, user_ptr, user_items, self_loops, deg_eps, seg_nnz=128):
     """Build the normalised (U+I)^2 bipartite adjacency on the device (graph.hip)."""
     lib = _lib.load()
     dev = user_ptr.device

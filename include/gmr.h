@@ -131,7 +131,9 @@ int gmr_sort_batch_keys(int64_t n_batches, const int32_t* keys, const int64_t* o
                         void* stream);
 /* deterministic reductions */
 int gmr_sum_f32(int64_t n, const float* x, float scale, float* out, int32_t accumulate, void* stream);
-int gmr_sqnorm_f32(int64_t n, const float* x, float scale, float* out, int32_t accumulate, void* stream);
+#define GMR_SQNORM_PARTS 1024 /* workspace doubles of gmr_sqnorm_f32 */
+int gmr_sqnorm_f32(int64_t n, const float* x, float scale, float* out, int32_t accumulate, double* workspace,
+                   void* stream);
 int gmr_sum_f64(int64_t n, const double* x, double scale, double* out, int32_t accumulate, void* stream);
 int gmr_colsum_f32(int64_t rows, int64_t cols, const float* x, int64_t ld, const int32_t* group, int32_t n_groups,
                    float* out, int32_t accumulate, void* stream);
