@@ -66,9 +66,10 @@ __device__ __forceinline__ float epi_apply(const Epi& e, float acc, int64_t m, i
 // Loads a BK-deep tile slice of an operand into registers (float4 granules).
 // KC: operand stored [rows][k] (k contiguous), tile = R rows x BK.
 // MC: operand stored [k][rows] (rows contiguous), tile = BK x R.
-template <int R, bool KC, bool VEC>
+template <int R, bool KC, bool VEC, int NT>
 struct Stage {
-  static constexpr int N4 = R * BK / 4 / 256;  // float4 per thread
+  static constexpr int N4 = R * BK / 4 / NT;  // float4 per thread
+  static_assert(N4 * NT * 4 == R * BK, "tile rows x BK must split evenly over the block");
   float4 r[N4];
 
   __device__ __forceinline__ void load(const float* __restrict__ p, int64_t ld, int64_t r0, int64_t nrows,
@@ -76,7 +77,7 @@ struct Stage {
     const int t = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < N4; ++i) {
-      const int idx = t + 256 * i;
+      const int idx = t + NT * i;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (KC) {
         const int rr = idx / (BK / 4), k4 = (idx % (BK / 4)) * 4;
@@ -119,7 +120,7 @@ struct Stage {
     const int t = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < N4; ++i) {
-      const int idx = t + 256 * i;
+      const int idx = t + NT * i;
       if (KC) {
         const int rr = idx / (BK / 4), k4 = (idx % (BK / 4)) * 4;
         *reinterpret_cast<float4*>(s + rr * LD + k4) = r[i];
@@ -142,14 +143,17 @@ __device__ __forceinline__ float4 frag4(const float* s, int row, int h, int q) {
   }
 }
 
-template <int BM, int BN, bool AKC, bool BKC, bool VEC>
-__global__ void __launch_bounds__(256) gemm_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
-                                                   int64_t lda, const float* __restrict__ B, int64_t ldb,
-                                                   float* __restrict__ C, int64_t ldc, Epi epi, int tiles_n,
-                                                   int64_t k_per_split, float* __restrict__ ws) {
-  constexpr int TM = BM / 64, TN = BN / 64;
-  using SA = Stage<BM, AKC, VEC>;
-  using SB = Stage<BN, BKC, VEC>;
+template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, bool VEC>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t N, int64_t K,
+                                                             const float* __restrict__ A, int64_t lda,
+                                                             const float* __restrict__ B, int64_t ldb,
+                                                             float* __restrict__ C, int64_t ldc, Epi epi, int tiles_n,
+                                                             int64_t k_per_split, float* __restrict__ ws) {
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;  // wave tile
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  using SA = Stage<BM, AKC, VEC, NT>;
+  using SB = Stage<BN, BKC, VEC, NT>;
   __shared__ __attribute__((aligned(16))) float smem[2 * (SA::WORDS + SB::WORDS)];
   constexpr int STAGE_WORDS = SA::WORDS + SB::WORDS;
 
@@ -165,7 +169,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(int64_t M, int64_t N, int64_t
 
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WGN, wn = w % WGN;
   const int h = lane >> 5, l32 = lane & 31;
 
   floatx16 acc[TM][TN];
@@ -198,9 +202,9 @@ __global__ void __launch_bounds__(256) gemm_kernel(int64_t M, int64_t N, int64_t
     for (int qq = 0; qq < 4; ++qq) {
       float4 fa[TM], fb[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = frag4<AKC, SA::LD>(a_s, wm * (BM / 2) + i * 32 + l32, h, qq);
+      for (int i = 0; i < TM; ++i) fa[i] = frag4<AKC, SA::LD>(a_s, wm * WTM + i * 32 + l32, h, qq);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = frag4<BKC, SB::LD>(b_s, wn * (BN / 2) + j * 32 + l32, h, qq);
+      for (int j = 0; j < TN; ++j) fb[j] = frag4<BKC, SB::LD>(b_s, wn * WTN + j * 32 + l32, h, qq);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -224,11 +228,11 @@ __global__ void __launch_bounds__(256) gemm_kernel(int64_t M, int64_t N, int64_t
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int64_t n = n0 + wn * (BN / 2) + j * 32 + l32;
+      const int64_t n = n0 + wn * WTN + j * 32 + l32;
       if (n >= N) continue;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int64_t m = m0 + wm * (BM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int64_t m = m0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (m >= M) continue;
         if (ws) {
           ws[((int64_t)blockIdx.z * M + m) * N + n] = acc[i][j][e];
@@ -251,27 +255,32 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const flo
   *cp = epi_apply(epi, s, m, n, cp);
 }
 
-template <int BM, int BN, bool AKC, bool BKC>
+template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC>
 void launch_t(bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
               const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n, int64_t kps,
               float* ws) {
+  const dim3 blk(64 * WGM * WGN);
   if (vec)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AKC, BKC, true>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc,
-                       epi, tiles_n, kps, ws);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, AKC, BKC, true>), grid, blk, 0, st, M, N, K, A, lda, B, ldb, C,
+                       ldc, epi, tiles_n, kps, ws);
   else
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AKC, BKC, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc,
-                       epi, tiles_n, kps, ws);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, AKC, BKC, false>), grid, blk, 0, st, M, N, K, A, lda, B, ldb, C,
+                       ldc, epi, tiles_n, kps, ws);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WGM, int WGN>
 void launch_tile(int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A,
                  int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n,
                  int64_t kps, float* ws) {
   // AKC = A is k-contiguous (not transposed); BKC = B is k-contiguous (transposed)
-  if (!ta && tb) launch_t<BM, BN, true, true>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
-  else if (!ta && !tb) launch_t<BM, BN, true, false>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
-  else if (ta && !tb) launch_t<BM, BN, false, false>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
-  else launch_t<BM, BN, false, true>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+  if (!ta && tb)
+    launch_t<BM, BN, WGM, WGN, true, true>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+  else if (!ta && !tb)
+    launch_t<BM, BN, WGM, WGN, true, false>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+  else if (ta && !tb)
+    launch_t<BM, BN, WGM, WGN, false, false>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+  else
+    launch_t<BM, BN, WGM, WGN, false, true>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
 }
 
 }  // namespace
@@ -294,7 +303,8 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   GMR_ARG(!(epilogue == GMR_EPI_POSTERIOR || epilogue == GMR_EPI_DTANH || epilogue == GMR_EPI_ROWSCALE_AUX) || aux,
           "epilogue needs aux");
   GMR_ARG(epilogue != GMR_EPI_ROWSCALE_AUX || rowvec1, "epilogue needs rowvec1");
-  GMR_ARG(tile == 0 || tile == 64 || tile == 128, "tile must be 0 (auto), 64 or 128");
+  GMR_ARG(tile == 0 || tile == 64 || tile == 128 || tile == 256 || tile == 256128 || tile == 128256,
+          "tile must be 0 (auto), 64, 128, 256, 256128 or 128256");
   Epi e;
   e.kind = epilogue;
   e.alpha = alpha;
@@ -309,10 +319,17 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   e.rv2 = rowvec2;
   const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
   if (tile == 0) {
-    int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128);
-    tile = (t128 >= 512) ? 128 : 64;
+    // measured on MI355X (scripts/gemm_bench.py): 256^2 tiles win the long-K products of the
+    // denoiser (M >= 2048, N >= 1000, K >= 4096; one 16-wave block per CU), 128^2 the wide
+    // K ~ 1000 ones, 64^2 (with split-K) the skinny N = 64 / K = 64 products and the TN updates.
+    const bool tn = trans_a && !trans_b;
+    if (!tn && M >= 2048 && N >= 1000 && K >= 4096) tile = 256;
+    else if (!tn && M * N >= (int64_t)8 << 20 && K >= 512) tile = 128;
+    else tile = 64;
   }
-  const int64_t tm = (M + tile - 1) / tile, tn = (N + tile - 1) / tile;
+  const int bm = tile == 256128 ? 256 : tile == 128256 ? 128 : tile;
+  const int bn = tile == 256128 ? 128 : tile == 128256 ? 256 : tile;
+  const int64_t tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
   GMR_ARG(tm * tn < (1ll << 31), "too many tiles");
   int splits = split_k;
   if (splits <= 0) {  // auto: aim for >= 512 workgroups on 256 CUs
@@ -329,10 +346,22 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   }
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)(tm * tn), 1, (unsigned)splits);
-  if (tile == 128)
-    launch_tile<128, 128>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
-  else
-    launch_tile<64, 64>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+  switch (tile) {
+    case 256:
+      launch_tile<256, 256, 4, 4>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      break;
+    case 256128:
+      launch_tile<256, 128, 4, 2>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      break;
+    case 128256:
+      launch_tile<128, 256, 2, 4>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      break;
+    case 128:
+      launch_tile<128, 128, 2, 2>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      break;
+    default:
+      launch_tile<64, 64, 2, 2>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+  }
   GMR_LAUNCHED();
   if (ws) {
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gmr::grid_for(M * N, 256)), dim3(256), 0, st, M, N, splits, ws, C,

@@ -1,0 +1,69 @@
+"""Per-shape timing of gmr_gemm_f32 on the DiffMM-baby GEMM shapes (HIP events, 1 process).
+
+python scripts/gemm_bench.py [--tiles 0,64,128] [--reps 20]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "generative-multimodal-recommendation_amd"))
+
+import torch  # noqa: E402
+
+from gmr import kernels as K  # noqa: E402
+
+# name, M, N, K, trans_a, trans_b, calls per epoch
+SHAPES = [
+    ("psample_h (NT)", 8192, 1000, 7050, 0, 1, 30),
+    ("psample_out (NT)", 8192, 7050, 1000, 0, 1, 30),
+    ("train_h (NT)", 2048, 1000, 7050, 0, 1, 20),
+    ("train_out (NT)", 2048, 7050, 1000, 0, 1, 20),
+    ("train_Z (NN,N=64)", 2048, 64, 7050, 0, 0, 20),
+    ("dout+=G f^T (NT,K=64)", 2048, 7050, 64, 0, 1, 20),
+    ("dW2 (TN)", 7050, 1000, 2048, 1, 0, 20),
+    ("dh (NN)", 2048, 1000, 7050, 0, 0, 20),
+    ("dW1 (TN)", 1000, 7050, 2048, 1, 0, 20),
+    ("cl_logits_u (NT,K=64)", 2048, 19445, 64, 0, 1, 60),
+    ("cl_dp1_u (NN,N=64)", 2048, 64, 19445, 0, 0, 60),
+    ("cl_dtab_u (TN,N=64)", 19445, 64, 2048, 1, 0, 60),
+    ("proj_v (NN,N=64)", 7050, 64, 4096, 0, 0, 60),
+    ("proj_v_grad (TN,N=64)", 4096, 64, 7050, 1, 0, 60),
+    ("eval_scores (NT,K=64)", 4096, 7050, 64, 0, 1, 5),
+]
+
+
+def run(args):
+    torch.manual_seed(0)
+    dev = "cuda"
+    tot_ms = 0.0
+    print(f"{'shape':26s} {'tile':>4s} {'us':>9s} {'TF/s':>7s} {'ms/epoch':>9s}")
+    for name, M, N, Kd, ta, tb, calls in SHAPES:
+        A = torch.randn((Kd, M) if ta else (M, Kd), device=dev)
+        B = torch.randn((N, Kd) if tb else (Kd, N), device=dev)
+        C = torch.empty((M, N), device=dev)
+        best = None
+        for tile in args.tiles:
+            for _ in range(3):
+                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(args.reps):
+                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile)
+            e.record()
+            torch.cuda.synchronize()
+            us = 1e3 * s.elapsed_time(e) / args.reps
+            tf = 2.0 * M * N * Kd / (us * 1e-6) / 1e12
+            print(f"{name:26s} {tile:7d} {us:9.1f} {tf:7.1f} {us * calls / 1e3:9.2f}")
+            best = us if best is None else min(best, us)
+        tot_ms += best * calls / 1e3
+    print(f"total GEMM ms/epoch (best tile per shape): {tot_ms:.1f}")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", default="0,64,128")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    a.tiles = [int(t) for t in a.tiles.split(",")]
+    run(a)
