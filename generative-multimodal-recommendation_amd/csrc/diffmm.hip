@@ -147,7 +147,7 @@ __global__ void normalize_bwd_kernel(int64_t n, int cols, const float* __restric
 // contributions (scaled by 1/B): slot b -> d a, slot B+b -> d p, slot 2B+b -> d n.
 __global__ void bpr_kernel(int B, int64_t U, const float* __restrict__ Emb, const int* __restrict__ users,
                            const int* __restrict__ pos, const int* __restrict__ neg, float* __restrict__ loss,
-                           float* __restrict__ contrib) {
+                           float* __restrict__ contrib, float inv_norm) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = gid >> 4;
   const bool ok = b < B;
@@ -161,7 +161,7 @@ __global__ void bpr_kernel(int B, int64_t U, const float* __restrict__ Emb, cons
   float x = row16_sum(dot4(a, p) - dot4(a, q));
   if (!ok) return;
   float s = 1.f / (1.f + expf(-x));
-  float gx = -(s * (1.f - s)) / (1e-10f + s) / (float)B;
+  float gx = -(s * (1.f - s)) / (1e-10f + s) * inv_norm;  // inv_norm = 1 / rows of the (global) batch
   if ((gid & 15) == 0) loss[b] = -logf(1e-10f + s);
   st4(contrib + (int64_t)b * 64 + c, gmr::f4_scale(gx, sub4(p, q)));
   st4(contrib + ((int64_t)B + b) * 64 + c, gmr::f4_scale(gx, a));
@@ -515,9 +515,10 @@ extern "C" int gmr_normalize_rows_bwd_f32(int64_t n, int32_t cols, const float* 
 }
 
 extern "C" int gmr_bpr_fwd_bwd(int32_t B, int64_t U, const float* Emb, const int32_t* users, const int32_t* pos,
-                               const int32_t* neg, float* loss, float* contrib, void* stream) {
+                               const int32_t* neg, float* loss, float* contrib, float inv_norm, void* stream) {
   GMR_ARG(Emb && users && pos && neg && loss && contrib && B > 0, "bad args");
-  hipLaunchKernelGGL(bpr_kernel, ROWS16((int64_t)B), 0, (hipStream_t)stream, B, U, Emb, users, pos, neg, loss, contrib);
+  hipLaunchKernelGGL(bpr_kernel, ROWS16((int64_t)B), 0, (hipStream_t)stream, B, U, Emb, users, pos, neg, loss, contrib,
+                     inv_norm);
   GMR_LAUNCHED();
   return GMR_OK;
 }

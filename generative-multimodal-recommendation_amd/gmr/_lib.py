@@ -45,7 +45,7 @@ SIGNATURES = {
     "gmr_dmm_assemble": (I32, [I64, I64, P, P, P, P, P, F32, P, P, P]),
     "gmr_normalize_rows_f32": (I32, [I64, I32, P, I64, P, I64, P, P]),
     "gmr_normalize_rows_bwd_f32": (I32, [I64, I32, P, I64, P, P, I64, P, I64, F32, I32, P]),
-    "gmr_bpr_fwd_bwd": (I32, [I32, I64, P, P, P, P, P, P, P]),
+    "gmr_bpr_fwd_bwd": (I32, [I32, I64, P, P, P, P, P, P, F32, P]),
     "gmr_row_softmax_f32": (I32, [I64, I64, P, I64, F32, P, P]),
     "gmr_contrast_rows": (I32, [I32, P, P, I64, P, F32, F32, P, P, I64, P]),
     "gmr_gather_rows_f32": (I32, [I32, I32, P, I64, P, I64, P, I64, P]),

@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from . import dist
 from . import kernels as K
 from .abstract_recommender import GeneralRecommender
 from .denoise import Denoiser
@@ -201,11 +202,11 @@ class DiffMM(GeneralRecommender):
         return w["Emb"]
 
     # ================================================================= fused rec step
-    def _contrast(self, w, nodes, off, n_table, slot0, loss_out, B):
+    def _contrast(self, w, nodes, off, n_table, slot0, loss_out, B, norm):
         """InfoNCE of CLN[:, :64] (view 1) vs CLN[:, 64:] (view 2) for the gathered nodes."""
         CLN, P1 = w["CLN"], w["P1"][:B]
         inv_t = 1.0 / self.temp
-        coef = self.ssl_reg / B
+        coef = self.ssl_reg / norm
         table = CLN[off:off + n_table, 64:]
         L = w["logits"][:B, :n_table]
         K.gather_rows(CLN[:, :64], nodes, P1, off=off)
@@ -217,16 +218,19 @@ class DiffMM(GeneralRecommender):
         _lib.call("gmr_contrast_rows", B, ptr(CLN), ptr(nodes), off, ptr(w["lse"]), inv_t, coef, ptr(loss_out),
                   ptr(contrib), contrib.stride(0), stream())
 
-    def rec_step(self, users, pos, neg, plan_bpr=None, plan_cl=None):
+    def rec_step(self, users, pos, neg, plan_bpr=None, plan_cl=None, norm_rows=None, reg_share=1.0):
         """Loss of calculate_loss (cl_method 0) and all rec-parameter gradients (into rec_slab.grad).
 
         users/pos/neg: int32 device tensors of one batch; plan_*: sorted scatter plans (built here
-        when not supplied by the loader)."""
+        when not supplied by the loader).  Data parallel: norm_rows = rows of the global batch (the
+        batch means use it) and reg_share = 1 / ranks (the regulariser is counted once after the
+        gradient all-reduce); the defaults give the single-device loss."""
         if self.image_UI_matrix is None or self.text_UI_matrix is None:
             raise RuntimeError("the UI graphs are built by DiffMMTrainer before the BPR phase")
         if self.cl_method != 0:
             raise NotImplementedError("cl_method = 0 (DiffMM.yaml) is the configured hot path")
         B = users.numel()
+        nr = float(norm_rows or B)
         w = self._work(B)
         U, I, N = self.n_users, self.n_items, self.N
         s = self.rec_slab
@@ -237,14 +241,15 @@ class DiffMM(GeneralRecommender):
         K.zero_(w["dCLN"])  # [:, 64:] is then overwritten by the d-table GEMMs, [:, :64] by scatters
         # --- losses and their sparse gradient contributions
         _lib.call("gmr_bpr_fwd_bwd", B, U, ptr(w["Emb"]), ptr(users), ptr(pos), ptr(neg), ptr(w["loss_bpr"]),
-                  ptr(w["contrib_bpr"]), stream())
-        self._contrast(w, users, 0, U, 0, w["loss_cu"], B)
-        self._contrast(w, pos, U, I, B, w["loss_ci"], B)
+                  ptr(w["contrib_bpr"]), 1.0 / nr, stream())
+        self._contrast(w, users, 0, U, 0, w["loss_cu"], B, nr)
+        self._contrast(w, pos, U, I, B, w["loss_ci"], B, nr)
         loss = w["loss"][:1]
-        _lib.call("gmr_sum_f32", B, ptr(w["loss_bpr"]), 1.0 / B, ptr(loss), 0, stream())
-        _lib.call("gmr_sqnorm_f32", N * 64, ptr(E0), self.reg_weight, ptr(loss), 1, ptr(w["sqws"]), stream())
-        _lib.call("gmr_sum_f32", B, ptr(w["loss_cu"]), self.ssl_reg / B, ptr(loss), 1, stream())
-        _lib.call("gmr_sum_f32", B, ptr(w["loss_ci"]), self.ssl_reg / B, ptr(loss), 1, stream())
+        _lib.call("gmr_sum_f32", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(loss), 0, stream())
+        _lib.call("gmr_sqnorm_f32", N * 64, ptr(E0), self.reg_weight * reg_share, ptr(loss), 1, ptr(w["sqws"]),
+                  stream())
+        _lib.call("gmr_sum_f32", B, ptr(w["loss_cu"]), self.ssl_reg / nr, ptr(loss), 1, stream())
+        _lib.call("gmr_sum_f32", B, ptr(w["loss_ci"]), self.ssl_reg / nr, ptr(loss), 1, stream())
         # --- backward
         dEmb, dCLN = w["dEmb"], w["dCLN"]
         K.zero_(dEmb)
@@ -272,7 +277,7 @@ class DiffMM(GeneralRecommender):
         _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
         adj.spmm(w["T3"], [(w["DG"][:, :64],), (w["DG"][:, 64:],)])
         _lib.call("gmr_dmm_assemble", N, U, ptr(w["T2"]), ptr(w["T3"]), ptr(w["OutI"]), ptr(w["OutT"]), ptr(E0),
-                  2.0 * self.reg_weight, ptr(s.gview("E0")), ptr(w["dNF"]), stream())
+                  2.0 * self.reg_weight * reg_share, ptr(s.gview("E0")), ptr(w["dNF"]), stream())
         # modality projections: normalize + leaky-relu backward, then W grads
         dNF = w["dNF"]
         K.normalize_rows_bwd(w["NF"][:, :64], w["nrmF"][0], dNF[:, :64], dNF[:, :64], slope=0.2)
@@ -389,12 +394,14 @@ class DiffMM(GeneralRecommender):
                     "users": torch.arange(self.n_users, dtype=torch.int32, device=dev)}
         return self._dw
 
-    def diffusion_step(self, den, batch_users, feats, item_embeds, step, noise=None, keep=None, t=None):
+    def diffusion_step(self, den, batch_users, feats, item_embeds, step, noise=None, keep=None, t=None,
+                       norm_rows=None):
         """One GaussianDiffusion.training_losses + backward for one denoiser (diffmm.py:453-477).
 
         Writes the denoiser's gradients into its slab; returns (diff_loss, gc_loss) per-row
         fp64 views.  noise/keep/t may be supplied (parity tests); else drawn by Philox."""
         B = batch_users.numel()
+        nr = float(norm_rows or B)
         w = self._dwork(B)
         I, T = self.n_items, self.steps
         x, h, out, Z = w["x"][:B], w["h"][:B], w["out"][:B], w["Z"][:B]
@@ -414,8 +421,8 @@ class DiffMM(GeneralRecommender):
         den.output(h, o)
         K.gemm(o, feats, Z)                                                     # out @ feats
         _lib.call("gmr_diff_loss_rows", B, I, ptr(batch_users), ptr(self.user_ptr), ptr(self.user_items), ptr(tt),
-                  ptr(self._w_dev), ptr(o), o.stride(0), 1.0 / B, ptr(w["mse"]), ptr(w["diff"]), 1, stream())
-        gsc = self.e_loss * 2.0 / (64.0 * B)
+                  ptr(self._w_dev), ptr(o), o.stride(0), 1.0 / nr, ptr(w["mse"]), ptr(w["diff"]), 1, stream())
+        gsc = self.e_loss * 2.0 / (64.0 * nr)
         _lib.call("gmr_diff_gc_rows", B, ptr(batch_users), ptr(self.user_ptr), ptr(self.user_items),
                   ptr(item_embeds), item_embeds.stride(0), ptr(Z), 64, gsc, ptr(w["Gc"]), 64, ptr(w["gc"]), stream())
         K.gemm(w["Gc"][:B], feats, o, trans_b=True, beta=1.0)                  # dout += G feats^T
@@ -446,17 +453,21 @@ class DiffMM(GeneralRecommender):
 
     @torch.no_grad()
     def rebuild_ui_graphs(self, chunk=8192):
-        """Graph construction phase of DiffMMTrainer._train_epoch (trainer.py:529-576) on the device."""
+        """Graph construction phase of DiffMMTrainer._train_epoch (trainer.py:529-576) on the device.
+        Data parallel: each rank p_samples a contiguous user shard; top-k rows are all-gathered."""
         U, I, k = self.n_users, self.n_items, self.rebuild_k
         dev = self.device
-        topk = torch.empty((U, k), dtype=torch.int32, device=dev)
+        lo_r, hi_r, size = dist.padded_shard(U)
+        W = dist.world()
+        topk = torch.zeros((W * size, k), dtype=torch.int32, device=dev)
         uptr = torch.empty(U + 1, dtype=torch.int32, device=dev)
         uitems = torch.empty(U * k, dtype=torch.int32, device=dev)
         graphs = []
         for den in (self.denoise_model_image, self.denoise_model_text):
-            for lo in range(0, U, chunk):
-                self.p_sample_topk(den, lo, min(U, lo + chunk), topk, k)
-            K.topk_to_user_csr(topk, uptr, uitems)
+            for lo in range(lo_r, hi_r, chunk):
+                self.p_sample_topk(den, lo, min(hi_r, lo + chunk), topk, k)
+            dist.all_gather_rows_(topk, size)
+            K.topk_to_user_csr(topk[:U], uptr, uitems)
             g = K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0)
             if self.keepRate != 1:
                 raise NotImplementedError("SpAdjDropEdge with keep_rate < 1 (DiffMM.yaml uses keep_rate = 1)")

@@ -1,0 +1,102 @@
+"""Data parallelism across the GPUs of one node: one process per GPU, torch.distributed over RCCL
+(backend "nccl" is RCCL on ROCm, riding xGMI).  The reference has no distributed code (SURVEY.md
+F2); this module holds the sharding rules used by the trainers:
+
+  * diffusion phase  — every global step takes world x train_batch_size users of the epoch
+    permutation; rank r trains on its contiguous slice; denoiser gradients are all-reduced
+    (SUM of per-rank sums normalised by the global row count) before the identical Adam steps;
+  * graph rebuild    — users are split in contiguous shards; each rank p_samples its shard and
+    the int32 top-k lists are all-gathered; every rank builds the identical CSR;
+  * BPR phase        — global step g runs loader batches g*W .. g*W+W-1, one per rank; the
+    rec gradients are all-reduced (the regulariser is counted once);
+  * evaluation       — eval users are sharded; the top-K index rows are all-gathered.
+The per-GPU batch stays train_batch_size, so the number of optimizer steps per epoch shrinks
+with the world size (the global batch grows); world = 1 is exactly the reference schedule.
+Everything here also runs on CPU tensors with the gloo backend (tests/test_dist_cpu.py).
+"""
+import math
+
+import torch
+import torch.distributed as tdist
+
+
+def is_dist():
+    return tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1
+
+
+def world():
+    return tdist.get_world_size() if is_dist() else 1
+
+
+def rank():
+    return tdist.get_rank() if is_dist() else 0
+
+
+def shard(n, w=None, r=None):
+    """Contiguous [lo, hi) slice of n items for rank r of w (first n % w ranks get one more)."""
+    w = world() if w is None else w
+    r = rank() if r is None else r
+    q, rem = divmod(n, w)
+    lo = r * q + min(r, rem)
+    return lo, lo + q + (1 if r < rem else 0)
+
+
+def padded_shard(n, w=None, r=None):
+    """Equal-size shards (ceil(n / w)) for all-gathers: returns (lo, hi, size) with hi clipped to n."""
+    w = world() if w is None else w
+    r = rank() if r is None else r
+    s = -(-n // w)
+    lo = min(n, r * s)
+    return lo, min(n, lo + s), s
+
+
+def global_steps(n_batches, w=None):
+    return math.ceil(n_batches / (world() if w is None else w))
+
+
+def step_batches(g, n_batches, w=None):
+    w = world() if w is None else w
+    return [b for b in range(g * w, g * w + w) if b < n_batches]
+
+
+def dp_scales(rows):
+    """(norm_rows, reg_share) for one global step whose ranks hold `rows` rows each (0 = idle rank):
+    every active rank divides its batch sums by the global row count and adds 1/active of the
+    regulariser, so the SUM all-reduce equals the gradient of the global-batch loss."""
+    active = sum(1 for x in rows if x > 0)
+    return float(sum(rows)), (1.0 / active if active else 0.0)
+
+
+def all_reduce_(t):
+    if is_dist():
+        tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
+    return t
+
+
+def all_gather_rows_(full, size):
+    """full: (world * size, ...) buffer whose rank slice [rank*size, (rank+1)*size) is filled
+    locally; gathers every rank's slice in place."""
+    if is_dist():
+        r = rank()
+        local = full[r * size:(r + 1) * size].clone()
+        if tdist.get_backend() == "nccl":
+            tdist.all_gather_into_tensor(full, local)
+        else:  # gloo rehearsal (CPU tests, or several ranks sharing one GPU)
+            parts = list(full.split(size))
+            tdist.all_gather(parts, local)
+            for i, p in enumerate(parts):
+                full[i * size:(i + 1) * size].copy_(p)
+    return full
+
+
+def barrier():
+    if is_dist():
+        tdist.barrier()
+
+
+def max_scalar(x, device):
+    if not is_dist():
+        return x
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item())

@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from . import dist
 from . import kernels as K
 from .kernels import ptr, stream
 from .slab import FlatAdam
@@ -73,12 +74,26 @@ class Trainer:
         d = train_data.epoch()
         acc = self._loss_acc
         K.zero_(acc)
-        n = 0
-        for b, u, p, ng, pb, pc in train_data.batches(d):
-            loss = self.model.rec_step(u, p, ng, pb, pc)
-            _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
+        batches = list(train_data.batches(d))
+        W, r = dist.world(), dist.rank()
+        slabs = self.model.optim_slabs()
+        for g in range(dist.global_steps(len(batches), W)):
+            ids = dist.step_batches(g, len(batches), W)
+            rows = [batches[i][1].numel() for i in ids] + [0] * (W - len(ids))
+            norm, share = dist.dp_scales(rows)
+            mine = g * W + r
+            if mine < len(batches):
+                _, u, p, ng, pb, pc = batches[mine]
+                loss = self.model.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share)
+                _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
+            else:
+                for s_ in slabs:
+                    s_.zero_grad()
+            if W > 1:
+                for s_ in slabs:
+                    dist.all_reduce_(s_.grad)
             self.optimizer.step()
-            n += 1
+        dist.all_reduce_(acc)
         total = float(acc[0].item())
         if np.isnan(total):
             self.logger.info("Loss is nan at epoch: {}. Exiting.".format(epoch_idx))
@@ -165,13 +180,16 @@ class Trainer:
 
     @torch.no_grad()
     def topk_all(self, eval_data, kmax):
-        """Top-k indices of every eval user (n_eval x k int32, device); reference trainer.py:369-388."""
+        """Top-k indices of every eval user (n_eval x k int32, device); reference trainer.py:369-388.
+        Data parallel: each rank scores a contiguous shard of the eval users; rows are all-gathered."""
         d = eval_data.to_device()
         n = eval_data.pr_end
         E = eval_data.step
+        lo_r, hi_r, size = dist.padded_shard(n)
+        W = dist.world()
         out = getattr(self, "_topk_buf", None)
-        if out is None or out.shape != (n, kmax):
-            out = torch.empty((n, kmax), dtype=torch.int32, device=self.device)
+        if out is None or out.shape != (W * size, kmax):
+            out = torch.zeros((W * size, kmax), dtype=torch.int32, device=self.device)
             self._topk_buf = out
         m = self.model
         if hasattr(m, "forward_embeddings"):
@@ -181,19 +199,26 @@ class Trainer:
                 sb = torch.empty((min(E, n), (m.n_items + 3) // 4 * 4), dtype=torch.float32, device=self.device)
                 self._score_buf = sb
         mptr = d["mask_ptr"]
-        for lo in range(0, n, E):
-            hi = min(n, lo + E)
+        off = dist.rank() * size - lo_r  # row of user lo_r inside the padded gather buffer
+        for lo in range(lo_r, hi_r, E):
+            hi = min(hi_r, lo + E)
             users = d["eval_u32"][lo:hi]
             m0, m1 = int(mptr[lo]), int(mptr[hi])
             rows = d["mask_rows"][m0:m1] - lo
             cols = d["mask_cols"][m0:m1]
+            dst = out[off + lo:off + hi]
             if hasattr(m, "forward_embeddings"):
-                m.topk_from_embeddings(usr, itm, users, rows, cols, kmax, out[lo:hi], sb)
+                m.topk_from_embeddings(usr, itm, users, rows, cols, kmax, dst, sb)
             else:
                 scores = m.full_sort_predict([users.long()])
                 K.mask_scores(scores, rows, cols)
-                K.topk_rows(scores, kmax, out[lo:hi])
-        return out
+                K.topk_rows(scores, kmax, dst)
+        dist.all_gather_rows_(out, size)
+        if W == 1:
+            return out
+        parts = [out[r * size:r * size + (dist.padded_shard(n, W, r)[1] - dist.padded_shard(n, W, r)[0])]
+                 for r in range(W)]
+        return torch.cat(parts)
 
 
 class DiffMMTrainer(Trainer):
@@ -208,29 +233,41 @@ class DiffMMTrainer(Trainer):
         self._epoch_ctr = 0
 
     def diffusion_phase(self, epoch_idx):
-        """trainer.py:487-527 — train both denoisers over all users in shuffled batches."""
+        """trainer.py:487-527 — train both denoisers over all users in shuffled batches.
+        Data parallel: a global step covers world x batch users; each rank takes a contiguous slice."""
         m = self.model
         m.train()
         B = self.config["train_batch_size"]
         U = self.user_num
+        W, r = dist.world(), dist.rank()
         w = m._work(1)
         m._project(w)                                         # image/text feats, detached (:501-502)
         feats_i, feats_t = w["F"][:, :64], w["F"][:, 64:]
         iE = m.rec_slab.view("E0")[U:]                        # getItemEmbeds().detach() (:496)
         _lib.call("gmr_permutation", U, m.seed, 1000 + self._epoch_ctr, ptr(self._perm), stream())
         K.zero_(self._dloss)
+        dens = ((m.denoise_model_image, feats_i), (m.denoise_model_text, feats_t))
         steps = 0
-        for bi, lo in enumerate(range(0, U, B)):
-            users = self._perm[lo:min(U, lo + B)]
+        for g, lo in enumerate(range(0, U, B * W)):
+            hi = min(U, lo + B * W)
+            a, b = dist.shard(hi - lo, W, r)
+            users = self._perm[lo + a:lo + b]
             nb = users.numel()
-            base = (self._epoch_ctr * 100000 + bi) * 2
-            for j, (den, feats) in enumerate(((m.denoise_model_image, feats_i), (m.denoise_model_text, feats_t))):
-                diff, gc = m.diffusion_step(den, users, feats, iE, base + j)
-                _lib.call("gmr_sum_f64", nb, ptr(diff), 1.0 / nb, ptr(self._dloss[j:j + 1]), 1, stream())
-                _lib.call("gmr_sum_f64", nb, ptr(gc), m.e_loss / nb, ptr(self._dloss[j:j + 1]), 1, stream())
+            base = ((self._epoch_ctr * 100000 + g) * W + r) * 2
+            for j, (den, feats) in enumerate(dens):
+                if nb > 0:
+                    diff, gc = m.diffusion_step(den, users, feats, iE, base + j, norm_rows=hi - lo)
+                    _lib.call("gmr_sum_f64", nb, ptr(diff), 1.0 / (hi - lo), ptr(self._dloss[j:j + 1]), 1, stream())
+                    _lib.call("gmr_sum_f64", nb, ptr(gc), m.e_loss / (hi - lo), ptr(self._dloss[j:j + 1]), 1,
+                              stream())
+                else:
+                    den.slab.zero_grad()
+                if W > 1:
+                    dist.all_reduce_(den.slab.grad)
             self.denoise_opt_image.step()
             self.denoise_opt_text.step()
             steps += 1
+        dist.all_reduce_(self._dloss)
         self._epoch_ctr += 1
         return steps
 

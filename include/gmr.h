@@ -115,7 +115,7 @@ int gmr_normalize_rows_bwd_f32(int64_t n, int32_t cols, const float* y, int64_t 
 /* K7 BPR: -log(1e-10 + sigmoid(<a,p> - <a,n>)) with gathers; per-row loss + 3B contribution rows
  * (diffmm.py:220-227, common/loss.py:33-37) */
 int gmr_bpr_fwd_bwd(int32_t B, int64_t U, const float* Emb, const int32_t* users, const int32_t* pos,
-                    const int32_t* neg, float* loss, float* contrib, void* stream);
+                    const int32_t* neg, float* loss, float* contrib, float inv_norm, void* stream);
 /* K8 InfoNCE pieces (diffmm.py:251-258): in-place row softmax of logits with log-sum-exp out,
  * and the per-row terms of the gathered batch */
 int gmr_row_softmax_f32(int64_t rows, int64_t cols, float* L, int64_t ld, float coef, float* lse, void* stream);
