@@ -154,8 +154,9 @@ __global__ void time_bias_kernel(int T, int E, const float* __restrict__ embW, c
 __global__ void __launch_bounds__(256) loss_rows_kernel(int B, int I, const int* __restrict__ users,
                                                         const int* __restrict__ uptr, const int* __restrict__ uitems,
                                                         const int* __restrict__ t, const double* __restrict__ wtab,
-                                                        float* __restrict__ out, int64_t ld, float grad_scale,
-                                                        double* __restrict__ mse_out, double* __restrict__ diff_out,
+                                                        const float* __restrict__ pt, float* __restrict__ out,
+                                                        int64_t ld, float grad_scale, double* __restrict__ mse_out,
+                                                        double* __restrict__ diff_out, double* __restrict__ loss_out,
                                                         int write_grad) {
   extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
   const int b = blockIdx.x;
@@ -169,7 +170,8 @@ __global__ void __launch_bounds__(256) loss_rows_kernel(int B, int I, const int*
   }
   __syncthreads();
   const double w = wtab[t[b]];
-  const float ca = (float)(w * 2.0 / (double)I) * grad_scale;
+  const double div = pt ? (double)pt[b] : 1.0;
+  const float ca = (float)(w / div * 2.0 / (double)I) * grad_scale;
   float* row = out + (int64_t)b * ld;
   float s = 0.f;
   for (int i = threadIdx.x; i < I; i += 256) {
@@ -186,6 +188,7 @@ __global__ void __launch_bounds__(256) loss_rows_kernel(int B, int I, const int*
     const double mse = (double)((red[0] + red[1]) + (red[2] + red[3])) / (double)I;
     mse_out[b] = mse;
     diff_out[b] = w * mse;
+    if (loss_out) loss_out[b] = w * mse / div;
   }
 }
 
@@ -309,11 +312,120 @@ __global__ void __launch_bounds__(1024) time_bwd_e_kernel(int T, int E, int H, c
   }
 }
 
+// DiffRec GaussianDiffusion.sample_timesteps (models/diffrec.py:234-250).  Until every t has a
+// full loss history: uniform t (same Philox stream as sample_t_kernel) and pt = 1.  Then
+// pt_all = (1 - up) * sqrt(mean(hist^2)) / sum + up / T, t ~ pt_all (inverse CDF), pt = pt_all[t] * T.
+// One 1024-thread block; T <= 1024.
+__global__ void __launch_bounds__(1024) sample_t_importance_kernel(int B, int T, int Hn, const double* __restrict__ hist,
+                                                                  const int* __restrict__ count, double uniform_prob,
+                                                                  uint64_t seed, uint64_t step, int* __restrict__ t,
+                                                                  float* __restrict__ pt) {
+  __shared__ double cdf[1024];
+  __shared__ double pall[1024];
+  const int i = threadIdx.x;
+  const int full = __syncthreads_and(i >= T || count[i] == Hn);
+  if (!full) {
+    for (int b = i; b < B; b += 1024) {
+      uint4 r = gmr::Philox::gen(seed ^ 0xA5A5A5A5ull, step, (uint64_t)b);
+      t[b] = (int)(((uint64_t)r.x * (uint64_t)T) >> 32);
+      pt[b] = 1.f;
+    }
+    return;
+  }
+  if (i < T) {
+    double m = 0.0;
+    for (int j = 0; j < Hn; ++j) m += hist[(int64_t)i * Hn + j] * hist[(int64_t)i * Hn + j];
+    pall[i] = sqrt(m / (double)Hn);
+  }
+  __syncthreads();
+  if (i == 0) {
+    double tot = 0.0;
+    for (int j = 0; j < T; ++j) tot += pall[j];
+    double run = 0.0;
+    for (int j = 0; j < T; ++j) {
+      pall[j] = pall[j] / tot * (1.0 - uniform_prob) + uniform_prob / (double)T;
+      run += pall[j];
+      cdf[j] = run;
+    }
+  }
+  __syncthreads();
+  for (int b = i; b < B; b += 1024) {
+    uint4 r = gmr::Philox::gen(seed ^ 0x5EED5EEDull, step, (uint64_t)b);
+    const double u = (((uint64_t)r.x << 21) ^ (uint64_t)(r.y >> 11)) * (1.0 / 9007199254740992.0) * cdf[T - 1];
+    int lo = 0, hi = T - 1;  // first j with cdf[j] > u
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+    }
+    t[b] = lo;
+    pt[b] = (float)(pall[lo] * (double)T);
+  }
+}
+
+// Lt_history / Lt_count update of training_losses (models/diffrec.py:279-286), with the
+// reference's per-sample sequential semantics: the rows of the batch are applied in order
+// (rows with t < 0 are padding and skipped).  Thread i owns timestep i; the batch is scanned
+// backwards through LDS so each thread keeps the latest Hn losses of its timestep.
+__global__ void __launch_bounds__(1024) lt_update_kernel(int B, int T, int Hn, const int* __restrict__ t,
+                                                         const double* __restrict__ loss, double* __restrict__ hist,
+                                                         int* __restrict__ count) {
+  __shared__ int st[1024];
+  const int i = threadIdx.x;
+  int seen = 0;          // matches found so far (scanning from the end), capped at Hn
+  int keep[16];          // batch rows of the latest min(seen, Hn) matches, latest first
+  for (int end = B; end > 0; end -= 1024) {
+    const int beg = max(0, end - 1024);
+    __syncthreads();
+    if (beg + i < end) st[i] = t[beg + i];
+    __syncthreads();
+    if (i < T && seen < Hn) {  // once Hn matches are known the older rows no longer matter
+      for (int b = end - 1; b >= beg && seen < Hn; --b) {
+        if (st[b - beg] == i) keep[seen++] = b;
+      }
+    }
+  }
+  if (i >= T || seen == 0) return;
+  double* h = hist + (int64_t)i * Hn;
+  const int c = count[i];
+  if (c + seen <= Hn && seen < Hn) {  // (seen == Hn may mean more matches: always the shift branch)
+    for (int j = 0; j < seen; ++j) h[c + j] = loss[keep[seen - 1 - j]];
+    count[i] = c + seen;
+  } else {
+    const int kn = min(seen, Hn), ko = Hn - kn;
+    double old[16];
+    for (int j = 0; j < ko; ++j) old[j] = h[c - ko + j];
+    for (int j = 0; j < ko; ++j) h[j] = old[j];
+    for (int j = 0; j < kn; ++j) h[ko + j] = loss[keep[kn - 1 - j]];
+    count[i] = Hn;
+  }
+}
+
 }  // namespace
 
 extern "C" int gmr_diff_sample_t(int32_t B, int32_t T, uint64_t seed, uint64_t step, int32_t* t, void* stream) {
   GMR_ARG(t && B > 0 && T > 0, "bad args");
   hipLaunchKernelGGL(sample_t_kernel, dim3(gmr::grid_for(B, 256)), dim3(256), 0, (hipStream_t)stream, B, T, seed, step, t);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_diff_sample_t_importance(int32_t B, int32_t T, int32_t hist_len, const double* hist,
+                                            const int32_t* count, double uniform_prob, uint64_t seed, uint64_t step,
+                                            int32_t* t, float* pt, void* stream) {
+  GMR_ARG(hist && count && t && pt && B > 0 && T > 0 && T <= 1024, "bad args (T <= 1024)");
+  GMR_ARG(hist_len >= 1 && hist_len <= 16, "history length must be 1..16");
+  hipLaunchKernelGGL(sample_t_importance_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, T, hist_len, hist,
+                     count, uniform_prob, seed, step, t, pt);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_diff_history_update(int32_t B, int32_t T, int32_t hist_len, const int32_t* t, const double* loss,
+                                       double* hist, int32_t* count, void* stream) {
+  GMR_ARG(t && loss && hist && count && B > 0 && T > 0 && T <= 1024, "bad args (T <= 1024)");
+  GMR_ARG(hist_len >= 1 && hist_len <= 16, "history length must be 1..16");
+  hipLaunchKernelGGL(lt_update_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, T, hist_len, t, loss, hist,
+                     count);
   GMR_LAUNCHED();
   return GMR_OK;
 }
@@ -359,14 +471,14 @@ extern "C" int gmr_diff_time_bias(int32_t T, int32_t E, const float* emb_W, cons
 }
 
 extern "C" int gmr_diff_loss_rows(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr,
-                                  const int32_t* user_items, const int32_t* t, const double* wtab, float* out,
-                                  int64_t ld, float grad_scale, double* mse_out, double* diff_out, int32_t write_grad,
-                                  void* stream) {
+                                  const int32_t* user_items, const int32_t* t, const double* wtab, const float* pt,
+                                  float* out, int64_t ld, float grad_scale, double* mse_out, double* diff_out,
+                                  double* loss_out, int32_t write_grad, void* stream) {
   GMR_ARG(users && user_ptr && user_items && t && wtab && out && mse_out && diff_out && B > 0 && I > 0, "bad args");
   const size_t dyn = sizeof(uint32_t) * (size_t)((I + 31) / 32);
   GMR_ARG(dyn <= 60000, "item count too large for the LDS bitmap");
   hipLaunchKernelGGL(loss_rows_kernel, dim3(B), dim3(256), dyn, (hipStream_t)stream, B, I, users, user_ptr, user_items,
-                     t, wtab, out, ld, grad_scale, mse_out, diff_out, write_grad);
+                     t, wtab, pt, out, ld, grad_scale, mse_out, diff_out, loss_out, write_grad);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -220,15 +220,226 @@ __global__ void __launch_bounds__(256) spmm_fix_kernel(PlanView pv, float alpha,
   *reinterpret_cast<float4*>(yp) = o;
 }
 
+// ----------------------------------------------------------------------------------------
+// Blocked variant (plans with seg_nnz >= 512 = T): rows are packed into blocks of whole rows,
+// a new block starting at row 0, every T-th row, and at each row that contains an nnz index
+// that is a positive multiple of T, so a block holds <= ~T nnz plus at most one long row.
+// One 1024-thread workgroup (128 lane groups of 8) owns one block and one 32-float column
+// slice (XCD-pinned as in the group variant): it stages the block's rowptr in LDS, splits
+// the block's nnz range evenly over its 128 groups (merge-path), and each group walks its
+// range 16 neighbours at a time with all 16 gathers in flight, emitting rows as it crosses
+// row ends.  Rows cut by group boundaries are summed in LDS in group order, so results are
+// deterministic and no second pass (or partial buffer) is needed; hub rows get the whole
+// workgroup.  Few, long-lived waves: the short-wave variants are bound by the wave launch
+// rate on this graph shape (SQ counters, profiles/).
+constexpr int kBlkThreads = 1024;
+constexpr int kBlkGroups = kBlkThreads / 8;
+
+__host__ __device__ inline int64_t blk_max_blocks(int64_t n_rows, int64_t nnz, int T) {
+  return (nnz + T - 1) / T + (n_rows + T - 1) / T + 2;
+}
+
+__global__ void __launch_bounds__(1024) blk_plan_kernel(const int* __restrict__ rowptr, int n_rows, int T,
+                                                        int max_blocks, int* __restrict__ plan) {
+  __shared__ int s_cnt[1024];
+  const int t = threadIdx.x;
+  const int chunk = (n_rows + 1023) / 1024;
+  const int r0 = t * chunk, r1 = min(n_rows, r0 + chunk);
+  auto starts = [&](int r) -> bool {
+    if (r == 0 || r % T == 0) return true;
+    const int a = rowptr[r], b = rowptr[r + 1];
+    const int first_mult = ((a + T - 1) / T) * T;  // smallest multiple of T >= a
+    return first_mult > 0 && first_mult < b;
+  };
+  int n = 0;
+  for (int r = r0; r < r1; ++r) n += starts(r) ? 1 : 0;
+  s_cnt[t] = n;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    int v = t >= off ? s_cnt[t - off] : 0;
+    __syncthreads();
+    s_cnt[t] += v;
+    __syncthreads();
+  }
+  int o = s_cnt[t] - n;
+  int* blk_row = plan + kPlanHdr;
+  int* blk_nnz = blk_row + max_blocks + 1;
+  for (int r = r0; r < r1; ++r)
+    if (starts(r)) {
+      blk_row[o] = r;
+      blk_nnz[o] = rowptr[r];
+      ++o;
+    }
+  if (t == 1023) {
+    plan[0] = s_cnt[1023];
+    plan[1] = plan[2] = 0;
+    plan[3] = T;
+    blk_row[s_cnt[1023]] = n_rows;
+    blk_nnz[s_cnt[1023]] = rowptr[n_rows];
+  }
+}
+
+template <int NB>
+__global__ void __launch_bounds__(kBlkThreads) spmm_blk_kernel(const int* __restrict__ rowptr,
+                                                               const int* __restrict__ col,
+                                                               const float* __restrict__ val,
+                                                               const int* __restrict__ plan, int T, int max_blocks,
+                                                               Src src, float alpha, float beta,
+                                                               float* __restrict__ y, int64_t ldy) {
+  constexpr int NS = 2 * NB, RP = 8 / NS;
+  extern __shared__ __attribute__((aligned(16))) int s_rp[];  // T + 1 entries
+  __shared__ float4 s_part[kBlkGroups][2][8];
+  __shared__ int s_prow[kBlkGroups][2];
+  const int xcd = blockIdx.x & 7;
+  const int slice = xcd % NS, rpart = xcd / NS;
+  const int nblk = plan[0];
+  const int b_lo = (int)((int64_t)nblk * rpart / RP), b_hi = (int)((int64_t)nblk * (rpart + 1) / RP);
+  const int bi = b_lo + (int)(blockIdx.x >> 3);
+  if (bi >= b_hi) return;
+  const int* blk_row = plan + kPlanHdr;
+  const int* blk_nnz = blk_row + max_blocks + 1;
+  // the block's row and nnz ranges come from the plan, so the rowptr staging and the first
+  // col/val loads are issued together (one dependent round trip instead of two)
+  const int row0 = blk_row[bi], nrows = blk_row[bi + 1] - row0;
+  const int E0 = blk_nnz[bi], E1 = blk_nnz[bi + 1];
+  const int grp = threadIdx.x >> 3, sub = threadIdx.x & 7;
+  const int wg = (threadIdx.x & 63) >> 3;  // group index inside the wave (shuffle base)
+  const int L = (E1 - E0 + kBlkGroups - 1) / kBlkGroups;
+  const int a = min(E1, E0 + grp * L), b = min(E1, a + L);
+  int ca = 0, cb = 0;
+  float va = 0.f, vb = 0.f;
+  if (a + sub < b) {
+    ca = col[a + sub];
+    va = val[a + sub];
+  }
+  if (a + 8 + sub < b) {
+    cb = col[a + 8 + sub];
+    vb = val[a + 8 + sub];
+  }
+  for (int i = threadIdx.x; i <= nrows; i += kBlkThreads) s_rp[i] = rowptr[row0 + i];
+  s_prow[grp][0] = s_prow[grp][1] = -1;
+  const int blk = slice >> 1;
+  const int c4 = (slice & 1) * 32 + sub * 4;
+  const float* lo = src.lo[blk] + c4;
+  const float* hi = src.hi[blk] + c4;
+  const int64_t ldl = src.ld_lo[blk], ldh = src.ld_hi[blk];
+  const int64_t split = src.split;
+  const int ycol = slice * 32 + sub * 4;
+  // first 16 gathers go out before the barrier (they do not need the row table)
+  float4 xs[16];
+  float vs[16];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = __shfl(ca, (wg << 3) + u);
+    vs[u] = __shfl(va, (wg << 3) + u);
+    xs[u] = *reinterpret_cast<const float4*>(c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh);
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = __shfl(cb, (wg << 3) + u);
+    vs[8 + u] = __shfl(vb, (wg << 3) + u);
+    xs[8 + u] = *reinterpret_cast<const float4*>(c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh);
+  }
+  __syncthreads();
+  if (a < b) {
+    int lo_r = 0, hi_r = nrows - 1;  // largest r with s_rp[r] <= a
+    while (lo_r < hi_r) {
+      const int mid = (lo_r + hi_r + 1) >> 1;
+      if (s_rp[mid] <= a) lo_r = mid; else hi_r = mid - 1;
+    }
+    int r = lo_r;
+    int rend = s_rp[r + 1];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto emit = [&](int rr, float4 v) {
+      const int rb = s_rp[rr], re = s_rp[rr + 1];
+      if (rb >= a && re <= b) {
+        float* yp = y + (int64_t)(row0 + rr) * ldy + ycol;
+        float4 o = gmr::f4_scale(alpha, v);
+        if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
+        *reinterpret_cast<float4*>(yp) = o;
+      } else {
+        const int k = rb < a ? 0 : 1;  // 0: continues a row begun by an earlier group; 1: row owner
+        s_part[grp][k][sub] = v;
+        if (sub == 0) s_prow[grp][k] = rr;
+      }
+    };
+    for (int e = a;;) {
+      const int cnt = min(16, b - e);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        if (u < cnt) {
+          while (e + u >= rend) {  // leave finished rows (empty ones are written by the pass below)
+            if (s_rp[r] != rend) emit(r, acc);
+            acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            ++r;
+            rend = s_rp[r + 1];
+          }
+          acc = gmr::f4_fma(vs[u], xs[u], acc);
+        }
+      }
+      e += 16;
+      if (e >= b) break;
+      // long ranges (hub blocks): next 16 neighbours
+      const int ea = e + sub, eb = e + 8 + sub;
+      ca = cb = 0;
+      va = vb = 0.f;
+      if (ea < b) {
+        ca = col[ea];
+        va = val[ea];
+      }
+      if (eb < b) {
+        cb = col[eb];
+        vb = val[eb];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = __shfl(ca, (wg << 3) + u);
+        vs[u] = __shfl(va, (wg << 3) + u);
+        xs[u] = *reinterpret_cast<const float4*>(c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = __shfl(cb, (wg << 3) + u);
+        vs[8 + u] = __shfl(vb, (wg << 3) + u);
+        xs[8 + u] =
+            *reinterpret_cast<const float4*>(c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh);
+      }
+    }
+    emit(r, acc);
+  }
+  // empty rows: Y = beta * Y
+  for (int i = grp; i < nrows; i += kBlkGroups) {
+    if (s_rp[i] == s_rp[i + 1]) {
+      float* yp = y + (int64_t)(row0 + i) * ldy + ycol;
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (beta != 0.f) o = gmr::f4_scale(beta, *reinterpret_cast<const float4*>(yp));
+      *reinterpret_cast<float4*>(yp) = o;
+    }
+  }
+  __syncthreads();
+  // rows cut by group boundaries: the owner adds the continuations in group order
+  if (s_prow[grp][1] >= 0) {
+    const int rr = s_prow[grp][1];
+    float4 v = s_part[grp][1][sub];
+    for (int k = grp + 1; k < kBlkGroups && s_prow[k][0] == rr; ++k) v = gmr::f4_add(v, s_part[k][0][sub]);
+    float* yp = y + (int64_t)(row0 + rr) * ldy + ycol;
+    float4 o = gmr::f4_scale(alpha, v);
+    if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
+    *reinterpret_cast<float4*>(yp) = o;
+  }
+}
+
 }  // namespace
 
 extern "C" int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_nnz) {
   if (seg_nnz <= 0) return -1;
+  if (seg_nnz >= 512) return kPlanHdr + 2 * (blk_max_blocks(n_rows, nnz, seg_nnz) + 1);
   return kPlanHdr + 4 * plan_max_seg(n_rows, nnz, seg_nnz) + 3 * plan_max_fix(n_rows, nnz, seg_nnz);
 }
 
 extern "C" int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t seg_nnz) {
   if (seg_nnz <= 0) return -1;
+  if (seg_nnz >= 512) return 1;  // the blocked variant combines in LDS
   return 2 * ((nnz + seg_nnz - 1) / seg_nnz) + 2;
 }
 
@@ -236,7 +447,16 @@ extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_
                                    int32_t* plan, void* stream) {
   GMR_ARG(rowptr && plan, "null pointer");
   GMR_ARG(n_rows > 0 && n_rows < (1ll << 31) && nnz >= 0 && nnz < (1ll << 31), "bad size");
-  GMR_ARG(seg_nnz >= 64 && seg_nnz % 64 == 0, "seg_nnz must be a positive multiple of 64");
+  GMR_ARG((seg_nnz >= 64 && seg_nnz < 512 && seg_nnz % 64 == 0) || (seg_nnz >= 512 && seg_nnz <= 8192),
+          "seg_nnz: a multiple of 64 below 512 (segment plan) or 512..8192 (blocked plan)");
+  GMR_ARG(n_rows < (1 << 30), "n_rows too large");
+  if (seg_nnz >= 512) {
+    GMR_ARG(seg_nnz <= 8192, "blocked plans take seg_nnz <= 8192");
+    hipLaunchKernelGGL(blk_plan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, (int)n_rows, seg_nnz,
+                       (int)blk_max_blocks(n_rows, nnz, seg_nnz), plan);
+    GMR_LAUNCHED();
+    return GMR_OK;
+  }
   PlanView pv = plan_view(plan, n_rows, nnz, seg_nnz);
   hipLaunchKernelGGL(plan_build_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, (int)n_rows, seg_nnz,
                      pv);
@@ -244,11 +464,20 @@ extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_
   return GMR_OK;
 }
 
+extern "C" int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream) {
+  GMR_ARG(plan && host_hdr, "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemcpyAsync(host_hdr, plan, sizeof(int32_t) * kPlanHdr, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return gmr::hip_status(__func__, e);
+  return GMR_OK;
+}
+
 extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
                                 int64_t nnz, const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,
                                 const float* const* x_lo, const int64_t* ld_lo, const float* const* x_hi,
                                 const int64_t* ld_hi, int64_t split, float alpha, float beta, float* y, int64_t ldy,
-                                void* stream) {
+                                int32_t flags, void* stream) {
   GMR_ARG(rowptr && col && val && plan && y && x_lo && ld_lo, "null pointer");
   GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "n_blocks must be 1, 2 or 4");
   GMR_ARG(n_rows > 0 && nnz >= 0 && ldy >= 64 * n_blocks && ldy % 4 == 0, "bad shape");
@@ -265,31 +494,48 @@ extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const
     GMR_ARG(((uintptr_t)s.lo[b] & 15) == 0 && ((uintptr_t)s.hi[b] & 15) == 0, "sources must be 16-byte aligned");
     GMR_ARG(s.ld_lo[b] % 4 == 0 && s.ld_hi[b] % 4 == 0, "source ld must be a multiple of 4");
   }
+  hipStream_t st0 = (hipStream_t)stream;
+  if (seg_nnz >= 512) {
+    const int64_t mb = blk_max_blocks(n_rows, nnz, seg_nnz);
+    const int rp = 8 / (2 * n_blocks);
+    const dim3 grid((unsigned)(8 * ((mb + rp - 1) / rp)));
+    const size_t lds = sizeof(int) * (size_t)(seg_nnz + 1);
+    switch (n_blocks) {
+      case 1:
+        hipLaunchKernelGGL(spmm_blk_kernel<1>, grid, dim3(kBlkThreads), lds, st0, rowptr, col, val, plan, seg_nnz,
+                           (int)mb, s, alpha, beta, y, ldy);
+        break;
+      case 2:
+        hipLaunchKernelGGL(spmm_blk_kernel<2>, grid, dim3(kBlkThreads), lds, st0, rowptr, col, val, plan, seg_nnz,
+                           (int)mb, s, alpha, beta, y, ldy);
+        break;
+      default:
+        hipLaunchKernelGGL(spmm_blk_kernel<4>, grid, dim3(kBlkThreads), lds, st0, rowptr, col, val, plan, seg_nnz,
+                           (int)mb, s, alpha, beta, y, ldy);
+        break;
+    }
+    GMR_LAUNCHED();
+    return GMR_OK;
+  }
   PlanView pv = plan_view(const_cast<int32_t*>(plan), n_rows, nnz, seg_nnz);
   const int64_t max_seg = plan_max_seg(n_rows, nnz, seg_nnz);
-  const int grid = gmr::grid_for(max_seg, 4);
-  hipStream_t st = (hipStream_t)stream;
   const int64_t max_fix = plan_max_fix(n_rows, nnz, seg_nnz);
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = gmr::grid_for(max_seg, 4);
+  const int fix_grid = gmr::grid_for(max_fix * 16 * n_blocks, 256);
+  const bool fix = !(flags & GMR_SPMM_NO_SPLIT_ROWS);
+#define GMR_SPMM_LAUNCH(NBV)                                                                                       \
+  hipLaunchKernelGGL(spmm_seg_kernel<NBV>, dim3(grid), dim3(256), 0, st, col, val, pv, s, alpha, beta, y, ldy,     \
+                     partial);                                                                                   \
+  GMR_LAUNCHED();                                                                                                \
+  if (fix)                                                                                                       \
+    hipLaunchKernelGGL(spmm_fix_kernel<NBV>, dim3(fix_grid), dim3(256), 0, st, pv, alpha, beta, y, ldy, partial);
   switch (n_blocks) {
-    case 1:
-      hipLaunchKernelGGL(spmm_seg_kernel<1>, dim3(grid), dim3(256), 0, st, col, val, pv, s, alpha, beta, y, ldy, partial);
-      GMR_LAUNCHED();
-      hipLaunchKernelGGL(spmm_fix_kernel<1>, dim3(gmr::grid_for(max_fix * 16, 256)), dim3(256), 0, st, pv, alpha, beta,
-                         y, ldy, partial);
-      break;
-    case 2:
-      hipLaunchKernelGGL(spmm_seg_kernel<2>, dim3(grid), dim3(256), 0, st, col, val, pv, s, alpha, beta, y, ldy, partial);
-      GMR_LAUNCHED();
-      hipLaunchKernelGGL(spmm_fix_kernel<2>, dim3(gmr::grid_for(max_fix * 32, 256)), dim3(256), 0, st, pv, alpha, beta,
-                         y, ldy, partial);
-      break;
-    default:
-      hipLaunchKernelGGL(spmm_seg_kernel<4>, dim3(grid), dim3(256), 0, st, col, val, pv, s, alpha, beta, y, ldy, partial);
-      GMR_LAUNCHED();
-      hipLaunchKernelGGL(spmm_fix_kernel<4>, dim3(gmr::grid_for(max_fix * 64, 256)), dim3(256), 0, st, pv, alpha, beta,
-                         y, ldy, partial);
-      break;
+    case 1: GMR_SPMM_LAUNCH(1); break;
+    case 2: GMR_SPMM_LAUNCH(2); break;
+    default: GMR_SPMM_LAUNCH(4); break;
   }
+#undef GMR_SPMM_LAUNCH
   GMR_LAUNCHED();
   return GMR_OK;
 }

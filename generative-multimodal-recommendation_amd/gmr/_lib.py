@@ -26,7 +26,8 @@ SIGNATURES = {
     "gmr_spmm_plan_words": (I64, [I64, I64, I32]),
     "gmr_spmm_partial_rows": (I64, [I64, I64, I32]),
     "gmr_spmm_plan_build": (I32, [P, I64, I64, I32, P, P]),
-    "gmr_spmm_csr_f32": (I32, [P, P, P, I64, I64, P, I32, P, I32, P, P, P, P, I64, F32, F32, P, I64, P]),
+    "gmr_spmm_plan_info": (I32, [P, P, P]),
+    "gmr_spmm_csr_f32": (I32, [P, P, P, I64, I64, P, I32, P, I32, P, P, P, P, I64, F32, F32, P, I64, I32, P]),
     "gmr_bipartite_nnz": (I64, [I64, I64, I64, I32]),
     "gmr_bipartite_workspace_ints": (I64, [I64, I64]),
     "gmr_bipartite_symnorm_build": (I32, [I64, I64, P, P, I64, I32, F64, P, P, P, P, P]),
@@ -61,7 +62,9 @@ SIGNATURES = {
     "gmr_diff_qsample": (I32, [I32, I32, P, P, P, P, P, P, P, I64, P, I64, F32, I32, U64, U64, P, I64, P]),
     "gmr_diff_densify": (I32, [I32, I32, P, P, P, P, I64, P]),
     "gmr_diff_time_bias": (I32, [I32, I32, P, P, P, I64, I64, P, I32, P, P, P, P]),
-    "gmr_diff_loss_rows": (I32, [I32, I32, P, P, P, P, P, P, I64, F32, P, P, I32, P]),
+    "gmr_diff_loss_rows": (I32, [I32, I32, P, P, P, P, P, P, P, I64, F32, P, P, P, I32, P]),
+    "gmr_diff_sample_t_importance": (I32, [I32, I32, I32, P, P, F64, U64, U64, P, P, P]),
+    "gmr_diff_history_update": (I32, [I32, I32, I32, P, P, P, P, P]),
     "gmr_diff_gc_rows": (I32, [I32, P, P, P, P, I64, P, I64, F32, P, I64, P, P]),
     "gmr_diff_time_bwd": (I32, [I32, I32, I32, P, P, P, P, I64, I64, P, P, P, P, I32, P]),
     "gmr_mask_scores_f32": (I32, [I64, P, P, P, I64, F32, P]),

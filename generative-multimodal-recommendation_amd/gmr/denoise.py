@@ -30,6 +30,8 @@ class _Linear(nn.Module):
 
 
 class Denoiser(nn.Module):
+    PARAM_NAMES = ("emb_W", "emb_b", "W1", "b1", "W2", "b2")
+
     def __init__(self, n_items, hidden, emb_size, device, dropout=0.5, norm=False):
         super().__init__()
         if norm:
@@ -45,6 +47,11 @@ class Denoiser(nn.Module):
         self.out_layers = nn.ModuleList([_Linear(self.slab.parameter("W2"), self.slab.parameter("b2"))])
         self.device = device
         self._tb = None
+
+    def params(self):
+        """nn.Parameters in PARAM_NAMES order (views of the slab)."""
+        return [self.emb_layer.weight, self.emb_layer.bias, self.in_layers[0].weight, self.in_layers[0].bias,
+                self.out_layers[0].weight, self.out_layers[0].bias]
 
     @torch.no_grad()
     def init_like_reference(self):

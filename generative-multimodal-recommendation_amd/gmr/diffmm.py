@@ -421,7 +421,8 @@ class DiffMM(GeneralRecommender):
         den.output(h, o)
         K.gemm(o, feats, Z)                                                     # out @ feats
         _lib.call("gmr_diff_loss_rows", B, I, ptr(batch_users), ptr(self.user_ptr), ptr(self.user_items), ptr(tt),
-                  ptr(self._w_dev), ptr(o), o.stride(0), 1.0 / nr, ptr(w["mse"]), ptr(w["diff"]), 1, stream())
+                  ptr(self._w_dev), None, ptr(o), o.stride(0), 1.0 / nr, ptr(w["mse"]), ptr(w["diff"]), None, 1,
+                  stream())
         gsc = self.e_loss * 2.0 / (64.0 * nr)
         _lib.call("gmr_diff_gc_rows", B, ptr(batch_users), ptr(self.user_ptr), ptr(self.user_items),
                   ptr(item_embeds), item_embeds.stride(0), ptr(Z), 64, gsc, ptr(w["Gc"]), 64, ptr(w["gc"]), stream())

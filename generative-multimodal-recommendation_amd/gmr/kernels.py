@@ -106,10 +106,18 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
 
 
 # ----------------------------------------------------------------------------- SpMM
+# SpMM plan: 64..448 = segment plan (wave per <= seg_nnz segment), 512..8192 = blocked plan
+# (see include/gmr.h).  The segment plan at 128 measured fastest on the DiffMM graphs
+# (scripts/spmm_bench.py).
+SPMM_SEG_NNZ = 128
+SPMM_NO_SPLIT_ROWS = 1
+
+
 class CSR:
     """Device CSR (int32 rowptr/col, fp32 val) of an n x n matrix with its SpMM work plan."""
 
-    def __init__(self, rowptr, col, val, n_cols=None, seg_nnz=128, symmetric=True):
+    def __init__(self, rowptr, col, val, n_cols=None, seg_nnz=None, symmetric=True):
+        seg_nnz = SPMM_SEG_NNZ if seg_nnz is None else seg_nnz
         self.rowptr, self.col, self.val = rowptr, col, val
         self.n_rows = rowptr.numel() - 1
         self.n_cols = self.n_rows if n_cols is None else n_cols
@@ -122,6 +130,11 @@ class CSR:
         prow = _lib.load().gmr_spmm_partial_rows(self.n_rows, self.nnz, seg_nnz)
         self.partial = torch.empty((prow, 256), dtype=torch.float32, device=dev)
         _lib.call("gmr_spmm_plan_build", ptr(rowptr), self.n_rows, self.nnz, seg_nnz, ptr(self.plan), stream())
+        hdr = (ctypes.c_int32 * 4)()
+        _lib.call("gmr_spmm_plan_info", ptr(self.plan), hdr, stream())  # one sync per graph build
+        self.plan_header = tuple(hdr)
+        # segment plan without split rows: the combine pass is skipped
+        self.flags = SPMM_NO_SPLIT_ROWS if (seg_nnz < 512 and hdr[1] == 0) else 0
 
     def spmm(self, out, blocks, split=None, alpha=1.0, beta=0.0):
         """out = alpha * A @ X + beta * out; X = column blocks [(lo, hi), ...] of 64 columns each.
@@ -149,11 +162,11 @@ class CSR:
         with _Probe("spmm", (self.nnz, self.n_rows, self.n_cols, nb, beta != 0.0)):
             _lib.call("gmr_spmm_csr_f32", ptr(self.rowptr), ptr(self.col), ptr(self.val), self.n_rows, self.nnz,
                       ptr(self.plan), self.seg_nnz, ptr(self.partial), nb, lo, ldl, hi, ldh, split, float(alpha),
-                      float(beta), ptr(out), _ld(out), stream())
+                      float(beta), ptr(out), _ld(out), self.flags, stream())
         return out
 
 
-def bipartite_symnorm(n_users, n_items, user_ptr, user_items, self_loops, deg_eps, seg_nnz=128):
+def bipartite_symnorm(n_users, n_items, user_ptr, user_items, self_loops, deg_eps, seg_nnz=None):
     """Build the normalised (U+I)^2 bipartite adjacency on the device (graph.hip)."""
     lib = _lib.load()
     dev = user_ptr.device

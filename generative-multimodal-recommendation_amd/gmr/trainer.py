@@ -77,6 +77,7 @@ class Trainer:
         batches = list(train_data.batches(d))
         W, r = dist.world(), dist.rank()
         slabs = self.model.optim_slabs()
+        hook = getattr(self.model, "dp_step_end", None)  # per-global-step model state sync (DiffRec)
         for g in range(dist.global_steps(len(batches), W)):
             ids = dist.step_batches(g, len(batches), W)
             rows = [batches[i][1].numel() for i in ids] + [0] * (W - len(ids))
@@ -92,6 +93,8 @@ class Trainer:
             if W > 1:
                 for s_ in slabs:
                     dist.all_reduce_(s_.grad)
+            if hook is not None:
+                hook()
             self.optimizer.step()
         dist.all_reduce_(acc)
         total = float(acc[0].item())

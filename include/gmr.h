@@ -48,17 +48,28 @@ int gmr_zero(void* ptr, int64_t bytes, void* stream);
  * Replaces torch.spmm / torch.sparse.mm: models/diffmm.py:136,139,142,146,149,152,176,179,285;
  * lightgcn.py:120.  X is n_blocks (1,2,4) column blocks of 64 floats; block b reads source
  * row s from x_lo[b] + s*ld_lo[b] when s < split, else x_hi[b] + (s-split)*ld_hi[b]
- * (x_lo/x_hi/ld_* are HOST arrays of device pointers / strides).  A plan (built once per
- * matrix by gmr_spmm_plan_build) cuts rows into <= seg_nnz segments for load balance;
- * `partial` holds gmr_spmm_partial_rows(...) x (64*n_blocks) floats for hub rows. */
+ * (x_lo/x_hi/ld_* are HOST arrays of device pointers / strides).  A plan is built once per
+ * matrix by gmr_spmm_plan_build; seg_nnz selects the schedule:
+ *   64..448 (multiple of 64): segment plan — rows cut into <= seg_nnz segments, one wave per
+ *            segment, hub rows combined in segment order by a second pass that reads
+ *            `partial` (gmr_spmm_partial_rows(...) x (64*n_blocks) floats);
+ *   512..8192: blocked plan — whole rows packed into ~seg_nnz-nnz blocks, one 1024-thread
+ *            workgroup per block and XCD-pinned 32-column slice, rows cut by the in-block
+ *            nnz split combined in LDS (no second pass, `partial` unused).
+ * Both are deterministic.  flags: GMR_SPMM_NO_SPLIT_ROWS when the segment plan has no row
+ * longer than seg_nnz (gmr_spmm_plan_info header word 1 == 0): the combine pass is skipped. */
+#define GMR_SPMM_NO_SPLIT_ROWS 1
 int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_nnz);
 int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t seg_nnz);
 int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t seg_nnz, int32_t* plan,
                         void* stream);
+/* Copies the 4-word plan header to the host (synchronises the stream): segment plan
+ * {n_segments, n_split_rows, n_partials, 0}; blocked plan {n_blocks, 0, 0, seg_nnz}. */
+int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream);
 int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                      const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,
                      const float* const* x_lo, const int64_t* ld_lo, const float* const* x_hi, const int64_t* ld_hi,
-                     int64_t split, float alpha, float beta, float* y, int64_t ldy, void* stream);
+                     int64_t split, float alpha, float beta, float* y, int64_t ldy, int32_t flags, void* stream);
 
 /* ---------------------------------------------------------------- K11 graph construction
  * Symmetric-normalised bipartite adjacency (N = U + I) in CSR from a user->items CSR
@@ -160,8 +171,16 @@ int gmr_diff_time_bias(int32_t T, int32_t E, const float* emb_W, const float* em
                        int64_t col_off, const float* b1, int32_t H, float* EB, float* temb_out, float* emb_out,
                        void* stream);
 int gmr_diff_loss_rows(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
-                       const int32_t* t, const double* wtab, float* out, int64_t ld, float grad_scale,
-                       double* mse_out, double* diff_out, int32_t write_grad, void* stream);
+                       const int32_t* t, const double* wtab, const float* pt, float* out, int64_t ld, float grad_scale,
+                       double* mse_out, double* diff_out, double* loss_out, int32_t write_grad, void* stream);
+/* DiffRec importance sampling of t (models/diffrec.py:234-250): uniform t and pt = 1 until every
+ * t has hist_len recorded losses, then t ~ (1-up) sqrt(mean(hist^2))/sum + up/T, pt = p[t]*T. */
+int gmr_diff_sample_t_importance(int32_t B, int32_t T, int32_t hist_len, const double* hist, const int32_t* count,
+                                 double uniform_prob, uint64_t seed, uint64_t step, int32_t* t, float* pt,
+                                 void* stream);
+/* Lt_history / Lt_count update (models/diffrec.py:279-286), rows applied in batch order; t < 0 skips. */
+int gmr_diff_history_update(int32_t B, int32_t T, int32_t hist_len, const int32_t* t, const double* loss,
+                            double* hist, int32_t* count, void* stream);
 int gmr_diff_gc_rows(int32_t B, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
                      const float* item_embeds, int64_t ld_ie, const float* Z, int64_t ldz, float gscale, float* G,
                      int64_t ldg, double* gc_out, void* stream);

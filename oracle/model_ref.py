@@ -179,6 +179,40 @@ def diffmm_p_sample(w, tab, x0, emb_dim=10, steps=5):
     return x
 
 
+def diffrec_training_losses(w, tab, x0, t, noise, keep, pt, emb_dim):
+    """GaussianDiffusion.training_losses(reweight=True) with injected t/pt/noise/dropout —
+    diffrec.py:252-289: per row (SNR(t-1) - SNR(t), 1 at t=0) * mean_I (x0 - f(x_t))^2, and the
+    same divided by pt (the returned loss)."""
+    sa = torch.as_tensor(tab["sqrt_alphas_cumprod"][t], dtype=torch.float32)[:, None]
+    s1 = torch.as_tensor(tab["sqrt_one_minus_alphas_cumprod"][t], dtype=torch.float32)[:, None]
+    xt = sa * x0 + s1 * noise
+    out = denoise(w, xt, torch.as_tensor(t), emb_dim, keep=keep)
+    mse = ((x0 - out) ** 2).mean(1)
+    wl = torch.as_tensor(snr_weight(tab, t), dtype=torch.float32) * mse
+    return wl, wl / torch.as_tensor(pt)
+
+
+def lt_history_update(hist, count, t, loss):
+    """Lt_history / Lt_count update, sample by sample in batch order — diffrec.py:279-286."""
+    hist, count = hist.copy(), count.copy()
+    n = hist.shape[1]
+    for ti, lv in zip(np.asarray(t), np.asarray(loss)):
+        if count[ti] < n:
+            hist[ti, count[ti]] = lv
+            count[ti] += 1
+        else:
+            hist[ti, :-1] = hist[ti, 1:].copy()
+            hist[ti, -1] = lv
+    return hist, count
+
+
+def importance_pt_all(hist, uniform_prob=0.001):
+    """pt_all of sample_timesteps('importance') — diffrec.py:238-245 (fp64)."""
+    lt = np.sqrt(np.mean(hist ** 2, axis=-1))
+    p = lt / lt.sum()
+    return p * (1 - uniform_prob) + uniform_prob / len(p)
+
+
 def diffrec_p_sample(w, tab, x0, emb_dim, steps):
     """DiffRec p_sample (x0 mean type, eval mode) — diffrec.py:191-221, 291-310."""
     return diffmm_p_sample(w, tab, x0, emb_dim, steps)

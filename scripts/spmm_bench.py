@@ -1,0 +1,82 @@
+"""SpMM microbenchmark on the baby-shaped DiffMM graphs (HIP events, 1 process).
+
+python scripts/spmm_bench.py [--segs 128,64,32] [--reps 50]
+Times gmr_spmm_csr_f32 for norm_adj (no self loops) and a rebuilt UI graph (top-1 per user +
+self loops) at 1, 2 and 4 column blocks, per plan segment length, checks every variant against
+the first, and prints GB/s with the SURVEY.md 8(d) byte formula.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "generative-multimodal-recommendation_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from gmr import kernels as K  # noqa: E402
+from gmr.configurator import Config  # noqa: E402
+from gmr.dataloader import TrainDataLoader  # noqa: E402
+from gmr.synthetic import make_dataset  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--segs", default="128,1024")
+    ap.add_argument("--reps", type=int, default=50)
+    args = ap.parse_args()
+    segs = [int(x) for x in args.segs.split(",")]
+    cfg = Config("DiffMM", "baby", {"synthetic": "baby"})
+    ds = make_dataset(cfg, "baby", seed=0)
+    tr, _, _ = ds.split()
+    tl = TrainDataLoader(cfg, tr, batch_size=2048, shuffle=True)
+    U, I = ds.user_num, ds.item_num
+    N = U + I
+    dev = "cuda"
+    uptr = torch.as_tensor(tl.uptr_np).to(dev)
+    uit = torch.as_tensor(tl.uitems_np).to(dev)
+    rng = np.random.default_rng(0)
+    top1 = torch.as_tensor(rng.integers(0, I, U).astype(np.int32)).to(dev)
+    graphs = {}
+    for seg in segs:
+        graphs[("norm_adj", seg)] = K.bipartite_symnorm(U, I, uptr, uit, self_loops=False, deg_eps=1e-7, seg_nnz=seg)
+        graphs[("ui_top1", seg)] = K.bipartite_symnorm(U, I, torch.arange(U + 1, dtype=torch.int32, device=dev), top1,
+                                                       self_loops=True, deg_eps=0.0, seg_nnz=seg)
+    X = torch.randn(N, 256, device=dev)
+    t = torch.empty_like(X)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(args.reps):
+        t.copy_(X)
+    e.record()
+    torch.cuda.synchronize()
+    us = 1e3 * s.elapsed_time(e) / args.reps
+    print(f"copy N x 256 fp32: {us:.1f} us, {2 * X.numel() * 4 / us / 1e3:.0f} GB/s")
+    print(f"{'graph':10s} {'nnz':>7s} {'nb':>2s} {'seg':>4s} {'us':>8s} {'GB/s':>7s} {'frac':>6s} max|diff|")
+    for name in ("norm_adj", "ui_top1"):
+        for nb in (1, 2, 4):
+            ref = None
+            for seg in segs:
+                g = graphs[(name, seg)]
+                Y = torch.empty(N, 64 * nb, device=dev)
+                blocks = [(X[:, 64 * b:64 * b + 64],) for b in range(nb)]
+                for _ in range(3):
+                    g.spmm(Y, blocks)
+                s.record()
+                for _ in range(args.reps):
+                    g.spmm(Y, blocks)
+                e.record()
+                torch.cuda.synchronize()
+                us = 1e3 * s.elapsed_time(e) / args.reps
+                d = 64 * nb
+                byts = 8.0 * g.nnz + 4.0 * (N + 1) + 4.0 * d * N * 2
+                gbs = byts / us / 1e3
+                if ref is None:
+                    ref = Y.clone()
+                diff = (Y - ref).abs().max().item()
+                print(f"{name:10s} {g.nnz:7d} {nb:2d} {seg:4d} {us:8.2f} {gbs:7.0f} {gbs / 8000:6.3f} {diff:.2e}")
+
+
+if __name__ == "__main__":
+    main()

@@ -357,6 +357,41 @@ def gen_diffrec(ref, tmp):
         t = torch.as_tensor(rng.integers(0, T, size=U))
         out["fwd_t"] = t.numpy()
         out["fwd_out"] = dnn(torch.from_numpy(x0), t).numpy()
+    # training_losses(reweight=True) while the Lt histories fill (uniform t): draws replayed from
+    # the seed (randint -> randn_like -> dropout bernoulli, diffrec.py:232-262, :80)
+    dnn.train()
+    xs = torch.from_numpy(x0)
+    steps = []
+    for s in range(12):
+        if bool((gd.Lt_count == gd.history_num_per_term).all()):
+            break
+        torch.manual_seed(100 + s)
+        for p_ in dnn.parameters():
+            p_.grad = None
+        terms = gd.training_losses(dnn, xs, reweight=True)
+        terms["loss"].mean().backward()
+        torch.manual_seed(100 + s)
+        ts = torch.randint(0, T, (U,)).long()
+        noise = torch.randn_like(xs)
+        keep = torch.empty_like(xs).bernoulli_(0.5)
+        rec = {"t": ts.numpy(), "noise": noise.numpy(), "keep": keep.numpy(),
+               "loss": terms["loss"].detach().numpy().astype(np.float64),
+               "hist": gd.Lt_history.numpy().copy(), "count": gd.Lt_count.numpy().astype(np.int64).copy()}
+        if s == 0:
+            for n, p_ in dnn.named_parameters():
+                rec["g_" + n.replace(".", "_")] = p_.grad.numpy().copy()
+        steps.append(rec)
+    out["train_steps"] = len(steps)
+    for s, rec in enumerate(steps):
+        for k, v in rec.items():
+            out[f"train{s}_{k}"] = v
+    # importance sampling once every history is full (diffrec.py:234-250): pt = pt_all[t] * T
+    assert bool((gd.Lt_count == gd.history_num_per_term).all())
+    torch.manual_seed(7)
+    it, ipt = gd.sample_timesteps(4000, torch.device("cpu"), "importance")
+    out["imp_hist"] = gd.Lt_history.numpy().copy()
+    out["imp_t"] = it.numpy()
+    out["imp_pt"] = ipt.numpy()
     return out
 
 

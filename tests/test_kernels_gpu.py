@@ -67,16 +67,23 @@ def test_bipartite_build_large_hubs(K):
     assert np.array_equal(csr.val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
 
 
+SPMM_SEGS = [64, 128, 512, 2048]  # segment plans (short, default) and blocked plans
+
+
+@pytest.mark.parametrize("seg", SPMM_SEGS)
 @pytest.mark.parametrize("nb", [1, 2, 4])
-def test_spmm_vs_oracle(K, nb):
+def test_spmm_vs_oracle(K, nb, seg):
     rng = _rng(2)
     U, I = 2500, 900
-    rows = np.repeat(np.arange(U), rng.integers(1, 20, size=U))
+    deg = rng.integers(1, 20, size=U)
+    deg[::97] = 0  # users without interactions -> empty rows
+    rows = np.repeat(np.arange(U), deg)
     p = 1.0 / np.arange(1, I + 1) ** 1.1
-    cols = rng.choice(I, size=rows.size, p=p / p.sum())  # hub items -> multi-segment rows
+    cols = rng.choice(I, size=rows.size, p=p / p.sum())  # hub items (rows > 1024 nnz) and never-seen items
     rp, col, val = graph_ref.norm_adj_csr(U, I, rows, cols)
+    assert np.diff(rp).max() > 1024 and (np.diff(rp) == 0).any()
     N = U + I
-    csr = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=64)
+    csr = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=seg)
     X = rng.standard_normal((N, 64 * nb)).astype(np.float32)
     Y0 = rng.standard_normal((N, 64 * nb)).astype(np.float32)
     Xd, Yd = _dev(X), _dev(Y0)
@@ -87,13 +94,14 @@ def test_spmm_vs_oracle(K, nb):
     np.testing.assert_allclose(Yd.cpu().numpy(), want, rtol=1e-5, atol=1e-5)
 
 
-def test_spmm_split_sources(K):
+@pytest.mark.parametrize("seg", SPMM_SEGS)
+def test_spmm_split_sources(K, seg):
     rng = _rng(3)
     U, I = 300, 200
     rows = np.repeat(np.arange(U), 6)
     cols = rng.integers(0, I, size=rows.size)
     rp, col, val = graph_ref.norm_adj_csr(U, I, rows, cols)
-    csr = K.CSR(_dev(rp), _dev(col), _dev(val))
+    csr = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=seg)
     uE = rng.standard_normal((U, 64)).astype(np.float32)
     F = rng.standard_normal((I, 128)).astype(np.float32)
     uEd, Fd = _dev(uE), _dev(F)

@@ -176,6 +176,41 @@ def test_diffrec_psample(golden):
     np.testing.assert_allclose(ps.numpy(), g["psample"], rtol=1e-4, atol=1e-6)
 
 
+def _diffrec_w(g, grad=False):
+    w = {"emb_W": g["dnn_emb_layer_weight"], "emb_b": g["dnn_emb_layer_bias"], "W1": g["dnn_in_layers_0_weight"],
+         "b1": g["dnn_in_layers_0_bias"], "W2": g["dnn_out_layers_0_weight"], "b2": g["dnn_out_layers_0_bias"]}
+    return {k: torch.tensor(v, requires_grad=grad) for k, v in w.items()}
+
+
+def test_diffrec_training_losses_and_history(golden):
+    """training_losses(reweight=True) rows, gradients and the Lt history/count after each step."""
+    g = golden("diffrec_tiny")
+    T = int(g["T"])
+    tab = model_ref.diffrec_schedule(steps=T)
+    x0 = torch.as_tensor(g["x0"])
+    hist = np.zeros((T, 10))
+    count = np.zeros(T, np.int64)
+    for s in range(int(g["train_steps"])):
+        w = _diffrec_w(g, grad=(s == 0))
+        t = g[f"train{s}_t"]
+        wl, loss = model_ref.diffrec_training_losses(w, tab, x0, t, torch.as_tensor(g[f"train{s}_noise"]),
+                                                     torch.as_tensor(g[f"train{s}_keep"]), np.ones(len(t), np.float32),
+                                                     int(g["E"]))
+        np.testing.assert_allclose(loss.detach().numpy(), g[f"train{s}_loss"], rtol=1e-5, atol=1e-9)
+        if s == 0:
+            loss.mean().backward()
+            for k, n in [("emb_W", "emb_layer_weight"), ("emb_b", "emb_layer_bias"), ("W1", "in_layers_0_weight"),
+                         ("b1", "in_layers_0_bias"), ("W2", "out_layers_0_weight"), ("b2", "out_layers_0_bias")]:
+                want = g[f"train0_g_{n}"]  # fp32 reassociation: atol relative to the tensor's scale
+                np.testing.assert_allclose(w[k].grad.numpy(), want, rtol=1e-4, atol=1e-5 * np.abs(want).max())
+        # the history holds the reference's own fp32 losses: feed those (bit-exact bookkeeping)
+        hist, count = model_ref.lt_history_update(hist, count, t, g[f"train{s}_loss"])
+        np.testing.assert_array_equal(count, g[f"train{s}_count"])
+        np.testing.assert_array_equal(hist, g[f"train{s}_hist"])
+    pt_all = model_ref.importance_pt_all(g["imp_hist"])
+    np.testing.assert_allclose(pt_all[g["imp_t"]] * T, g["imp_pt"], rtol=1e-12)
+
+
 def test_vbpr(golden):
     g = golden("vbpr_tiny")
     p = {k[2:]: torch.tensor(g[k], requires_grad=True) for k in g if k.startswith("p_")}
