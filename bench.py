@@ -69,7 +69,7 @@ def summarize_probe(p):
         ms = [s.elapsed_time(e) for s, e, _ in recs]
         tot_ms = float(np.sum(ms))
         if tag == "gemm":
-            work = sum(2.0 * M * N * K for M, N, K in (r[2] for r in recs))
+            work = sum(2.0 * r[2][0] * r[2][1] * r[2][2] for r in recs)
             achieved = work / (tot_ms * 1e-3) / 1e12
             out[tag] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": round(achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
@@ -88,6 +88,22 @@ def summarize_probe(p):
                         "avg_us": round(1e3 * tot_ms / len(recs), 2), "total_ms": round(tot_ms, 3),
                         "algorithmic_per_launch": byts / len(recs), "kernel": "spmm_seg_kernel (CSR, wave/segment)"}
     return out
+
+
+def report_shapes(p):
+    """Per-shape breakdown of one probed epoch (GMR_PROBE_REPORT=1), to stderr."""
+    for tag, recs in p.items():
+        groups = {}
+        for s_, e_, meta in recs:
+            groups.setdefault(meta, []).append(s_.elapsed_time(e_))
+        rows = sorted(groups.items(), key=lambda kv: -sum(kv[1]))
+        log(f"--- {tag}: {len(recs)} launches, {sum(sum(v) for v in groups.values()):.2f} ms")
+        for meta, ms in rows[:25]:
+            tot = sum(ms)
+            extra = ""
+            if tag == "gemm":
+                extra = f"{2.0 * meta[0] * meta[1] * meta[2] * len(ms) / (tot * 1e-3) / 1e12:7.1f} TF/s"
+            log(f"  {str(meta):44s} n={len(ms):4d} total={tot:8.2f} ms avg={1e3 * tot / len(ms):8.1f} us {extra}")
 
 
 def cpu_baseline(model, tl, budget_s=30.0):
@@ -192,7 +208,10 @@ def main():
         trainer._train_epoch(tl, i)
         torch.cuda.synchronize()
         if i == args.warmup - 1:
-            probe_all = summarize_probe(K.probe_end())
+            raw = K.probe_end()
+            probe_all = summarize_probe(raw)
+            if os.environ.get("GMR_PROBE_REPORT"):
+                report_shapes(raw)
         log(f"warmup epoch {i}: {time.time() - t0:.3f}s")
     dominant = max(probe_all, key=lambda k: probe_all[k]["total_ms"]) if probe_all else "gemm"
 

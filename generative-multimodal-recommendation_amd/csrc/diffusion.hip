@@ -400,6 +400,46 @@ __global__ void __launch_bounds__(1024) lt_update_kernel(int B, int T, int Hn, c
   }
 }
 
+// 32x32 LDS-tiled transpose: out[c][r] = in[r][c] (rows x cols, leading dims ldi / ldo).
+__global__ void __launch_bounds__(256) transpose_kernel(int64_t rows, int64_t cols, const float* __restrict__ in,
+                                                        int64_t ldi, float* __restrict__ out, int64_t ldo) {
+  __shared__ float t[32][33];
+  const int64_t r0 = (int64_t)blockIdx.y * 32, c0 = (int64_t)blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int64_t r = r0 + ty + k, c = c0 + tx;
+    t[ty + k][tx] = (r < rows && c < cols) ? in[r * ldi + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int64_t c = c0 + ty + k, r = r0 + tx;
+    if (c < cols && r < rows) out[c * ldo + r] = t[tx][ty + k];
+  }
+}
+
+// First p_sample step on a binary x0: h[b] = tanh(sum_{i in items(b)} W1T[i] + EB), the sparse
+// form of tanh(x0 @ W1[:, :I]^T + EB[t]) (x0 rows hold ~6 ones out of I).  One block per row,
+// float4 columns; the items are summed in ascending order.
+__global__ void __launch_bounds__(256) sparse_hidden_kernel(int B, int H, const int* __restrict__ users,
+                                                            const int* __restrict__ uptr,
+                                                            const int* __restrict__ uitems,
+                                                            const float* __restrict__ W1T, int64_t ldw,
+                                                            const float* __restrict__ eb, float* __restrict__ h,
+                                                            int64_t ldh) {
+  const int b = blockIdx.x;
+  const int u = users[b];
+  const int beg = uptr[u], end = uptr[u + 1];
+  for (int c = threadIdx.x * 4; c < H; c += 1024) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e = beg; e < end; ++e) acc = gmr::f4_add(acc, *reinterpret_cast<const float4*>(W1T + (int64_t)uitems[e] * ldw + c));
+    const float4 bb = *reinterpret_cast<const float4*>(eb + c);
+    float4 o = make_float4(tanhf(acc.x + bb.x), tanhf(acc.y + bb.y), tanhf(acc.z + bb.z), tanhf(acc.w + bb.w));
+    *reinterpret_cast<float4*>(h + (int64_t)b * ldh + c) = o;
+  }
+}
+
 }  // namespace
 
 extern "C" int gmr_diff_sample_t(int32_t B, int32_t T, uint64_t seed, uint64_t step, int32_t* t, void* stream) {
@@ -455,6 +495,27 @@ extern "C" int gmr_diff_densify(int32_t B, int32_t I, const int32_t* users, cons
   hipLaunchKernelGGL(densify_zero_kernel, dim3(gmr::grid_for((int64_t)B * I, 256)), dim3(256), 0, st, B, I, x, ldx);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(densify_ones_kernel, dim3(B), dim3(64), 0, st, B, users, user_ptr, user_items, x, ldx);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_transpose_f32(int64_t rows, int64_t cols, const float* in, int64_t ldi, float* out, int64_t ldo,
+                                 void* stream) {
+  GMR_ARG(in && out && rows > 0 && cols > 0 && ldi >= cols && ldo >= rows, "bad args");
+  dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32));
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, in, ldi, out, ldo);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_diff_sparse_hidden(int32_t B, int32_t H, const int32_t* users, const int32_t* user_ptr,
+                                      const int32_t* user_items, const float* W1T, int64_t ldw, const float* eb,
+                                      float* h, int64_t ldh, void* stream) {
+  GMR_ARG(users && user_ptr && user_items && W1T && eb && h && B > 0 && H > 0, "bad args");
+  GMR_ARG(H % 4 == 0 && ldw % 4 == 0 && ldh % 4 == 0, "H and the leading dims must be multiples of 4");
+  GMR_ARG(((uintptr_t)W1T & 15) == 0 && ((uintptr_t)eb & 15) == 0 && ((uintptr_t)h & 15) == 0, "16-byte alignment");
+  hipLaunchKernelGGL(sparse_hidden_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, H, users, user_ptr,
+                     user_items, W1T, ldw, eb, h, ldh);
   GMR_LAUNCHED();
   return GMR_OK;
 }

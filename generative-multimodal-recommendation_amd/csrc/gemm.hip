@@ -35,32 +35,53 @@ struct Epi {
   const float* rv2;
 };
 
-__device__ __forceinline__ float epi_apply(const Epi& e, float acc, int64_t m, int64_t n, float* cp) {
+// Per-element inputs of the epilogue, loaded in one batch before any store (the p_sample
+// posterior runs in place, C == aux, so a load/compute/store chain per element would make every
+// element a dependent memory round trip).
+__device__ __forceinline__ bool epi_reads_x(const Epi& e) {
+  return e.kind == GMR_EPI_POSTERIOR || e.kind == GMR_EPI_DTANH || e.kind == GMR_EPI_ROWSCALE_AUX ||
+         ((e.kind == GMR_EPI_NONE || e.kind == GMR_EPI_BIAS) && e.beta != 0.f);
+}
+__device__ __forceinline__ const float* epi_x_ptr(const Epi& e, float* C, int64_t ldc, int64_t m, int64_t n) {
+  return (e.kind == GMR_EPI_NONE || e.kind == GMR_EPI_BIAS) ? C + m * ldc + n : e.aux + m * e.ld_aux + n;
+}
+// r1 / r2: the POSTERIOR row coefficients (rv1[m] or slope, rv2[m] or beta), ROWSCALE_AUX's rv1[m]
+__device__ __forceinline__ float epi_fin(const Epi& e, float acc, float b, float x, float r1, float r2) {
   float v = e.alpha * acc;
-  float b = 0.f;
-  if (e.bias) b = e.bias[(e.bias_row ? (int64_t)e.bias_row[m] : 0) * e.ld_bias + n];
   switch (e.kind) {
     case GMR_EPI_NONE:
-      return e.beta != 0.f ? fmaf(e.beta, *cp, v) : v;
+      return e.beta != 0.f ? fmaf(e.beta, x, v) : v;
     case GMR_EPI_BIAS:
       v += b;
-      return e.beta != 0.f ? fmaf(e.beta, *cp, v) : v;
+      return e.beta != 0.f ? fmaf(e.beta, x, v) : v;
     case GMR_EPI_BIAS_TANH:
       return tanhf(v + b);
     case GMR_EPI_LEAKY:
       v += b;
       return v > 0.f ? v : v * e.slope;
-    case GMR_EPI_POSTERIOR:  // scalar coefficients (slope, beta) when the row vectors are absent
-      return (e.rv1 ? e.rv1[m] : e.slope) * (v + b) + (e.rv2 ? e.rv2[m] : e.beta) * e.aux[m * e.ld_aux + n];
-    case GMR_EPI_DTANH: {
-      float h = e.aux[m * e.ld_aux + n];
-      return v * (1.f - h * h);
-    }
+    case GMR_EPI_POSTERIOR:
+      return r1 * (v + b) + r2 * x;
+    case GMR_EPI_DTANH:
+      return v * (1.f - x * x);
     case GMR_EPI_ROWSCALE_AUX:
-      return v + b + e.rv1[m] * e.aux[m * e.ld_aux + n];
+      return v + b + r1 * x;
     default:
       return v;
   }
+}
+__device__ __forceinline__ float epi_r1(const Epi& e, int64_t m) {
+  if (e.kind == GMR_EPI_POSTERIOR) return e.rv1 ? e.rv1[m] : e.slope;
+  if (e.kind == GMR_EPI_ROWSCALE_AUX) return e.rv1[m];
+  return 0.f;
+}
+__device__ __forceinline__ float epi_r2(const Epi& e, int64_t m) {
+  return e.kind == GMR_EPI_POSTERIOR ? (e.rv2 ? e.rv2[m] : e.beta) : 0.f;
+}
+// scalar form (split-K reduce)
+__device__ __forceinline__ float epi_apply(const Epi& e, float acc, int64_t m, int64_t n, float* C, int64_t ldc) {
+  const float b = e.bias ? e.bias[(e.bias_row ? (int64_t)e.bias_row[m] : 0) * e.ld_bias + n] : 0.f;
+  const float x = epi_reads_x(e) ? *epi_x_ptr(e, C, ldc, m, n) : 0.f;
+  return epi_fin(e, acc, b, x, epi_r1(e, m), epi_r2(e, m));
 }
 
 // Loads a BK-deep tile slice of an operand into registers (float4 granules).
@@ -224,22 +245,57 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t
   }
 
   // epilogue: acc element e of lane -> row (e&3) + 8(e>>2) + 4h, col l32
+  if (ws) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn * WTN + j * 32 + l32;
+        if (n >= N) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int64_t m = m0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (m < M) ws[((int64_t)blockIdx.z * M + m) * N + n] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+  const bool rx = epi_reads_x(epi);
+  if (!rx && !epi.bias_row && !epi.rv1 && !epi.rv2) {
+    // no per-element inputs: one bias value per column at most
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn * WTN + j * 32 + l32;
+        if (n >= N) continue;
+        const float b = epi.bias ? epi.bias[n] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int64_t m = m0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (m < M) C[m * ldc + n] = epi_fin(epi, acc[i][j][e], b, 0.f, 0.f, 0.f);
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int64_t n = n0 + wn * WTN + j * 32 + l32;
       if (n >= N) continue;
+      float bv[16], xv[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {  // all loads of the 16 elements first (no store in between)
+        const int64_t m = m0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const bool ok = m < M;
+        bv[e] = (epi.bias && ok) ? epi.bias[(epi.bias_row ? (int64_t)epi.bias_row[m] : 0) * epi.ld_bias + n] : 0.f;
+        xv[e] = (rx && ok) ? *epi_x_ptr(epi, C, ldc, m, n) : 0.f;
+      }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int64_t m = m0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (m >= M) continue;
-        if (ws) {
-          ws[((int64_t)blockIdx.z * M + m) * N + n] = acc[i][j][e];
-        } else {
-          float* cp = C + m * ldc + n;
-          *cp = epi_apply(epi, acc[i][j][e], m, n, cp);
-        }
+        if (m < M) C[m * ldc + n] = epi_fin(epi, acc[i][j][e], bv[e], xv[e], epi_r1(epi, m), epi_r2(epi, m));
       }
     }
 }
@@ -249,10 +305,19 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const flo
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= M * N) return;
   const int64_t m = idx / N, n = idx % N;
+  const int64_t slab = M * N;
   float s = 0.f;
-  for (int z = 0; z < splits; ++z) s += ws[(int64_t)z * M * N + idx];
-  float* cp = C + m * ldc + n;
-  *cp = epi_apply(epi, s, m, n, cp);
+  int z = 0;
+  for (; z + 4 <= splits; z += 4) {  // four independent slab loads in flight, summed in slab order
+    const float a0 = ws[(int64_t)z * slab + idx], a1 = ws[(int64_t)(z + 1) * slab + idx];
+    const float a2 = ws[(int64_t)(z + 2) * slab + idx], a3 = ws[(int64_t)(z + 3) * slab + idx];
+    s += a0;
+    s += a1;
+    s += a2;
+    s += a3;
+  }
+  for (; z < splits; ++z) s += ws[(int64_t)z * slab + idx];
+  C[m * ldc + n] = epi_apply(epi, s, m, n, C, ldc);
 }
 
 template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC>

@@ -88,6 +88,22 @@ class Denoiser(nn.Module):
     def W1x(self):
         return self.slab.view("W1")[:, :self.I]
 
+    def refresh_w1t(self):
+        """W1T = W1[:, :I]^T (I x H), the gather-friendly copy used by hidden_sparse; call after
+        the weights change (once per graph rebuild / prediction pass)."""
+        if getattr(self, "_w1t", None) is None:
+            self._w1t = torch.empty((self.I, _r4(self.H)), device=self.device)[:, :self.H]
+        _lib.call("gmr_transpose_f32", self.H, self.I, ptr(self.slab.view("W1")), self.ld_w1, ptr(self._w1t),
+                  self._w1t.stride(0), stream())
+        return self._w1t
+
+    def hidden_sparse(self, users, user_ptr, user_items, h, eb_row):
+        """h = tanh(x0 @ W1[:, :I]^T + eb_row) for binary x0 rows given as the users' item lists
+        (the first p_sample step, whose input is the interaction history itself)."""
+        _lib.call("gmr_diff_sparse_hidden", users.numel(), self.H, ptr(users), ptr(user_ptr), ptr(user_items),
+                  ptr(self._w1t), self._w1t.stride(0), ptr(eb_row), ptr(h), h.stride(0), stream())
+        return h
+
     # ------------------------------------------------------------------ forward pieces
     def hidden(self, x, h, EB, t_rows=None, t_const=None):
         """h = tanh(x @ W1[:, :I]^T + EB[t])."""

@@ -431,7 +431,7 @@ class DiffMM(GeneralRecommender):
         return w["diff"][:B], w["gc"][:B]
 
     @torch.no_grad()
-    def p_sample_topk(self, den, users_lo, users_hi, out_topk, k, x_out=None):
+    def p_sample_topk(self, den, users_lo, users_hi, out_topk, k, x_out=None, w1t_fresh=False):
         """p_sample(x0, steps=0, no noise) for users [lo, hi) + per-row top-k (trainer.py:545-546)."""
         B = users_hi - users_lo
         w = self._dwork(min(B, 8192))
@@ -442,9 +442,14 @@ class DiffMM(GeneralRecommender):
         _lib.call("gmr_diff_densify", B, I, ptr(users), ptr(self.user_ptr), ptr(self.user_items), ptr(x),
                   x.stride(0), stream())
         EB, _, _ = den.time_bias(T)
+        if not w1t_fresh:
+            den.refresh_w1t()
         xi = x[:, :I]
         for i in reversed(range(T)):
-            den.hidden(xi, h, EB, t_const=i)
+            if i == T - 1:  # the first model call sees the binary history: sparse hidden layer
+                den.hidden_sparse(users, self.user_ptr, self.user_items, h, EB[i])
+            else:
+                den.hidden(xi, h, EB, t_const=i)
             den.posterior_step(h, xi, float(np.float32(self.tables["c1"][i])), float(np.float32(self.tables["c2"][i])))
         if x_out is not None:
             x_out.copy_(xi)
@@ -465,8 +470,9 @@ class DiffMM(GeneralRecommender):
         uitems = torch.empty(U * k, dtype=torch.int32, device=dev)
         graphs = []
         for den in (self.denoise_model_image, self.denoise_model_text):
+            den.refresh_w1t()
             for lo in range(lo_r, hi_r, chunk):
-                self.p_sample_topk(den, lo, min(hi_r, lo + chunk), topk, k)
+                self.p_sample_topk(den, lo, min(hi_r, lo + chunk), topk, k, w1t_fresh=True)
             dist.all_gather_rows_(topk, size)
             K.topk_to_user_csr(topk[:U], uptr, uitems)
             g = K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0)

@@ -207,9 +207,13 @@ class DiffRec(GeneralRecommender):
         _lib.call("gmr_diff_densify", B, I, ptr(users), ptr(self.user_ptr), ptr(self.user_items), ptr(x),
                   x.stride(0), stream())
         EB, _, _ = den.time_bias(T)
+        den.refresh_w1t()
         xi = x[:, :I]
         for i in reversed(range(T)):
-            den.hidden(xi, h, EB, t_const=i)
+            if i == T - 1:  # binary history input: sparse hidden layer
+                den.hidden_sparse(users, self.user_ptr, self.user_items, h, EB[i])
+            else:
+                den.hidden(xi, h, EB, t_const=i)
             den.posterior_step(h, xi, float(np.float32(self.tables["c1"][i])),
                                float(np.float32(self.tables["c2"][i])))
         return xi

@@ -97,7 +97,7 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
         if t.dtype != torch.float32:
             raise TypeError("gemm is fp32")
     ws = workspace(16 * M * N, C.device)
-    with _Probe("gemm", (M, N, K)):
+    with _Probe("gemm", (M, N, K, int(trans_a), int(trans_b), epi)):
         _lib.call("gmr_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), ptr(A), _ld(A), ptr(B), _ld(B),
                   float(beta), ptr(C), _ld(C), epi, ptr(bias), ptr(bias_row), ld_bias, ptr(aux),
                   _ld(aux) if aux is not None else 0, ptr(rv1), ptr(rv2), float(slope), tile, split_k, ptr(ws),

@@ -173,6 +173,15 @@ int gmr_diff_time_bias(int32_t T, int32_t E, const float* emb_W, const float* em
 int gmr_diff_loss_rows(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
                        const int32_t* t, const double* wtab, const float* pt, float* out, int64_t ld, float grad_scale,
                        double* mse_out, double* diff_out, double* loss_out, int32_t write_grad, void* stream);
+/* out[c][r] = in[r][c] for a rows x cols fp32 matrix. */
+int gmr_transpose_f32(int64_t rows, int64_t cols, const float* in, int64_t ldi, float* out, int64_t ldo,
+                      void* stream);
+/* First p_sample step on binary x0 rows (models/diffmm.py:408-426 with steps = 0, the loop's
+ * first model call): h[b] = tanh(sum over the user's items i of W1T[i, :] + eb), W1T = W1[:, :I]^T
+ * (I x H) — the sparse form of the hidden GEMM. */
+int gmr_diff_sparse_hidden(int32_t B, int32_t H, const int32_t* users, const int32_t* user_ptr,
+                           const int32_t* user_items, const float* W1T, int64_t ldw, const float* eb, float* h,
+                           int64_t ldh, void* stream);
 /* DiffRec importance sampling of t (models/diffrec.py:234-250): uniform t and pt = 1 until every
  * t has hist_len recorded losses, then t ~ (1-up) sqrt(mean(hist^2))/sum + up/T, pt = p[t]*T. */
 int gmr_diff_sample_t_importance(int32_t B, int32_t T, int32_t hist_len, const double* hist, const int32_t* count,

@@ -15,21 +15,24 @@ from gmr import kernels as K  # noqa: E402
 
 # name, M, N, K, trans_a, trans_b, calls per epoch
 SHAPES = [
-    ("psample_h (NT)", 8192, 1000, 7050, 0, 1, 30),
-    ("psample_out (NT)", 8192, 7050, 1000, 0, 1, 30),
+    ("square4096 (NT)", 4096, 4096, 4096, 0, 1, 0),
+    ("square8192 (NT)", 8192, 8192, 8192, 0, 1, 0),
+    ("psample_h19k (NT)", 19445, 1000, 7050, 0, 1, 10),
+    ("psample_out19k (NT)", 19445, 7050, 1000, 0, 1, 10),
+    ("psample_h (NT)", 8192, 1000, 7050, 0, 1, 20),
+    ("psample_out (NT)", 8192, 7050, 1000, 0, 1, 20),
     ("train_h (NT)", 2048, 1000, 7050, 0, 1, 20),
     ("train_out (NT)", 2048, 7050, 1000, 0, 1, 20),
-    ("train_Z (NN,N=64)", 2048, 64, 7050, 0, 0, 20),
-    ("dout+=G f^T (NT,K=64)", 2048, 7050, 64, 0, 1, 20),
-    ("dW2 (TN)", 7050, 1000, 2048, 1, 0, 20),
     ("dh (NN)", 2048, 1000, 7050, 0, 0, 20),
+    ("dW2 (TN)", 7050, 1000, 2048, 1, 0, 20),
     ("dW1 (TN)", 1000, 7050, 2048, 1, 0, 20),
-    ("cl_logits_u (NT,K=64)", 2048, 19445, 64, 0, 1, 60),
-    ("cl_dp1_u (NN,N=64)", 2048, 64, 19445, 0, 0, 60),
-    ("cl_dtab_u (TN,N=64)", 19445, 64, 2048, 1, 0, 60),
     ("proj_v (NN,N=64)", 7050, 64, 4096, 0, 0, 60),
     ("proj_v_grad (TN,N=64)", 4096, 64, 7050, 1, 0, 60),
-    ("eval_scores (NT,K=64)", 4096, 7050, 64, 0, 1, 5),
+    ("cl_logits_u (NT,K=64)", 2048, 19445, 64, 0, 1, 60),
+    ("cl_dtab_u (TN,N=64)", 19445, 64, 2048, 1, 0, 60),
+    ("cl_dp1_u (NN,N=64)", 2048, 64, 19445, 0, 0, 60),
+    ("dout+=G f^T (NT,K=64)", 2048, 7050, 64, 0, 1, 40),
+    ("train_Z (NN,N=64)", 2048, 64, 7050, 0, 0, 40),
 ]
 
 
@@ -39,9 +42,10 @@ def run(args):
     tot_ms = 0.0
     print(f"{'shape':26s} {'tile':>4s} {'us':>9s} {'TF/s':>7s} {'ms/epoch':>9s}")
     for name, M, N, Kd, ta, tb, calls in SHAPES:
-        A = torch.randn((Kd, M) if ta else (M, Kd), device=dev)
-        B = torch.randn((N, Kd) if tb else (Kd, N), device=dev)
-        C = torch.empty((M, N), device=dev)
+        r4 = lambda n: (n + 3) // 4 * 4  # noqa: E731  (the model's buffers pad rows to 16 bytes)
+        A = torch.randn((Kd, r4(M)) if ta else (M, r4(Kd)), device=dev)[:, :(M if ta else Kd)]
+        B = torch.randn((N, r4(Kd)) if tb else (Kd, r4(N)), device=dev)[:, :(Kd if tb else N)]
+        C = torch.empty((M, r4(N)), device=dev)[:, :N]
         best = None
         for tile in args.tiles:
             for _ in range(3):
@@ -62,7 +66,7 @@ def run(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--tiles", default="0,64,128")
+    ap.add_argument("--tiles", default="0,64,128,256,256128,128256")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     a.tiles = [int(t) for t in a.tiles.split(",")]
