@@ -63,6 +63,8 @@ SIGNATURES = {
     "gmr_diff_densify": (I32, [I32, I32, P, P, P, P, I64, P]),
     "gmr_diff_time_bias": (I32, [I32, I32, P, P, P, I64, I64, P, I32, P, P, P, P]),
     "gmr_diff_loss_rows": (I32, [I32, I32, P, P, P, P, P, P, P, I64, F32, P, P, P, I32, P]),
+    "gmr_vbpr_loss_fwd_bwd": (I32, [I32, I32, P, I64, P, P, P, I64, F32, P, P, P, P, P, I64, P]),
+    "gmr_fill2d_f32": (I32, [I64, I64, P, I64, F32, P]),
     "gmr_transpose_f32": (I32, [I64, I64, P, I64, P, I64, P]),
     "gmr_diff_sparse_hidden": (I32, [I32, I32, P, P, P, P, I64, P, P, I64, P]),
     "gmr_diff_sample_t_importance": (I32, [I32, I32, I32, P, P, F64, U64, U64, P, P, P]),

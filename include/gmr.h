@@ -129,6 +129,14 @@ int gmr_bpr_fwd_bwd(int32_t B, int64_t U, const float* Emb, const int32_t* users
                     const int32_t* neg, float* loss, float* contrib, float inv_norm, void* stream);
 /* K8 InfoNCE pieces (diffmm.py:251-258): in-place row softmax of logits with log-sum-exp out,
  * and the per-row terms of the gathered batch */
+/* VBPR calculate_loss (models/vbpr.py:76-97; common/loss.py BPRLoss + EmbLoss): rows of one
+ * (U + I) x D table (items at item_off); loss = mean -log(1e-10 + sigmoid(<u,p> - <u,n>)) +
+ * reg_weight * (||U||_F + ||P||_F + ||N||_F) / B; contrib = [dU; dP; dN] (3B x D) for
+ * gmr_scatter_sorted_f32.  Workspaces: x_ws B floats, sq_ws 3B doubles, coef_ws 3 floats. */
+int gmr_vbpr_loss_fwd_bwd(int32_t B, int32_t D, const float* table, int64_t ldt, const int32_t* users,
+                          const int32_t* pos, const int32_t* neg, int64_t item_off, float reg_weight, float* x_ws,
+                          double* sq_ws, float* coef_ws, float* loss, float* contrib, int64_t ldc, void* stream);
+int gmr_fill2d_f32(int64_t rows, int64_t cols, float* p, int64_t ld, float value, void* stream);
 int gmr_row_softmax_f32(int64_t rows, int64_t cols, float* L, int64_t ld, float coef, float* lse, void* stream);
 int gmr_contrast_rows(int32_t B, const float* CLN, const int32_t* nodes, int64_t node_off, const float* lse,
                       float inv_temp, float coef, float* loss, float* contrib, int64_t ld_contrib, void* stream);
