@@ -60,9 +60,21 @@ def setup(args):
     return cfg, ds, tr, tl, vl, model, trainer
 
 
+def pmc_traffic():
+    """HBM bytes per launch per kernel class from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, made by scripts/pmc_traffic.sh on the same workload)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return {}, None
+    with open(files[-1]) as f:
+        return json.load(f), os.path.relpath(files[-1], ROOT)
+
+
 def summarize_probe(p):
     """Aggregate HIP-event timings per kernel class into roofline objects."""
     out = {}
+    pmc, pmc_src = pmc_traffic()
     for tag, recs in p.items():
         if not recs:
             continue
@@ -87,6 +99,11 @@ def summarize_probe(p):
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "launches": len(recs),
                         "avg_us": round(1e3 * tot_ms / len(recs), 2), "total_ms": round(tot_ms, 3),
                         "algorithmic_per_launch": byts / len(recs), "kernel": "spmm_seg_kernel (CSR, wave/segment)"}
+    for tag, o in out.items():
+        if tag in pmc:
+            o["traffic"] = round(pmc[tag]["traffic_per_launch"])
+            o["traffic_unit"] = "bytes/launch (memory side: 2 x FETCH_SIZE + WRITE_SIZE)"
+            o["traffic_source"] = pmc_src
     return out
 
 
