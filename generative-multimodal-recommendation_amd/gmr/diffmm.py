@@ -287,6 +287,11 @@ class DiffMM(GeneralRecommender):
         self._step += 1
         return loss[0]
 
+    def graph_key(self):
+        """Identity of every device buffer a captured rec_step bakes in besides its inputs."""
+        gs = (self.norm_adj, self.image_UI_matrix, self.text_UI_matrix)
+        return tuple((g.rowptr.data_ptr(), g.plan.data_ptr(), g.flags) for g in gs if g is not None)
+
     def _plans(self, users, pos, neg):
         B = users.numel()
         dev = self.device

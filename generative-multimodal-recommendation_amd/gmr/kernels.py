@@ -16,12 +16,16 @@ _ws = {}
 
 # ---------------------------------------------------------------- live per-kernel timing (bench.py)
 _probe = None
+_probe_every = 1
+_probe_count = 0
 
 
-def probe_begin(tags):
-    """Record HIP events around every launch whose tag is in `tags` (on the launching stream)."""
-    global _probe
+def probe_begin(tags, every=1):
+    """Record HIP events around the launches whose tag is in `tags` (on the launching stream); with
+    every > 1 a hashed 1-in-`every` sample keeps the probe's own cost out of the timed region."""
+    global _probe, _probe_every, _probe_count
     _probe = {t: [] for t in tags}
+    _probe_every, _probe_count = max(1, int(every)), 0
 
 
 def probe_end():
@@ -32,7 +36,14 @@ def probe_end():
 
 class _Probe:
     def __init__(self, tag, meta):
+        global _probe_count
         self.rec = _probe.get(tag) if _probe is not None else None
+        if self.rec is not None and torch.cuda.is_current_stream_capturing():
+            self.rec = None  # launches captured into a HIP graph are not individually timed
+        if self.rec is not None and _probe_every > 1:
+            _probe_count += 1  # hashed 1-in-`every` selection: no aliasing with the launch pattern
+            if ((_probe_count * 2654435761) >> 13) % _probe_every:
+                self.rec = None
         self.meta = meta
 
     def __enter__(self):
