@@ -42,7 +42,7 @@ class _Probe:
             self.rec = None  # launches captured into a HIP graph are not individually timed
         if self.rec is not None and _probe_every > 1:
             _probe_count += 1  # hashed 1-in-`every` selection: no aliasing with the launch pattern
-            if ((_probe_count * 2654435761) >> 13) % _probe_every:
+            if (((_probe_count * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF) >> 40) % _probe_every:
                 self.rec = None
         self.meta = meta
 
