@@ -142,6 +142,7 @@ class DiffMM(GeneralRecommender):
         self._w = None
         self._dw = None
         self._step = 0
+        self._streams = K.Streams(2)
 
     # ================================================================= buffers
     def _work(self, B):
@@ -149,7 +150,6 @@ class DiffMM(GeneralRecommender):
             return self._w
         N, I, U, dev = self.N, self.n_items, self.n_users, self.device
         f = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731
-        nt = max(U, I)
         w = {"B": B,
              "F": f(I, 128), "NF": f(I, 128), "nrmF": f(2, I),
              "G": f(N, 128), "H": f(N, 128), "Qi": f(N, 128), "Qt": f(N, 128), "K2": f(N, 128),
@@ -158,7 +158,9 @@ class DiffMM(GeneralRecommender):
              "DG": f(N, 128), "T3": f(N, 128), "Tcl": f(N, 128), "Ri": f(N, 128), "Rt": f(N, 128),
              "OutI": f(N, 128), "OutT": f(N, 128), "dNF": f(I, 128),
              "partials": f(int(_lib.load().gmr_dmm_final_bwd_partials(N))),
-             "logits": f(B, (nt + 3) // 4 * 4), "lse": f(B), "P1": f(B, 64),
+             "logits_u": f(B, (U + 3) // 4 * 4), "lse_u": f(B), "P1_u": f(B, 64),
+             "logits_i": f(B, (I + 3) // 4 * 4), "lse_i": f(B), "P1_i": f(B, 64),
+             "part_cl": f(self.norm_adj.partial.shape[0], self.norm_adj.partial.shape[1]),
              "contrib_bpr": f(3 * B, 64), "contrib_cl": f(2 * B, 128),
              "loss_bpr": f(B), "loss_cu": f(B), "loss_ci": f(B), "loss": f(4),
              "sqws": torch.empty(1024, dtype=torch.float64, device=dev)}
@@ -180,12 +182,16 @@ class DiffMM(GeneralRecommender):
         iE = E0[U:]
         NF, G, H, Qi, Qt = w["NF"], w["G"], w["H"], w["Qi"], w["Qt"]
         adj, iadj, tadj = self.norm_adj, self.image_UI_matrix, self.text_UI_matrix
+        st = self._streams
         self._project(w)
+        # Qi = iadj @ [E0 | [uE; nimg]]: ris-adj term + contrastive view (diffmm.py:135-136, 175-176)
+        with st.on(0):
+            iadj.spmm(Qi, [(E0, iE), (E0, NF[:, :64])], split=U)
+        with st.on(1):
+            tadj.spmm(Qt, [(E0, iE), (E0, NF[:, 64:])], split=U)
         # G = adj @ [[uE; nimg] | [uE; ntxt]]                       (diffmm.py:138-139, 148-149)
         adj.spmm(G, [(E0, NF[:, :64]), (E0, NF[:, 64:])], split=U)
-        # Qi = iadj @ [E0 | [uE; nimg]]: ris-adj term + contrastive view (diffmm.py:135-136, 175-176)
-        iadj.spmm(Qi, [(E0, iE), (E0, NF[:, :64])], split=U)
-        tadj.spmm(Qt, [(E0, iE), (E0, NF[:, 64:])], split=U)
+        st.join(0, 1)
         # H = adj @ [[G_img[:U]; iE] | [G_txt[:U]; iE]]             (diffmm.py:141-143, 151-153)
         adj.spmm(H, [(G[:, :64], iE), (G[:, 64:], iE)], split=U)
         # E = G + H + ris_adj * [IA | TA] (over G);  M = w0 E_img + w1 E_txt  (:155-158)
@@ -202,20 +208,21 @@ class DiffMM(GeneralRecommender):
         return w["Emb"]
 
     # ================================================================= fused rec step
-    def _contrast(self, w, nodes, off, n_table, slot0, loss_out, B, norm):
+    def _contrast(self, w, nodes, off, n_table, slot0, loss_out, B, norm, slot="u"):
         """InfoNCE of CLN[:, :64] (view 1) vs CLN[:, 64:] (view 2) for the gathered nodes."""
-        CLN, P1 = w["CLN"], w["P1"][:B]
+        CLN, P1 = w["CLN"], w["P1_" + slot][:B]
         inv_t = 1.0 / self.temp
         coef = self.ssl_reg / norm
         table = CLN[off:off + n_table, 64:]
-        L = w["logits"][:B, :n_table]
+        L = w["logits_" + slot][:B, :n_table]
+        lse = w["lse_" + slot]
         K.gather_rows(CLN[:, :64], nodes, P1, off=off)
         K.gemm(P1, table, L, trans_b=True, alpha=inv_t)                         # logits / temp
-        _lib.call("gmr_row_softmax_f32", B, n_table, ptr(L), L.stride(0), coef, ptr(w["lse"]), stream())
+        _lib.call("gmr_row_softmax_f32", B, n_table, ptr(L), L.stride(0), coef, ptr(lse), stream())
         contrib = w["contrib_cl"][slot0:slot0 + B]
         K.gemm(L, table, contrib[:, :64], alpha=inv_t)                          # dp1 (dense part)
         K.gemm(L, P1, w["dCLN"][off:off + n_table, 64:], trans_a=True, alpha=inv_t)  # d table
-        _lib.call("gmr_contrast_rows", B, ptr(CLN), ptr(nodes), off, ptr(w["lse"]), inv_t, coef, ptr(loss_out),
+        _lib.call("gmr_contrast_rows", B, ptr(CLN), ptr(nodes), off, ptr(lse), inv_t, coef, ptr(loss_out),
                   ptr(contrib), contrib.stride(0), stream())
 
     def rec_step(self, users, pos, neg, plan_bpr=None, plan_cl=None, norm_rows=None, reg_share=1.0):
@@ -237,17 +244,21 @@ class DiffMM(GeneralRecommender):
         E0 = s.view("E0")
         if plan_bpr is None:
             plan_bpr, plan_cl = self._plans(users, pos, neg)
+        st = self._streams
         self._forward_mm(w, with_cl=True)
         K.zero_(w["dCLN"])  # [:, 64:] is then overwritten by the d-table GEMMs, [:, :64] by scatters
-        # --- losses and their sparse gradient contributions
+        # --- losses and their sparse gradient contributions (the two InfoNCE terms run side by side)
+        with st.on(0):
+            self._contrast(w, users, 0, U, 0, w["loss_cu"], B, nr, slot="u")
+        with st.on(1):
+            self._contrast(w, pos, U, I, B, w["loss_ci"], B, nr, slot="i")
         _lib.call("gmr_bpr_fwd_bwd", B, U, ptr(w["Emb"]), ptr(users), ptr(pos), ptr(neg), ptr(w["loss_bpr"]),
                   ptr(w["contrib_bpr"]), 1.0 / nr, stream())
-        self._contrast(w, users, 0, U, 0, w["loss_cu"], B, nr)
-        self._contrast(w, pos, U, I, B, w["loss_ci"], B, nr)
         loss = w["loss"][:1]
         _lib.call("gmr_sum_f32", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(loss), 0, stream())
         _lib.call("gmr_sqnorm_f32", N * 64, ptr(E0), self.reg_weight * reg_share, ptr(loss), 1, ptr(w["sqws"]),
                   stream())
+        st.join(0, 1)
         _lib.call("gmr_sum_f32", B, ptr(w["loss_cu"]), self.ssl_reg / nr, ptr(loss), 1, stream())
         _lib.call("gmr_sum_f32", B, ptr(w["loss_ci"]), self.ssl_reg / nr, ptr(loss), 1, stream())
         # --- backward
@@ -268,14 +279,19 @@ class DiffMM(GeneralRecommender):
         dK = w["dCLN"]
         K.normalize_rows_bwd(w["CLN"][:, :64], w["nrmCL"][0], dCLN[:, :64], dK[:, :64])
         K.normalize_rows_bwd(w["CLN"][:, 64:], w["nrmCL"][1], dCLN[:, 64:], dK[:, 64:])
-        adj.spmm(w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)])
-        _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
-                  ptr(w["Rt"]), stream())
-        iadj.spmm(w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)])          # iadj symmetric
-        tadj.spmm(w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)])
+        # the contrastive branch (side stream 0) and the two-hop GCN branch (main) only meet in assemble
+        with st.on(0):
+            adj.spmm(w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], partial=w["part_cl"])
+            _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
+                      ptr(w["Rt"]), stream())
+            with st.on(1):
+                tadj.spmm(w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)])
+            iadj.spmm(w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)])      # iadj symmetric
+            st.join(1)
         adj.spmm(w["T2"], [(w["dE"][:, :64],), (w["dE"][:, 64:],)])
         _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
         adj.spmm(w["T3"], [(w["DG"][:, :64],), (w["DG"][:, 64:],)])
+        st.join(0)
         _lib.call("gmr_dmm_assemble", N, U, ptr(w["T2"]), ptr(w["T3"]), ptr(w["OutI"]), ptr(w["OutT"]), ptr(E0),
                   2.0 * self.reg_weight * reg_share, ptr(s.gview("E0")), ptr(w["dNF"]), stream())
         # modality projections: normalize + leaky-relu backward, then W grads

@@ -62,6 +62,29 @@ def stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+class Streams:
+    """Fork/join helper over a few side streams (events preallocated): work issued inside
+    `with st.on(i):` runs on side stream i after everything already issued on the main stream;
+    st.join(i) makes the main stream wait for it."""
+
+    def __init__(self, n):
+        self.side = [torch.cuda.Stream() for _ in range(n)]
+        self.fork_ev = [torch.cuda.Event() for _ in range(n)]
+        self.join_ev = [torch.cuda.Event() for _ in range(n)]
+
+    def on(self, i):
+        main = torch.cuda.current_stream()
+        self.fork_ev[i].record(main)
+        self.side[i].wait_event(self.fork_ev[i])
+        return torch.cuda.stream(self.side[i])
+
+    def join(self, *idx):
+        main = torch.cuda.current_stream()
+        for i in idx:
+            self.join_ev[i].record(self.side[i])
+            main.wait_event(self.join_ev[i])
+
+
 def ptr(t):
     if t is None:
         return None
@@ -79,7 +102,9 @@ def _ld(t):
 
 
 def workspace(nfloats, device, tag="gemm"):
-    key = (tag, device)
+    """Cached scratch per (tag, device, stream): kernels running concurrently on different
+    streams never share one."""
+    key = (tag, device, torch.cuda.current_stream().cuda_stream)
     w = _ws.get(key)
     if w is None or w.numel() < nfloats:
         w = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
@@ -147,11 +172,12 @@ class CSR:
         # segment plan without split rows: the combine pass is skipped
         self.flags = SPMM_NO_SPLIT_ROWS if (seg_nnz < 512 and hdr[1] == 0) else 0
 
-    def spmm(self, out, blocks, split=None, alpha=1.0, beta=0.0):
+    def spmm(self, out, blocks, split=None, alpha=1.0, beta=0.0, partial=None):
         """out = alpha * A @ X + beta * out; X = column blocks [(lo, hi), ...] of 64 columns each.
 
         Source row s of a block reads lo[s] if s < split else hi[s - split] (hi may be None
-        when split is None, i.e. lo covers all rows)."""
+        when split is None, i.e. lo covers all rows).  `partial` overrides the hub-row scratch
+        (two products of one matrix running concurrently on different streams)."""
         nb = len(blocks)
         if nb not in (1, 2, 4):
             raise ValueError("1, 2 or 4 blocks of 64 columns")
@@ -172,7 +198,8 @@ class CSR:
                 raise ValueError("each block is 64 columns wide")
         with _Probe("spmm", (self.nnz, self.n_rows, self.n_cols, nb, beta != 0.0)):
             _lib.call("gmr_spmm_csr_f32", ptr(self.rowptr), ptr(self.col), ptr(self.val), self.n_rows, self.nnz,
-                      ptr(self.plan), self.seg_nnz, ptr(self.partial), nb, lo, ldl, hi, ldh, split, float(alpha),
+                      ptr(self.plan), self.seg_nnz, ptr(self.partial if partial is None else partial), nb, lo, ldl,
+                      hi, ldh, split, float(alpha),
                       float(beta), ptr(out), _ld(out), self.flags, stream())
         return out
 

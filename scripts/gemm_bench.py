@@ -42,6 +42,8 @@ def run(args):
     tot_ms = 0.0
     print(f"{'shape':26s} {'tile':>4s} {'us':>9s} {'TF/s':>7s} {'ms/epoch':>9s}")
     for name, M, N, Kd, ta, tb, calls in SHAPES:
+        if args.only and not any(o in name for o in args.only.split(",")):
+            continue
         r4 = lambda n: (n + 3) // 4 * 4  # noqa: E731  (the model's buffers pad rows to 16 bytes)
         A = torch.randn((Kd, r4(M)) if ta else (M, r4(Kd)), device=dev)[:, :(M if ta else Kd)]
         B = torch.randn((N, r4(Kd)) if tb else (Kd, r4(N)), device=dev)[:, :(Kd if tb else N)]
@@ -49,11 +51,11 @@ def run(args):
         best = None
         for tile in args.tiles:
             for _ in range(3):
-                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile)
+                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=args.split)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(args.reps):
-                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile)
+                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=args.split)
             e.record()
             torch.cuda.synchronize()
             us = 1e3 * s.elapsed_time(e) / args.reps
@@ -68,6 +70,8 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="0,64,128,256,256128,128256")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--split", type=int, default=0)
+    ap.add_argument("--only", default="", help="substring filter on shape names")
     a = ap.parse_args()
     a.tiles = [int(t) for t in a.tiles.split(",")]
     run(a)
