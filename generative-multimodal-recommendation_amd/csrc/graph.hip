@@ -8,8 +8,8 @@
 //   DiffMM.get_norm_adj_mat   models/diffmm.py:88-107   (no self loops, eps = 1e-7)
 //   DiffMMTrainer.buildUIMatrix + normalizeAdj   common/trainer.py:464-485  (self loops, eps = 0)
 // Columns are sorted inside each row, so the CSR equals the reference's coalesced COO.
-// Item rows are filled in user order by a single workgroup (rounds of 1024 entries with
-// an in-round stable rank), so the build is deterministic without a device sort.
+// Item rows are filled through atomically claimed slots, then each row is put in user order
+// by its own workgroup (rank count / LDS bitmap), so the build is deterministic.
 #include "gmr_common.h"
 
 namespace {
@@ -45,55 +45,77 @@ __global__ void __launch_bounds__(1024) rowptr_kernel(int U, int I, const int* _
   if (t == 1023) rowptr[N] = s[1023];
 }
 
+// user rows in place; every entry is also scattered into its item row at an atomically
+// claimed slot (order fixed afterwards by item_sort_kernel)
 __global__ void user_rows_kernel(int U, const int* __restrict__ uptr, const int* __restrict__ uitems, int sl,
-                                 const int* __restrict__ rowptr, int* __restrict__ col) {
+                                 const int* __restrict__ rowptr, int* __restrict__ col, int* __restrict__ fill) {
   const int u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= U) return;
   int o = rowptr[u];
   if (sl) col[o++] = u;
-  for (int e = uptr[u]; e < uptr[u + 1]; ++e) col[o++] = U + uitems[e];
-}
-
-__device__ __forceinline__ int user_of(const int* __restrict__ uptr, int U, int e) {
-  int lo = 0, hi = U;  // largest u with uptr[u] <= e
-  while (hi - lo > 1) {
-    int mid = (lo + hi) >> 1;
-    if (uptr[mid] <= e) lo = mid;
-    else hi = mid;
+  for (int e = uptr[u]; e < uptr[u + 1]; ++e) {
+    const int it = uitems[e];
+    col[o++] = U + it;
+    col[rowptr[U + it] + atomicAdd(&fill[it], 1)] = u;
   }
-  return lo;
 }
 
-__global__ void __launch_bounds__(1024) item_rows_kernel(int U, int nnz, const int* __restrict__ uptr,
-                                                         const int* __restrict__ uitems, const int* __restrict__ rowptr,
-                                                         int* __restrict__ col, int sl, int I) {
-  __shared__ int key[1024];
-  extern __shared__ __attribute__((aligned(16))) int running[];  // I ints
-  const int t = threadIdx.x;
-  for (int i = t; i < I; i += 1024) running[i] = 0;
+// One workgroup per item row: put the row's users in ascending order (the reference's
+// coalesced COO order).  Users of a row are distinct, so short rows rank each entry by a
+// count of smaller entries in LDS and long rows go through an LDS bitmap over all U users
+// with a popcount prefix — deterministic and independent of the atomic slot order.
+constexpr int kSortThreads = 256;
+__global__ void __launch_bounds__(kSortThreads) item_sort_kernel(int U, const int* __restrict__ rowptr,
+                                                                 int* __restrict__ col, int sl) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t bits[];  // (U + 31) / 32 words
+  __shared__ int s_val[kSortThreads];
+  __shared__ int s_part[kSortThreads];
+  const int i = blockIdx.x, t = threadIdx.x;
+  const int beg = rowptr[U + i];
+  const int L = rowptr[U + i + 1] - beg - sl;
+  if (sl && t == 0) col[beg + L] = U + i;
+  if (L <= 1) return;
+  if (L <= kSortThreads) {
+    const int v = t < L ? col[beg + t] : 0;
+    s_val[t] = v;
+    __syncthreads();
+    if (t < L) {
+      int r = 0;
+      for (int j = 0; j < L; ++j) r += s_val[j] < v;
+      col[beg + r] = v;
+    }
+    return;
+  }
+  const int W = (U + 31) >> 5;
+  for (int w = t; w < W; w += kSortThreads) bits[w] = 0u;
   __syncthreads();
-  for (int base = 0; base < nnz; base += 1024) {
-    const int e = base + t;
-    const int it = e < nnz ? uitems[e] : -1 - t;
-    key[t] = it;
+  for (int e = t; e < L; e += kSortThreads) {
+    const int v = col[beg + e];
+    atomicOr(&bits[v >> 5], 1u << (v & 31));
+  }
+  __syncthreads();
+  // contiguous word range per thread, block-exclusive scan of the range popcounts
+  const int per = (W + kSortThreads - 1) / kSortThreads;
+  const int w0 = min(W, t * per), w1 = min(W, w0 + per);
+  int cnt = 0;
+  for (int w = w0; w < w1; ++w) cnt += __popc(bits[w]);
+  s_part[t] = cnt;
+  __syncthreads();
+  for (int off = 1; off < kSortThreads; off <<= 1) {
+    const int a = t >= off ? s_part[t - off] : 0;
     __syncthreads();
-    int rank = 0;
-    bool last = true;
-    for (int j = 0; j < 1024; ++j) {
-      const int kj = key[j];
-      rank += (j < t) & (kj == it);
-      last &= !((j > t) & (kj == it));
-    }
-    if (e < nnz) {
-      const int u = user_of(uptr, U, e);
-      col[rowptr[U + it] + running[it] + rank] = u;
-    }
-    __syncthreads();
-    if (e < nnz && last) running[it] += rank + 1;
+    s_part[t] += a;
     __syncthreads();
   }
-  if (sl)
-    for (int i = t; i < I; i += 1024) col[rowptr[U + i + 1] - 1] = U + i;
+  int o = beg + s_part[t] - cnt;
+  for (int w = w0; w < w1; ++w) {
+    uint32_t b = bits[w];
+    while (b) {
+      const int k = __ffs(b) - 1;
+      col[o++] = (w << 5) + k;
+      b &= b - 1;
+    }
+  }
 }
 
 // one wave per row: values in fp64, rounded once to fp32
@@ -149,7 +171,7 @@ extern "C" int gmr_bipartite_symnorm_build(int64_t n_users, int64_t n_items, con
   hipStream_t st = (hipStream_t)stream;
   const int U = (int)n_users, I = (int)n_items, N = U + I;
   const int sl = self_loops ? 1 : 0;
-  GMR_ARG(n_items <= 36000, "n_items above the LDS budget of the item-row builder");
+  GMR_ARG(n_users <= 1200000, "n_users above the LDS bitmap budget of the item-row sort");
   int* cnt = workspace;
   hipError_t e = hipMemsetAsync(workspace, 0, sizeof(int) * 2 * (size_t)I, st);
   if (e != hipSuccess) return gmr::hip_status(__func__, e);
@@ -161,15 +183,14 @@ extern "C" int gmr_bipartite_symnorm_build(int64_t n_users, int64_t n_items, con
   hipLaunchKernelGGL(rowptr_kernel, dim3(1), dim3(1024), 0, st, U, I, user_ptr, cnt, sl, rowptr);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(user_rows_kernel, dim3(gmr::grid_for(U, 256)), dim3(256), 0, st, U, user_ptr, user_items, sl, rowptr,
-                     col);
+                     col, workspace + I);
   GMR_LAUNCHED();
-  const size_t dyn = sizeof(int) * (size_t)I;
+  const size_t dyn = sizeof(uint32_t) * (size_t)((U + 31) / 32);
   if (dyn > 65536) {
-    e = hipFuncSetAttribute((const void*)item_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    e = hipFuncSetAttribute((const void*)item_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
     if (e != hipSuccess) return gmr::hip_status(__func__, e);
   }
-  hipLaunchKernelGGL(item_rows_kernel, dim3(1), dim3(1024), dyn, st, U, (int)n_user_items, user_ptr,
-                     user_items, rowptr, col, sl, I);
+  hipLaunchKernelGGL(item_sort_kernel, dim3(I), dim3(kSortThreads), dyn, st, U, rowptr, col, sl);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(values_kernel, dim3(gmr::grid_for(N, 4)), dim3(256), 0, st, N, rowptr, col, deg_eps, val);
   GMR_LAUNCHED();

@@ -1,0 +1,435 @@
+"""Golden vectors for GenRecV1, made by importing the reference.
+
+Runs ONLY in the build container (the reference is mounted read-only at /root/reference and
+never travels to the GPU box).  Writes tests/golden/genrecv1_tiny.npz (+ a JSON sidecar).
+
+Reference entry points exercised (paths relative to GenMMRec/src):
+  models/genrecv1.py:16-125    GenRecV1.__init__ (init order under torch.manual_seed)
+  models/genrecv1.py:133-152   get_norm_adj_mat;  :128-131 _get_user_item_matrix (R)
+  models/genrecv1.py:225-353   projections, user_item_GCN, item_item_GCN, gate_attention_fusion, forward
+  models/genrecv1.py:355-427   calculate_loss (+ autograd grads), infoNCE_loss, full_sort_predict (eval mode)
+  models/genrecv1.py:443-457   SpAdjDropEdge (keep 0.5)
+  models/genrecv1.py:460-648   FlipInterestDiffusion: get_cum, q_sample, p_sample, training_losses
+  models/genrecv1.py:650-710   ModalDenoiseTransformer forward (+ grads of the BCE path)
+  common/trainer.py:673-687    _build_knn_adj -> utils/utils.py:184-197 build_knn_normalized_graph
+  common/trainer.py:464-485    buildUIMatrix;  :736-789 the rebuild (gen_topk mask, debias, rebuild_k top-k)
+  common/interest_cluster.py   MultimodalCluster (StandardScaler + KMeans labels), InterestDebiase
+
+Every random draw of the reference (torch.randint / rand / rand_like / bernoulli, random.sample)
+is recorded by wrapping those functions while the reference runs, so the HIP path can be checked
+with the same draws injected.  Dropout modules of the rec model are recorded through forward
+hooks (keep masks); the transformer denoiser's dropouts are set to p = 0 for the fixtures (its
+dropout path is checked statistically and against a torch fp32 twin in the GPU tests).
+
+Usage:  python tests/golden/make_golden_genrec.py
+"""
+import json
+import os
+import random
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from make_golden import REF_SRC, Cfg, MockLoader, coo_of, make_interactions  # noqa: E402
+
+OUT = HERE
+
+
+def _import_reference():
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF_SRC)
+    du = types.ModuleType("utils.data_utils")
+    for n in ["ImageResize", "ImagePad", "image_to_tensor", "load_decompress_img_from_lmdb_value"]:
+        setattr(du, n, None)
+    sys.modules["utils.data_utils"] = du
+    sys.modules["lmdb"] = types.ModuleType("lmdb")
+    import torch
+    # torch_scatter is absent: scatter_add via index_add_ (utils/utils.py:153, GenRecV1 only)
+    ts = types.ModuleType("torch_scatter")
+
+    def scatter_add(src, index, dim=0, dim_size=None):
+        out = torch.zeros(dim_size, dtype=src.dtype)
+        return out.index_add_(0, index, src)
+
+    ts.scatter_add = scatter_add
+    sys.modules["torch_scatter"] = ts
+    np.float = float
+    import models.genrecv1 as genrecv1
+    import common.trainer as trainer
+    import common.interest_cluster as interest_cluster
+    import utils.utils as uutils
+    return dict(genrecv1=genrecv1, trainer=trainer, interest_cluster=interest_cluster, utils=uutils)
+
+
+class Recorder:
+    """Wraps torch.randint/rand/rand_like/bernoulli and random.sample; records every result."""
+
+    def __init__(self):
+        import torch
+        self.torch = torch
+        self.log = []
+        self.orig = {}
+
+    def __enter__(self):
+        torch = self.torch
+        for name in ("randint", "rand", "rand_like", "bernoulli"):
+            f = getattr(torch, name)
+            self.orig[name] = f
+
+            def wrap(*a, _f=f, _n=name, **k):
+                r = _f(*a, **k)
+                self.log.append((_n, r.detach().clone()))
+                return r
+            setattr(torch, name, wrap)
+        self.orig["sample"] = random.sample
+
+        def samp(pop, n):
+            r = self.orig["sample"](pop, n)
+            self.log.append(("sample", list(r)))
+            return r
+        random.sample = samp
+        return self
+
+    def __exit__(self, *a):
+        for name in ("randint", "rand", "rand_like", "bernoulli"):
+            setattr(self.torch, name, self.orig[name])
+        random.sample = self.orig["sample"]
+
+    def take(self, name):
+        for j, (n, r) in enumerate(self.log):
+            if n == name:
+                self.log.pop(j)
+                return r
+        raise KeyError(name)
+
+
+def _cfg(tmp, ds, extra=None):
+    import torch
+    c = Cfg(USER_ID_FIELD="userID", ITEM_ID_FIELD="itemID", NEG_PREFIX="neg__", train_batch_size=24,
+            device=torch.device("cpu"), end2end=False, is_multimodal_model=True, data_path=tmp + "/",
+            dataset=ds, vision_feature_file="image_feat.npy", text_feature_file="text_feat.npy",
+            learning_rate=1e-3,
+            # GenRecV1.yaml
+            visual_modality=True, text_modality=True, audio_modality=False, embedding_size=64, n_layers=1,
+            reg_weight=1e-5, keep_rate=0.5, temperature=0.55, sparse_temp=0.5, ssl_reg1=0.1, ssl_reg2=0.1,
+            ssl_gen1=0.01, ssl_gen2=0.01, ssl_gen3=0.01, OpenInterestDebiase=True, kmeans_cluster_num=20,
+            use_auto_optimal_k=False, sample_ratio=0.1, gen_topk=5, rebuild_k=10, d_emb_size=10, nhead=8,
+            num_layers=6, steps=5, flip_temp=1.0, bayesian_samplinge_schedule=True, sampling_steps=5, knn_k=10)
+    if extra:
+        c.update(extra)
+    return c
+
+
+def _dropout_hooks(model):
+    """keep masks of every nn.Dropout call, in call order (name, mask)."""
+    import torch
+    rec = []
+
+    def hook(mod, inp, out, _name=None):
+        x = inp[0]
+        keep = torch.where(x != 0, (out != 0).float(), torch.ones_like(x))
+        rec.append((mod._gmr_name, keep))
+
+    hs = []
+    for n, m in model.named_modules():
+        if isinstance(m, torch.nn.Dropout):
+            m._gmr_name = n
+            hs.append(m.register_forward_hook(hook))
+    return rec, hs
+
+
+def _bn_state(model, out, prefix):
+    import torch
+    for n, m in model.named_modules():
+        if isinstance(m, torch.nn.BatchNorm1d) and not n.startswith("denoise"):
+            out[f"{prefix}bn_{n.replace('.', '_')}_mean"] = m.running_mean.numpy().copy()
+            out[f"{prefix}bn_{n.replace('.', '_')}_var"] = m.running_var.numpy().copy()
+
+
+def gen_model(ref, tmp):
+    """Rec model rows G1-G3 at U=97, I=61."""
+    import torch
+    g1 = ref["genrecv1"]
+    uu = ref["utils"]
+    rng = np.random.default_rng(21)
+    U, I, DV, DT = 97, 61, 48, 40
+    rows, cols = make_interactions(rng, U, I)
+    ddir = os.path.join(tmp, "gtiny")
+    os.makedirs(ddir, exist_ok=True)
+    v = rng.standard_normal((I, DV)).astype(np.float32)
+    t = rng.standard_normal((I, DT)).astype(np.float32)
+    np.save(os.path.join(ddir, "image_feat.npy"), v)
+    np.save(os.path.join(ddir, "text_feat.npy"), t)
+    cfg = _cfg(tmp, "gtiny")
+    torch.manual_seed(999)
+    model = g1.GenRecV1(cfg, MockLoader(U, I, rows, cols))
+    out = {"U": np.int64(U), "I": np.int64(I), "train_rows": rows, "train_cols": cols, "v_feat": v, "t_feat": t}
+    for n, p in model.named_parameters():
+        if not n.startswith("denoise_model"):
+            out["p_" + n.replace(".", "_")] = p.detach().numpy().copy()
+    out["n_params_total"] = np.int64(sum(p.numel() for p in model.parameters()))
+    out["norm_adj_idx"], out["norm_adj_val"] = coo_of(model.norm_adj)
+    out["R_idx"], out["R_val"] = coo_of(model.R)
+    # kNN item-item graphs (trainer.py:673-687 -> utils.py:184-197), knn_k = 10
+    for key, feat in (("img", model.image_embedding), ("txt", model.text_embedding)):
+        fn = torch.nn.functional.normalize(feat, p=2, dim=-1)
+        g = uu.build_knn_normalized_graph(torch.mm(fn, fn.t()), topk=10, is_sparse=True, norm_type="sym")
+        out[f"ii_{key}_idx"], out[f"ii_{key}_val"] = coo_of(g)
+        setattr(model, "image_II_matrix" if key == "img" else "text_II_matrix", g)
+    # rebuilt image UI graph (rebuild_k = 10 distinct items per user) + SpAdjDropEdge(0.5)
+    tr = object.__new__(ref["trainer"].GenRecV1Trainer)
+    tr.user_num, tr.item_num, tr.device = U, I, torch.device("cpu")
+    k10 = np.stack([rng.choice(I, size=10, replace=False) for _ in range(U)])
+    ui = tr.buildUIMatrix(np.repeat(np.arange(U), 10), k10.reshape(-1), np.ones(10 * U))
+    out["ui_k10_items"] = k10.astype(np.int64)
+    out["ui_idx"], out["ui_val"] = coo_of(ui)
+    with Recorder() as rec:
+        dropped = model.edgeDropper(ui)
+    r = rec.take("rand").numpy()
+    keep = np.floor(r + 0.5).astype(bool)
+    idx = ui._indices().numpy()
+    # keep flag per edge of the coalesced (row-major) pre-drop graph
+    order = np.lexsort((idx[1], idx[0]))
+    out["ui_keep_sorted"] = keep[order].astype(np.uint8)
+    out["ui_drop_idx"], out["ui_drop_val"] = coo_of(dropped)
+    model.image_UI_matrix = dropped
+
+    # ---- forward in train mode (dropout masks recorded), BN running stats after it
+    model.train()
+    masks, hs = _dropout_hooks(model)
+    with torch.no_grad():
+        content, side = model.forward(model.R, model.norm_adj, model.image_UI_matrix, model.image_II_matrix,
+                                      model.text_II_matrix)
+        out["fwd_img_feats_eval"] = None
+    out["fwd_content"], out["fwd_side"] = content.numpy(), side.numpy()
+    out["fwd_mask_names"] = np.array([m[0] for m in masks])
+    for j, (_, m) in enumerate(masks):
+        out[f"fwd_mask{j}"] = m.numpy().astype(np.uint8)
+    _bn_state(model, out, "fwd_")
+    masks.clear()
+    # ---- calculate_loss + grads (train mode; fresh dropout draws recorded)
+    B = 24
+    users = torch.as_tensor(rng.integers(0, U, size=B))
+    pos = torch.as_tensor(rng.integers(0, I, size=B))
+    neg = torch.as_tensor(rng.integers(0, I, size=B))
+    out["bpr_users"], out["bpr_pos"], out["bpr_neg"] = users.numpy(), pos.numpy(), neg.numpy()
+    model.zero_grad()
+    loss = model.calculate_loss(torch.stack([users, pos, neg]))
+    loss.backward()
+    out["loss"] = np.float32(loss.item())
+    for j, (_, m) in enumerate(masks):
+        out[f"loss_mask{j}"] = m.numpy().astype(np.uint8)
+    _bn_state(model, out, "loss_")
+    for n, p in model.named_parameters():
+        if not n.startswith("denoise_model") and p.grad is not None:
+            out["g_" + n.replace(".", "_")] = p.grad.numpy().copy()
+    out["g_names"] = np.array([n for n, p in model.named_parameters()
+                               if not n.startswith("denoise_model") and p.grad is not None])
+    for h in hs:
+        h.remove()
+    # ---- full_sort_predict in eval mode (BN running stats, no dropout)
+    model.eval()
+    eval_users = np.arange(0, U, 3)
+    with torch.no_grad():
+        out["eval_scores"] = model.full_sort_predict([torch.as_tensor(eval_users)]).numpy()
+        out["eval_users"] = eval_users
+        c2, s2 = model.forward(model.R, model.norm_adj, model.image_UI_matrix, model.image_II_matrix,
+                               model.text_II_matrix)
+        out["eval_content"], out["eval_side"] = c2.numpy(), s2.numpy()
+    del out["fwd_img_feats_eval"]
+    return out
+
+
+def _den_params(den, out, prefix):
+    for n, p in den.named_parameters():
+        out[prefix + n.replace(".", "_")] = p.detach().numpy().copy()
+
+
+def _zero_dropout(mod):
+    import torch
+    for m in mod.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+        if isinstance(m, torch.nn.MultiheadAttention):
+            m.dropout = 0.0
+
+
+def gen_diffusion(ref, tmp):
+    """FlipInterestDiffusion + ModalDenoiseTransformer (rows G4, G5) at B=24, I=61, d_model=64."""
+    import torch
+    g1 = ref["genrecv1"]
+    rng = np.random.default_rng(22)
+    I, B, T = 61, 24, 5
+    cfg = _cfg(tmp, "gtiny")
+    torch.manual_seed(4321)
+    den = g1.ModalDenoiseTransformer(in_dims=I, out_dims=I, emb_size=10, nhead=8, num_layers=2,
+                                     dim_feedforward=64, dropout=0.2)
+    diff = g1.FlipInterestDiffusion(config=cfg, steps=T, base_temp=1.0)
+    out = {"I": np.int64(I), "B": np.int64(B), "T": np.int64(T), "d_model": np.int64(64), "n_layers": np.int64(2)}
+    _den_params(den, out, "den_")
+    out["den_names"] = np.array([n for n, _ in den.named_parameters()])
+    x0 = np.zeros((B, I), np.float32)
+    for b in range(B):
+        x0[b, rng.choice(I, size=int(rng.integers(2, 9)), replace=False)] = 1.0
+    out["x0"] = x0
+    x0t = torch.from_numpy(x0)
+    # eval-mode forward on fixed (x, t): x binary and non-binary inputs
+    xin = (rng.random((B, I)) < 0.4).astype(np.float32)
+    tq = torch.as_tensor(rng.integers(0, T, size=B))
+    den.eval()
+    with torch.no_grad():
+        out["fwd_x"], out["fwd_t"] = xin, tq.numpy()
+        out["fwd_out"] = den(torch.from_numpy(xin), tq).numpy()
+    # schedule from the batch sparsity (genrecv1.py:480-498)
+    g, e = diff.get_cum(x0t)
+    out["gamma_cum"], out["eps_cum"] = g.numpy(), e.numpy()
+    # training_losses in train mode with denoiser dropout p = 0; every draw recorded
+    den.train()
+    _zero_dropout(den)
+    calls = []
+    orig = diff.p_interest_shift_probs
+
+    def rec_call(model, x_t, t):
+        lg, pr = orig(model, x_t, t)
+        calls.append((x_t.detach().clone(), t.detach().clone(), lg.detach().clone()))
+        return lg, pr
+    diff.p_interest_shift_probs = rec_call
+    iE = torch.from_numpy(rng.standard_normal((I, 64)).astype(np.float32))
+    feats = torch.from_numpy(rng.standard_normal((I, 64)).astype(np.float32))
+    tfeats = torch.from_numpy(rng.standard_normal((I, 64)).astype(np.float32))
+    out["item_embeds"], out["img_feats"], out["txt_feats"] = iE.numpy(), feats.numpy(), tfeats.numpy()
+    torch.manual_seed(77)
+    den.zero_grad()
+    with Recorder() as rec:
+        loss = diff.training_losses(den, x0t, iE, torch.arange(B).float(), feats, tfeats)
+    loss.backward()
+    out["loss_total"] = np.float32(loss.item())
+    for n, p in den.named_parameters():
+        if p.grad is not None:
+            out["g_" + n.replace(".", "_")] = p.grad.numpy().copy()
+    out["g_names"] = np.array([n for n, p in den.named_parameters() if p.grad is not None])
+    # draws, in the order training_losses makes them (genrecv1.py:553-577)
+    out["tl_t"] = rec.take("randint").numpy()
+    out["tl_noise1"] = rec.take("rand_like").numpy()
+    out["tl_flip1"] = rec.take("bernoulli").numpy()
+    out["tl_noise2"] = rec.take("rand_like").numpy()
+    out["tl_flip2"] = rec.take("bernoulli").numpy()
+    for s in range(T):
+        out[f"tl_ps{s}"] = rec.take("bernoulli").numpy()
+    assert not rec.log, [n for n, _ in rec.log]
+    for j, (xt, tt, lg) in enumerate(calls):
+        out[f"tl_call{j}_x"], out[f"tl_call{j}_t"], out[f"tl_call{j}_logits"] = xt.numpy(), tt.numpy(), lg.numpy()
+    out["tl_ncalls"] = np.int64(len(calls))
+    # loss pieces recomputed from the recorded tensors with the reference's own helpers
+    with torch.no_grad():
+        lg0 = calls[0][2]
+        pw = torch.sum(1 - x0t) / (torch.sum(x0t) + 1e-8)
+        bce = torch.nn.functional.binary_cross_entropy_with_logits(lg0, x0t, pos_weight=pw)
+        probs0 = torch.sigmoid(lg0)
+        kl = diff._calc_kl_divergence(x0t, calls[0][0], calls[0][1], probs0)
+        cw = torch.clamp(calls[0][1].float() / T, 0, 0.5)
+        out["loss_bce"] = np.float32(bce.item())
+        out["loss_kl"] = np.float32((cw * kl).mean().item())
+        gen = torch.from_numpy(out[f"tl_ps{T - 1}"])
+        fe = iE * feats
+        out["loss_cl"] = np.float32(diff.infoNCE_loss(x0t @ fe, gen @ fe, 0.5).item())
+    diff.p_interest_shift_probs = orig
+    return out
+
+
+def gen_rebuild(ref, tmp):
+    """Graph rebuild (trainer.py:736-789): p_sample, gen_topk mask, InterestDebiase, rebuild_k top-k;
+    KMeans labels (interest_cluster.py:60-79)."""
+    import torch
+    g1 = ref["genrecv1"]
+    ic = ref["interest_cluster"]
+    rng = np.random.default_rng(23)
+    I, B, T = 61, 96, 5
+    cfg = _cfg(tmp, "gtiny")
+    torch.manual_seed(999)
+    den = g1.ModalDenoiseTransformer(in_dims=I, out_dims=I, emb_size=10, nhead=8, num_layers=2,
+                                     dim_feedforward=64, dropout=0.2)
+    diff = g1.FlipInterestDiffusion(config=cfg, steps=T, base_temp=1.0)
+    out = {}
+    _den_params(den, out, "den_")
+    x0 = np.zeros((B, I), np.float32)
+    for b in range(B):
+        x0[b, rng.choice(I, size=int(rng.integers(2, 9)), replace=False)] = 1.0
+    x0[5] = 0.0  # a user with no history: empty interest map (interest_cluster.py:350-354)
+    out["x0"] = x0
+    # clustered features: KMeans labels are the reference's; the debias step consumes them
+    centers = rng.standard_normal((4, 16)) * 4
+    lab_true = rng.integers(0, 4, size=I)
+    feat = (centers[lab_true] + rng.standard_normal((I, 16)) * 0.3).astype(np.float32)
+    mc = ic.MultimodalCluster(20, 20, 20, 20, 20, 20, 20, False, 3, 7, 237, 10)
+    np.random.seed(5)
+    labels = mc.multimodal_specific_cluster(torch.from_numpy(feat), "image_modal", 4)
+    out["km_feat"], out["km_labels"], out["km_true"] = feat, np.asarray(labels, np.int64), lab_true
+    out["km_scaled"] = mc.stand_norm.fit_transform(feat).astype(np.float32)
+    x0t = torch.from_numpy(x0)
+    den.train()
+    _zero_dropout(den)
+    calls = []
+    orig = diff.p_interest_shift_probs
+
+    def rec_call(model, x_t, t):
+        lg, pr = orig(model, x_t, t)
+        calls.append(lg.detach().clone())
+        return lg, pr
+    diff.p_interest_shift_probs = rec_call
+    torch.manual_seed(88)
+    random.seed(3)
+    with torch.no_grad(), Recorder() as rec:
+        dn, dp = diff.p_sample(den, x0t, 5, True)
+        _, ind = torch.topk(dp, k=5, dim=1)
+        mask = torch.zeros_like(dp, dtype=torch.bool).scatter_(1, ind, True)
+        dn2 = torch.where(mask, dn, x0t)
+        judge = ic.InterestDebiase(origin_interaction_graph=x0t, generated_interaction_graph=dn2,
+                                   interest_cluster_space_dict={"image_modal": labels, "text_modal": labels},
+                                   image_modality="image_modal", text_modality="text_modal", audio_modality=None,
+                                   sample_ratio=0.1)
+        dn3 = judge.interest_query_debiase()
+        top_v, top_i = torch.topk(dn3 * dp, k=10)
+    out["ps_noise"] = rec.take("rand_like").numpy()
+    out["ps_flip"] = rec.take("bernoulli").numpy()
+    for s in range(T):
+        out[f"ps_step{s}"] = rec.take("bernoulli").numpy()
+    # safe_sample draws only when int(len * 0.1) > 0 (interest_cluster.py:234-243)
+    flips = (dn2 - x0t).numpy()
+    for name, cnt in (("dislike", int((flips > 0).sum())), ("like", int((flips < 0).sum()))):
+        out[f"ps_n_{name}"] = np.int64(cnt)
+        smp = rec.take("sample") if int(cnt * 0.1) > 0 else []
+        out[f"ps_{name}_sample"] = np.asarray(smp, np.int64).reshape(-1, 2)
+    for j, lg in enumerate(calls):
+        out[f"ps_call{j}_logits"] = lg.numpy()
+    out["ps_out"], out["ps_probs"] = dn.numpy(), dp.numpy()
+    out["gen_mask"] = mask.numpy().astype(np.uint8)
+    out["denoised"], out["debiased"] = dn2.numpy(), dn3.numpy()
+    out["rebuild_top_vals"], out["rebuild_top_idx"] = top_v.numpy(), top_i.numpy()
+    diff.p_interest_shift_probs = orig
+    return out
+
+
+def main():
+    ref = _import_reference()
+    import torch
+    import sklearn
+    meta = {"torch": torch.__version__, "numpy": np.__version__, "sklearn": sklearn.__version__,
+            "reference": REF_SRC, "generator": "tests/golden/make_golden_genrec.py"}
+    with tempfile.TemporaryDirectory() as tmp:
+        out = {}
+        for pre, fn in (("m_", gen_model), ("d_", gen_diffusion), ("r_", gen_rebuild)):
+            for k, v in fn(ref, tmp).items():
+                out[pre + k] = v
+    np.savez_compressed(os.path.join(OUT, "genrecv1_tiny.npz"), **out)
+    with open(os.path.join(OUT, "genrecv1_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print("wrote", os.path.join(OUT, "genrecv1_tiny.npz"), len(out), "arrays")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,182 @@
+"""Pin the GenRecV1 CPU oracle (oracle/genrec_ref.py) against the reference's golden vectors
+(tests/golden/make_golden_genrec.py -> genrecv1_tiny.npz)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import genrec_ref, graph_ref
+from genrec_fixture import (BN_NAMES, den_params, fresh_bn_state, masks_of, model_graphs, model_params,
+                            sparse_graphs, sub)
+
+
+@pytest.fixture(scope="module")
+def G(golden):
+    g = golden("genrecv1_tiny")
+    return {"m": sub(g, "m_"), "d": sub(g, "d_"), "r": sub(g, "r_")}
+
+
+def _coo_csr(n, idx, val):
+    return graph_ref.coo_to_csr(n, idx, val)
+
+
+def test_graphs_vs_reference(G):
+    m = G["m"]
+    U, I = int(m["U"]), int(m["I"])
+    N = U + I
+    csrs, dims = model_graphs(m)
+    rp, col, val = _coo_csr(N, m["norm_adj_idx"], m["norm_adj_val"])
+    assert np.array_equal(csrs["norm_adj"][1], col) and np.array_equal(csrs["norm_adj"][2].view(np.uint32),
+                                                                       val.view(np.uint32))
+    rp, col, val = _coo_csr(U, m["R_idx"], m["R_val"])
+    assert np.array_equal(csrs["R"][0], rp) and np.array_equal(csrs["R"][1], col)
+    rp, col, val = _coo_csr(N, m["ui_idx"], m["ui_val"])
+    assert np.array_equal(csrs["ui_full"][1], col)
+    assert np.array_equal(csrs["ui_full"][2].view(np.uint32), val.view(np.uint32))
+    rp, col, val = _coo_csr(N, m["ui_drop_idx"], m["ui_drop_val"])
+    assert np.array_equal(csrs["ui_img"][0], rp) and np.array_equal(csrs["ui_img"][1], col)
+    assert np.array_equal(csrs["ui_img"][2].view(np.uint32), val.view(np.uint32))
+    for key in ("img", "txt"):
+        rp, col, val = _coo_csr(I, m[f"ii_{key}_idx"], m[f"ii_{key}_val"])
+        mine = csrs["ii_" + key]
+        assert np.array_equal(mine[0], rp) and np.array_equal(mine[1], col)
+        np.testing.assert_allclose(mine[2], val, rtol=1e-6, atol=1e-7)
+
+
+def _forward(m, masks_prefix, train=True):
+    csrs, dims = model_graphs(m)
+    graphs = sparse_graphs({k: v for k, v in csrs.items() if k != "ui_full"}, dims)
+    p = model_params(m)
+    feats = {"image": torch.as_tensor(m["v_feat"]), "text": torch.as_tensor(m["t_feat"])}
+    state = fresh_bn_state()
+    masks = masks_of(m, masks_prefix) if masks_prefix else None
+    c, s = genrec_ref.forward(p, feats, graphs, state, train, masks)
+    return c, s, state, (p, feats, graphs)
+
+
+def test_forward_train_mode(G):
+    m = G["m"]
+    c, s, state, _ = _forward(m, "fwd")
+    np.testing.assert_allclose(c.detach().numpy(), m["fwd_content"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(s.detach().numpy(), m["fwd_side"], rtol=1e-4, atol=1e-6)
+    for n in BN_NAMES[:-1]:
+        np.testing.assert_allclose(state[n][0].numpy(), m[f"fwd_bn_{n}_mean"], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(state[n][1].numpy(), m[f"fwd_bn_{n}_var"], rtol=1e-5, atol=1e-7)
+
+
+def test_calculate_loss_and_grads(G):
+    m = G["m"]
+    csrs, dims = model_graphs(m)
+    graphs = sparse_graphs({k: v for k, v in csrs.items() if k != "ui_full"}, dims)
+    p = model_params(m, requires_grad=True)
+    feats = {"image": torch.as_tensor(m["v_feat"]), "text": torch.as_tensor(m["t_feat"])}
+    state = fresh_bn_state()
+    genrec_ref.forward(p, feats, graphs, state, True, masks_of(m, "fwd"))  # BN running stats as the reference
+    loss = genrec_ref.calculate_loss(p, feats, graphs, state, torch.as_tensor(m["bpr_users"]),
+                                     torch.as_tensor(m["bpr_pos"]), torch.as_tensor(m["bpr_neg"]),
+                                     masks_of(m, "loss"))
+    loss.backward()
+    assert abs(loss.item() - float(m["loss"])) <= 2e-6 * abs(float(m["loss"]))
+    for n in [str(s) for s in m["g_names"]]:
+        k = n.replace(".", "_")
+        np.testing.assert_allclose(p[k].grad.numpy(), m["g_" + k], rtol=2e-4, atol=2e-7, err_msg=n)
+    for n in BN_NAMES[:-1]:
+        np.testing.assert_allclose(state[n][0].numpy(), m[f"loss_bn_{n}_mean"], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(state[n][1].numpy(), m[f"loss_bn_{n}_var"], rtol=1e-5, atol=1e-7)
+    # eval mode (running stats, no dropout) -> full_sort_predict
+    with torch.no_grad():
+        c, s = genrec_ref.forward({k: v.detach() for k, v in p.items()}, feats, graphs, state, False)
+    # parameters did not step between the reference's loss and eval calls
+    np.testing.assert_allclose(c.numpy(), m["eval_content"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(s.numpy(), m["eval_side"], rtol=1e-4, atol=1e-6)
+    U = int(m["U"])
+    sc = c[:U][m["eval_users"]] @ c[U:].t()
+    np.testing.assert_allclose(sc.numpy(), m["eval_scores"], rtol=1e-5, atol=1e-6)
+
+
+def test_denoiser_forward(G):
+    d = G["d"]
+    w = den_params(d)
+    out = genrec_ref.denoiser(w, d["fwd_x"], d["fwd_t"], int(d["n_layers"]))
+    np.testing.assert_allclose(out.numpy(), d["fwd_out"], rtol=1e-4, atol=1e-5)
+
+
+def test_flip_schedule(G):
+    d = G["d"]
+    g, e = genrec_ref.flip_schedule(d["x0"])
+    assert np.array_equal(g.numpy().view(np.uint32), d["gamma_cum"].view(np.uint32))
+    assert np.array_equal(e.numpy().view(np.uint32), d["eps_cum"].view(np.uint32))
+
+
+def test_training_losses(G):
+    d = G["d"]
+    w = {k: v.clone().requires_grad_(True) for k, v in den_params(d).items()}
+    g, e = genrec_ref.flip_schedule(d["x0"])
+    T = int(d["T"])
+    draws = [d[f"tl_ps{s}"] for s in range(T)]
+    total, bce, kl, cl, logits = genrec_ref.training_losses(
+        w, d["x0"], d["tl_t"], d["tl_flip1"], torch.as_tensor(d["item_embeds"]), torch.as_tensor(d["img_feats"]),
+        d["tl_flip2"], draws, g, e, int(d["n_layers"]))
+    np.testing.assert_allclose(logits.detach().numpy(), d["tl_call0_logits"], rtol=1e-4, atol=1e-5)
+    assert abs(bce.item() - float(d["loss_bce"])) <= 1e-5 * abs(float(d["loss_bce"]))
+    assert abs(kl.item() - float(d["loss_kl"])) <= 1e-5 * abs(float(d["loss_kl"]))
+    assert abs(cl.item() - float(d["loss_cl"])) <= 1e-5 * abs(float(d["loss_cl"]))
+    assert abs(total.item() - float(d["loss_total"])) <= 1e-5 * abs(float(d["loss_total"]))
+    total.backward()
+    for n in [str(s) for s in d["g_names"]]:
+        k = n.replace(".", "_")
+        got = w[k].grad.numpy() if w[k].grad is not None else np.zeros_like(d["g_" + k])  # zero-memory K/V weights
+        np.testing.assert_allclose(got, d["g_" + k], rtol=2e-3, atol=1e-6, err_msg=n)
+    # the p_sample model calls see the recorded inputs
+    for j in range(1, int(d["tl_ncalls"])):
+        lg = genrec_ref.denoiser(den_params(d), d[f"tl_call{j}_x"], d[f"tl_call{j}_t"], int(d["n_layers"]))
+        np.testing.assert_allclose(lg.numpy(), d[f"tl_call{j}_logits"], rtol=1e-4, atol=1e-5)
+
+
+def test_flip_prob_reproduces_draws(G):
+    """The recorded flip masks are Bernoulli(flip_prob) draws: the oracle's probabilities must make
+    them likely (mean log-likelihood well above chance) — a check of flip_prob itself."""
+    d = G["d"]
+    g, e = genrec_ref.flip_schedule(d["x0"])
+    pr = genrec_ref.flip_prob(d["x0"], d["tl_t"], torch.as_tensor(d["tl_noise1"]), g, e)
+    f = torch.as_tensor(d["tl_flip1"])
+    ll = (f * torch.log(pr) + (1 - f) * torch.log(1 - pr)).mean().item()
+    ll_half = np.log(0.5)
+    assert ll > ll_half
+    assert abs(pr.mean().item() - f.mean().item()) < 0.03
+
+
+def test_rebuild_rows(G):
+    r = G["r"]
+    mask, den, deb, order = genrec_ref.rebuild_rows(r["x0"], r["ps_out"], r["ps_probs"], r["km_labels"],
+                                                    r["ps_dislike_sample"], r["ps_like_sample"])
+    assert np.array_equal(mask, r["gen_mask"].astype(bool))
+    assert np.array_equal(den, r["denoised"])
+    assert np.array_equal(deb, r["debiased"])
+    score = deb * r["ps_probs"]
+    ref_i, ref_v = r["rebuild_top_idx"], r["rebuild_top_vals"]
+    for b in range(order.shape[0]):
+        nz = ref_v[b] > 0
+        # non-tied picks bit-exact; zero-valued picks: same count, all from the zero class
+        assert np.array_equal(order[b][nz], ref_i[b][nz])
+        assert np.all(score[b][order[b][~nz]] == 0)
+
+
+def test_psample_logits(G):
+    r = G["r"]
+    w = den_params(r)
+    T = 5
+    x = genrec_ref.flip_apply(r["x0"], r["ps_flip"])
+    for j, i in enumerate(reversed(range(T))):
+        lg = genrec_ref.denoiser(w, x, np.full(x.shape[0], i), 2)
+        np.testing.assert_allclose(lg.numpy(), r[f"ps_call{j}_logits"], rtol=1e-4, atol=1e-5)
+        x = torch.as_tensor(r[f"ps_step{j}"])
+    np.testing.assert_allclose(torch.sigmoid(lg).numpy(), r["ps_probs"], rtol=1e-5, atol=1e-6)
+
+
+def test_kmeans_labels_partition(G):
+    """The reference's KMeans labels recover the planted clusters (a permutation of them): the
+    fixture the device KMeans is held to."""
+    r = G["r"]
+    lab, true = r["km_labels"], r["km_true"]
+    pairs = set(zip(lab.tolist(), true.tolist()))
+    assert len(pairs) == len(set(lab.tolist())) == len(set(true.tolist()))

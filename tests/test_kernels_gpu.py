@@ -54,15 +54,22 @@ def test_bipartite_build_bit_exact(K, golden, self_loops, eps):
     assert np.array_equal(csr.val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
 
 
-def test_bipartite_build_large_hubs(K):
+@pytest.mark.parametrize("self_loops", [0, 1])
+def test_bipartite_build_large_hubs(K, self_loops):
+    # item rows above 256 users take the LDS-bitmap ordering path, shorter ones the rank path
     rng = _rng(1)
     U, I = 3000, 500
     rows = np.repeat(np.arange(U), 7)
     p = 1.0 / np.arange(1, I + 1) ** 1.2
     cols = rng.choice(I, size=rows.size, p=p / p.sum())
-    want = graph_ref.norm_adj_csr(U, I, rows, cols)
+    if self_loops:
+        want = graph_ref.ui_adj_csr(U, I, rows, cols)
+    else:
+        want = graph_ref.norm_adj_csr(U, I, rows, cols)
     uptr, uitems = _user_csr(U, I, rows, cols)
-    csr = K.bipartite_symnorm(U, I, _dev(uptr), _dev(uitems), 0, 1e-7)
+    assert np.bincount(uitems, minlength=I).max() > 256
+    csr = K.bipartite_symnorm(U, I, _dev(uptr), _dev(uitems), self_loops, 0.0 if self_loops else 1e-7)
+    assert np.array_equal(csr.rowptr.cpu().numpy(), want[0])
     assert np.array_equal(csr.col.cpu().numpy(), want[1])
     assert np.array_equal(csr.val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
 
