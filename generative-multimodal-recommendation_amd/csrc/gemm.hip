@@ -40,7 +40,7 @@ struct Epi {
 // element a dependent memory round trip).
 __device__ __forceinline__ bool epi_reads_x(const Epi& e) {
   return e.kind == GMR_EPI_POSTERIOR || e.kind == GMR_EPI_DTANH || e.kind == GMR_EPI_ROWSCALE_AUX ||
-         ((e.kind == GMR_EPI_NONE || e.kind == GMR_EPI_BIAS) && e.beta != 0.f);
+         e.kind == GMR_EPI_DRELU || ((e.kind == GMR_EPI_NONE || e.kind == GMR_EPI_BIAS) && e.beta != 0.f);
 }
 __device__ __forceinline__ const float* epi_x_ptr(const Epi& e, float* C, int64_t ldc, int64_t m, int64_t n) {
   return (e.kind == GMR_EPI_NONE || e.kind == GMR_EPI_BIAS) ? C + m * ldc + n : e.aux + m * e.ld_aux + n;
@@ -65,6 +65,10 @@ __device__ __forceinline__ float epi_fin(const Epi& e, float acc, float b, float
       return v * (1.f - x * x);
     case GMR_EPI_ROWSCALE_AUX:
       return v + b + r1 * x;
+    case GMR_EPI_BIAS_RELU:
+      return fmaxf(v + b, 0.f);
+    case GMR_EPI_DRELU:
+      return x > 0.f ? v : 0.f;
     default:
       return v;
   }
@@ -364,8 +368,9 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   GMR_ARG(A && B && C, "null operand");
   GMR_ARG(M > 0 && N > 0 && K > 0, "empty GEMM");
   GMR_ARG(lda >= (trans_a ? M : K) && ldb >= (trans_b ? K : N) && ldc >= N, "leading dimension too small");
-  GMR_ARG(epilogue >= GMR_EPI_NONE && epilogue <= GMR_EPI_ROWSCALE_AUX, "bad epilogue");
-  GMR_ARG(!(epilogue == GMR_EPI_POSTERIOR || epilogue == GMR_EPI_DTANH || epilogue == GMR_EPI_ROWSCALE_AUX) || aux,
+  GMR_ARG(epilogue >= GMR_EPI_NONE && epilogue <= GMR_EPI_DRELU, "bad epilogue");
+  GMR_ARG(!(epilogue == GMR_EPI_POSTERIOR || epilogue == GMR_EPI_DTANH || epilogue == GMR_EPI_ROWSCALE_AUX ||
+            epilogue == GMR_EPI_DRELU) || aux,
           "epilogue needs aux");
   GMR_ARG(epilogue != GMR_EPI_ROWSCALE_AUX || rowvec1, "epilogue needs rowvec1");
   GMR_ARG(tile == 0 || tile == 64 || tile == 128 || tile == 256 || tile == 256128 || tile == 128256,

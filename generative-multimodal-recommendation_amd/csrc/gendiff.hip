@@ -1,0 +1,502 @@
+// GenRecV1 generative side:
+//   FlipInterestDiffusion (models/genrecv1.py:460-648) — schedule from the batch sparsity, flip
+//   q_sample, the Bayesian p_sample step, BCE(pos_weight) + curriculum KL rows;
+//   ModalDenoiseTransformer (models/genrecv1.py:650-710) row kernels — LayerNorm (+ residual,
+//   + dropout, + GELU) forward/backward, adaLN modulation, dropout masks, time embedding, SiLU.
+// The dense products of the transformer run on the MFMA GEMM (gemm.hip).
+#include "gmr_common.h"
+
+namespace {
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+__device__ __forceinline__ float unit01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }  // [0, 1)
+
+// ----------------------------------------------------------------- schedule (get_cum, :480-498)
+// tables: [gamma_cum (T) | eps_cum (T) | pos_weight | sparsity]; fp32 op order of the reference
+// (no contraction), linspace as ATen's CPU kernel (start + step*i below the midpoint, end - step*(T-1-i) above).
+__global__ void flip_schedule_kernel(int B, const int* __restrict__ users, const int* __restrict__ user_ptr, int I,
+                                     int T, float* __restrict__ tab) {
+  __shared__ long long s_ones[256];
+  long long ones = 0;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const int u = users[b];
+    ones += user_ptr[u + 1] - user_ptr[u];
+  }
+  s_ones[threadIdx.x] = ones;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  long long tot = 0;
+  for (int j = 0; j < 256; ++j) tot += s_ones[j];
+  const long long n = (long long)B * I;
+  const float zeros = (float)(n - tot);
+  const float s = __fdiv_rn(zeros, (float)n);
+  const float gs = __fadd_rn(__fmul_rn(0.1f, __fsub_rn(1.f, s)), 0.001f);
+  const float ge = __fmul_rn(gs, 0.1f);
+  const float es = __fadd_rn(__fmul_rn(0.005f, s), 0.0001f);
+  const float ee = __fmul_rn(es, 0.1f);
+  const float gstep = __fdiv_rn(__fsub_rn(ge, gs), (float)(T - 1));
+  const float estep = __fdiv_rn(__fsub_rn(ee, es), (float)(T - 1));
+  const int half = T / 2;
+  float gc = 1.f, ec = 1.f;
+  for (int i = 0; i < T; ++i) {
+    float g, e;
+    if (i < half) {
+      g = __fadd_rn(gs, __fmul_rn(gstep, (float)i));
+      e = __fadd_rn(es, __fmul_rn(estep, (float)i));
+    } else {
+      g = __fsub_rn(ge, __fmul_rn(gstep, (float)(T - i - 1)));
+      e = __fsub_rn(ee, __fmul_rn(estep, (float)(T - i - 1)));
+    }
+    e = fminf(e, 0.01f);
+    gc = __fmul_rn(gc, __fsub_rn(1.f, g));
+    ec = __fmul_rn(ec, __fsub_rn(1.f, e));
+    tab[i] = __fsub_rn(1.f, gc);
+    tab[T + i] = __fsub_rn(1.f, ec);
+  }
+  tab[2 * T] = __fdiv_rn(zeros, __fadd_rn((float)tot, 1e-8f));
+  tab[2 * T + 1] = s;
+}
+
+// x_t = x0 xor Bernoulli(sigmoid((a_t - u) * temp)), a_t = gamma_cum[t] (x0 == 0) or eps_cum[t] (x0 == 1)
+__global__ void flip_qsample_kernel(int B, int I, const float* __restrict__ x0, int64_t ld0, const int* __restrict__ t,
+                                    int t_const, const float* __restrict__ tab, int T, float temp,
+                                    const uint8_t* __restrict__ flip, int64_t ldf, uint64_t seed, uint64_t step,
+                                    float* __restrict__ xt, int64_t ldt) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)B * I) return;
+  const int b = (int)(gid / I), i = (int)(gid % I);
+  const float x = x0[(int64_t)b * ld0 + i];
+  bool f;
+  if (flip) {
+    f = flip[(int64_t)b * ldf + i] != 0;
+  } else {
+    const int tt = t ? t[b] : t_const;
+    const float a = x == 0.f ? tab[tt] : tab[T + tt];
+    const uint4 r = gmr::Philox::gen(seed, step, (uint64_t)gid);
+    const float p = sigm((a - unit01(r.x)) * temp);
+    f = unit01(r.y) < p;
+  }
+  xt[(int64_t)b * ldt + i] = f ? 1.f - x : x;
+}
+
+// p_sample step on the model logits: probs = sigmoid(z); x = Bernoulli(p1 / (p0 + p1)) with
+// a0 = gamma_cum[qi], a1 = eps_cum[qi] (the q_sample(t = qi) tables re-indexed by row, :541-545), or
+// Bernoulli(probs) on the last step; draws (0/1 bytes) replace the Bernoulli when given
+__global__ void flip_step_kernel(int B, int I, const float* __restrict__ z, int64_t ldz, const float* __restrict__ tab,
+                                 int T, int qi, int last, const uint8_t* __restrict__ draws, int64_t ldd, uint64_t seed,
+                                 uint64_t step, float* __restrict__ x, int64_t ldx, float* __restrict__ probs,
+                                 int64_t ldp) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)B * I) return;
+  const int b = (int)(gid / I), i = (int)(gid % I);
+  const float p = sigm(z[(int64_t)b * ldz + i]);
+  if (probs) probs[(int64_t)b * ldp + i] = p;
+  float q = p;
+  if (!last) {
+    const float a0 = tab[qi], a1 = tab[T + qi];
+    const float p0 = p * (1.f - a0) + (1.f - p) * a1;
+    const float p1 = p * a0 + (1.f - p) * (1.f - a1);
+    q = p1 / (p0 + p1);
+  }
+  float v;
+  if (draws) {
+    v = draws[(int64_t)b * ldd + i] ? 1.f : 0.f;
+  } else {
+    const uint4 r = gmr::Philox::gen(seed, step, (uint64_t)gid);
+    v = unit01(r.x) < q ? 1.f : 0.f;
+  }
+  x[(int64_t)b * ldx + i] = v;
+}
+
+// per row: bce_row = sum_i (1-y) z - lw logsigmoid(z), lw = 1 + (pw-1) y (ATen's
+// binary_cross_entropy_with_logits); kl_row = cw[t] * mean_i KL(post || clamp(p)); the BCE
+// gradient (1-y) - lw sigmoid(-z) times grad_scale overwrites dz (may alias z)
+__global__ void __launch_bounds__(256) flip_loss_kernel(int B, int I, const float* __restrict__ x0, int64_t ld0,
+                                                        const float* z, int64_t ldz, const int* __restrict__ t,
+                                                        const float* __restrict__ tab, int T, float grad_scale,
+                                                        float* dz, int64_t lddz, double* __restrict__ bce_row,
+                                                        double* __restrict__ kl_row) {
+  const int b = blockIdx.x;
+  const float pw = tab[2 * T];
+  const float a0 = tab[T - 1], a1 = tab[2 * T - 1];
+  const float eps = 1e-8f;
+  double sb = 0.0, sk = 0.0;
+  for (int i = threadIdx.x; i < I; i += 256) {
+    const float y = x0[(int64_t)b * ld0 + i];
+    const float zz = z[(int64_t)b * ldz + i];
+    const float lw = (pw - 1.f) * y + 1.f;
+    const float ls = fminf(zz, 0.f) - log1pf(expf(-fabsf(zz)));  // log sigmoid
+    sb += (double)((1.f - y) * zz - lw * ls);
+    // KL against the true posterior (genrecv1.py:608-627)
+    const float num = (y == 0.f ? 1.f : 0.f) * (1.f - a0) + (y == 1.f ? 1.f : 0.f) * a1;
+    const float den = (y == 0.f ? 1.f : 0.f) * (1.f - a0 + a1) + (y == 1.f ? 1.f : 0.f) * (a0 + 1.f - a1);
+    const float post = fminf(fmaxf(num / (den + eps), eps), 1.f - eps);
+    const float pr = fminf(fmaxf(sigm(zz), eps), 1.f - eps);
+    const float kl = post * (logf(post + 1e-10f) - logf(pr + 1e-10f)) +
+                     (1.f - post) * (logf(1.f - post + 1e-10f) - logf(1.f - pr + 1e-10f));
+    sk += (double)kl;
+    if (dz) dz[(int64_t)b * lddz + i] = grad_scale * ((1.f - y) - lw * sigm(-zz));
+  }
+  __shared__ double rb[4], rk[4];
+  sb = gmr::wave_sum_d(sb);
+  sk = gmr::wave_sum_d(sk);
+  if ((threadIdx.x & 63) == 0) {
+    rb[threadIdx.x >> 6] = sb;
+    rk[threadIdx.x >> 6] = sk;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bce_row[b] = (rb[0] + rb[1]) + (rb[2] + rb[3]);
+    float cw = (float)t[b] / (float)T;
+    cw = fminf(fmaxf(cw, 0.f), 0.5f);
+    kl_row[b] = (double)cw * ((rk[0] + rk[1]) + (rk[2] + rk[3])) / (double)I;
+  }
+}
+
+// ----------------------------------------------------------------- LayerNorm (one wave per row, D <= 1024)
+// s = a + keep * scale * b (b: matrix, or a broadcast vector when ldb == 0); y = LN(s) w + bias [-> GELU]
+template <int PER>  // floats per lane (D = 64 * PER)
+__global__ void __launch_bounds__(256) ln_fwd_kernel(int64_t rows, const float* __restrict__ a, int64_t lda,
+                                                     const float* __restrict__ bsrc, int64_t ldb,
+                                                     const uint8_t* __restrict__ keep, int64_t ldk, float kscale,
+                                                     const float* __restrict__ w, const float* __restrict__ bias,
+                                                     float eps, int gelu, float* __restrict__ y, int64_t ldy,
+                                                     float* __restrict__ s_out, int64_t lds,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int lane = threadIdx.x & 63;
+  constexpr int D = 64 * PER;
+  float v[PER];
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = j * 64 + lane;
+    float x = a[r * lda + c];
+    if (bsrc) {
+      float bb = bsrc[(ldb ? r * ldb : 0) + c];
+      if (keep) bb = keep[r * ldk + c] ? bb * kscale : 0.f;
+      x += bb;
+    }
+    v[j] = x;
+    sum += x;
+  }
+  const float mean = gmr::wave_sum(sum) / (float)D;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const float d = v[j] - mean;
+    sq += d * d;
+  }
+  const float rstd = 1.f / sqrtf(gmr::wave_sum(sq) / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = j * 64 + lane;
+    if (s_out) s_out[r * lds + c] = v[j];
+    float o = (v[j] - mean) * rstd * w[c] + bias[c];
+    if (gelu) o = 0.5f * o * (1.f + erff(o * 0.70710678118654752f));
+    y[r * ldy + c] = o;
+  }
+  if (lane == 0) {
+    mean_out[r] = mean;
+    rstd_out[r] = rstd;
+  }
+}
+
+// dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy w (dy through GELU first);
+// dw/db column partials per block (rows blockIdx.x*RB .. ) -> part[blk][2*D]
+constexpr int kLnRowsPerBlock = 64;
+template <int PER>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(int64_t rows, const float* __restrict__ s, int64_t lds,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const float* __restrict__ w, const float* __restrict__ bias,
+                                                     int gelu, const float* __restrict__ dy, int64_t lddy,
+                                                     float* __restrict__ dx, int64_t lddx, int accumulate,
+                                                     float* __restrict__ part) {
+  constexpr int D = 64 * PER;
+  __shared__ float red[4][2 * D];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float pw[PER], pb[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) pw[j] = pb[j] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * kLnRowsPerBlock;
+  for (int64_t r = r0 + wv; r < rows && r < r0 + kLnRowsPerBlock; r += 4) {
+    const float mu = mean[r], rs = rstd[r];
+    float xh[PER], g[PER];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = j * 64 + lane;
+      xh[j] = (s[r * lds + c] - mu) * rs;
+      float d = dy[r * lddy + c];
+      if (gelu) {
+        const float u = xh[j] * w[c] + bias[c];
+        const float cdf = 0.5f * (1.f + erff(u * 0.70710678118654752f));
+        const float pdf = 0.3989422804014327f * expf(-0.5f * u * u);
+        d *= cdf + u * pdf;
+      }
+      pw[j] += d * xh[j];
+      pb[j] += d;
+      g[j] = d * w[c];
+      s1 += g[j];
+      s2 += g[j] * xh[j];
+    }
+    s1 = gmr::wave_sum(s1) / (float)D;
+    s2 = gmr::wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = j * 64 + lane;
+      float o = rs * (g[j] - s1 - xh[j] * s2);
+      if (accumulate) o += dx[r * lddx + c];
+      dx[r * lddx + c] = o;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    red[wv][j * 64 + lane] = pw[j];
+    red[wv][D + j * 64 + lane] = pb[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += 256)
+    part[(int64_t)blockIdx.x * 2 * D + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+}
+
+__global__ void ln_param_reduce_kernel(int P, int D, const float* __restrict__ part, float* __restrict__ dw,
+                                       float* __restrict__ db, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * D) return;
+  double s = 0.0;
+  for (int p = 0; p < P; ++p) s += part[(int64_t)p * 2 * D + c];
+  float* o = c < D ? dw + c : db + (c - D);
+  *o = (float)s + (accumulate ? *o : 0.f);
+}
+
+// ----------------------------------------------------------------- adaLN, dropout, time embedding, SiLU
+// h1 = h0 (1 + scale[t]) + shift[t]; S = T x 2D table [shift | scale] (chunk(2) order, :702)
+__global__ void adaln_fwd_kernel(int64_t rows, int D, const float* __restrict__ h0, int64_t ld0,
+                                 const int* __restrict__ t, int t_const, const float* __restrict__ S, int64_t lds,
+                                 float* __restrict__ h1, int64_t ld1) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= rows * D) return;
+  const int64_t r = gid / D;
+  const int c = (int)(gid % D);
+  const int tt = t ? t[r] : t_const;
+  const float* srow = S + (int64_t)tt * lds;
+  h1[r * ld1 + c] = h0[r * ld0 + c] * (1.f + srow[D + c]) + srow[c];
+}
+
+// dh0 = dh1 (1 + scale[t]); prod = dh1 * h0 (for the grouped column sums of dscale)
+__global__ void adaln_bwd_kernel(int64_t rows, int D, const float* __restrict__ h0, int64_t ld0,
+                                 const float* __restrict__ dh1, int64_t ldd, const int* __restrict__ t,
+                                 const float* __restrict__ S, int64_t lds, float* __restrict__ dh0, int64_t ldo,
+                                 float* __restrict__ prod, int64_t ldp) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= rows * D) return;
+  const int64_t r = gid / D;
+  const int c = (int)(gid % D);
+  const float g = dh1[r * ldd + c];
+  prod[r * ldp + c] = g * h0[r * ld0 + c];
+  dh0[r * ldo + c] = g * (1.f + S[(int64_t)t[r] * lds + D + c]);
+}
+
+// y = x * keep / p_keep; keep drawn per (row, column / group) when mask_in is null (written to
+// mask_out), else read from mask_in
+__global__ void dropout_kernel(int64_t rows, int D, int group, const float* __restrict__ x, int64_t ldx,
+                               float p_keep, const uint8_t* __restrict__ mask_in, uint8_t* __restrict__ mask_out,
+                               int64_t ldm, uint64_t seed, uint64_t step, float* __restrict__ y, int64_t ldy) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= rows * D) return;
+  const int64_t r = gid / D;
+  const int c = (int)(gid % D);
+  const int mc = c / group;
+  bool k;
+  if (mask_in) {
+    k = mask_in[r * ldm + mc] != 0;
+  } else {
+    const uint4 rr = gmr::Philox::gen(seed, step, (uint64_t)(r * (D / group) + mc));
+    k = unit01(rr.x) < p_keep;
+    if (mask_out && c % group == 0) mask_out[r * ldm + mc] = k ? 1 : 0;
+  }
+  y[r * ldy + c] = k ? x[r * ldx + c] / p_keep : 0.f;
+}
+
+// temb[t] = [cos(t f_k) | sin(t f_k)], f_k = exp(-ln(1e4) k / half) (:692-696); odd sizes zero-pad
+__global__ void time_embedding_kernel(int T, int E, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T * E) return;
+  const int t = i / E, k = i % E, half = E / 2;
+  float v = 0.f;
+  if (k < 2 * half) {
+    const int kk = k < half ? k : k - half;
+    const float f = expf(__fdiv_rn(__fmul_rn(-9.210340371976184f, (float)kk), (float)half));
+    const float a = __fmul_rn((float)t, f);
+    v = k < half ? cosf(a) : sinf(a);
+  }
+  out[i] = v;
+}
+
+__global__ void flip_total_kernel(const double* __restrict__ bk, const float* __restrict__ cl, float w_cl,
+                                  float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const float b = (float)bk[0], k = (float)bk[1], c = cl[0];
+  out[0] = b;
+  out[1] = k;
+  out[2] = c;
+  out[3] = b + k + w_cl * c;
+}
+
+__global__ void silu_kernel(int64_t n, const float* __restrict__ x, const float* __restrict__ dy,
+                            float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = x[i], s = sigm(v);
+  y[i] = dy ? dy[i] * s * (1.f + v * (1.f - s)) : v * s;
+}
+
+}  // namespace
+
+extern "C" int gmr_flip_schedule(int32_t B, const int32_t* users, const int32_t* user_ptr, int32_t I, int32_t T,
+                                 float* tables, void* stream) {
+  GMR_ARG(users && user_ptr && tables && B > 0 && I > 0 && T >= 2, "bad args");
+  hipLaunchKernelGGL(flip_schedule_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, users, user_ptr, I, T,
+                     tables);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_flip_qsample(int32_t B, int32_t I, const float* x0, int64_t ld0, const int32_t* t, int32_t t_const,
+                                const float* tables, int32_t T, float temp, const uint8_t* flip, int64_t ld_flip,
+                                uint64_t seed, uint64_t step, float* xt, int64_t ldt, void* stream) {
+  GMR_ARG(x0 && tables && xt && B > 0 && I > 0, "bad args");
+  GMR_ARG(t || (t_const >= 0 && t_const < T), "bad t");
+  hipLaunchKernelGGL(flip_qsample_kernel, dim3(gmr::grid_for((int64_t)B * I, 256)), dim3(256), 0, (hipStream_t)stream,
+                     B, I, x0, ld0, t, t_const, tables, T, temp, flip, ld_flip, seed, step, xt, ldt);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_flip_step(int32_t B, int32_t I, const float* z, int64_t ldz, const float* tables, int32_t T,
+                             int32_t qi, int32_t last, const uint8_t* draws, int64_t ldd, uint64_t seed, uint64_t step, float* x,
+                             int64_t ldx, float* probs, int64_t ldp, void* stream) {
+  GMR_ARG(z && tables && x && B > 0 && I > 0 && qi >= 0 && qi < T, "bad args");
+  hipLaunchKernelGGL(flip_step_kernel, dim3(gmr::grid_for((int64_t)B * I, 256)), dim3(256), 0, (hipStream_t)stream, B,
+                     I, z, ldz, tables, T, qi, last, draws, ldd, seed, step, x, ldx, probs, ldp);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_flip_loss_rows(int32_t B, int32_t I, const float* x0, int64_t ld0, const float* z, int64_t ldz,
+                                  const int32_t* t, const float* tables, int32_t T, float grad_scale, float* dz,
+                                  int64_t lddz, double* bce_row, double* kl_row, void* stream) {
+  GMR_ARG(x0 && z && t && tables && bce_row && kl_row && B > 0 && I > 0, "bad args");
+  hipLaunchKernelGGL(flip_loss_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, I, x0, ld0, z, ldz, t, tables, T,
+                     grad_scale, dz, lddz, bce_row, kl_row);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_layernorm_fwd(int64_t rows, int32_t D, const float* a, int64_t lda, const float* b, int64_t ldb,
+                                 const uint8_t* keep, int64_t ld_keep, float keep_scale, const float* w,
+                                 const float* bias, float eps, int32_t gelu, float* y, int64_t ldy, float* s_out,
+                                 int64_t lds, float* mean, float* rstd, void* stream) {
+  GMR_ARG(a && w && bias && y && mean && rstd && rows > 0, "bad args");
+  GMR_ARG(D == 64 || D == 128 || D == 256 || D == 512 || D == 1024, "D must be 64..1024 (power of two)");
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+#define GMR_LNF(P)                                                                                                \
+  hipLaunchKernelGGL(ln_fwd_kernel<P>, grid, dim3(256), 0, st, rows, a, lda, b, ldb, keep, ld_keep, keep_scale, w, \
+                     bias, eps, (int)gelu, y, ldy, s_out, lds, mean, rstd)
+  switch (D) {
+    case 64: GMR_LNF(1); break;
+    case 128: GMR_LNF(2); break;
+    case 256: GMR_LNF(4); break;
+    case 512: GMR_LNF(8); break;
+    default: GMR_LNF(16); break;
+  }
+#undef GMR_LNF
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int64_t gmr_layernorm_parts_floats(int64_t rows, int32_t D) {
+  return ((rows + kLnRowsPerBlock - 1) / kLnRowsPerBlock) * 2 * (int64_t)D;
+}
+
+extern "C" int gmr_layernorm_bwd(int64_t rows, int32_t D, const float* s, int64_t lds, const float* mean,
+                                 const float* rstd, const float* w, const float* bias, int32_t gelu, const float* dy,
+                                 int64_t lddy, float* dx, int64_t lddx, int32_t accumulate_dx, float* parts, float* dw,
+                                 float* db, int32_t accumulate_params, void* stream) {
+  GMR_ARG(s && mean && rstd && w && bias && dy && dx && parts && dw && db && rows > 0, "bad args");
+  GMR_ARG(D == 64 || D == 128 || D == 256 || D == 512 || D == 1024, "D must be 64..1024 (power of two)");
+  hipStream_t st = (hipStream_t)stream;
+  const int P = (int)((rows + kLnRowsPerBlock - 1) / kLnRowsPerBlock);
+#define GMR_LNB(PP)                                                                                              \
+  hipLaunchKernelGGL(ln_bwd_kernel<PP>, dim3(P), dim3(256), 0, st, rows, s, lds, mean, rstd, w, bias, (int)gelu, dy, \
+                     lddy, dx, lddx, (int)accumulate_dx, parts)
+  switch (D) {
+    case 64: GMR_LNB(1); break;
+    case 128: GMR_LNB(2); break;
+    case 256: GMR_LNB(4); break;
+    case 512: GMR_LNB(8); break;
+    default: GMR_LNB(16); break;
+  }
+#undef GMR_LNB
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(gmr::grid_for(2 * D, 256)), dim3(256), 0, st, P, D, parts, dw, db,
+                     (int)accumulate_params);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_adaln_fwd(int64_t rows, int32_t D, const float* h0, int64_t ld0, const int32_t* t, int32_t t_const,
+                             const float* S, int64_t lds, float* h1, int64_t ld1, void* stream) {
+  GMR_ARG(h0 && S && h1 && rows > 0 && D > 0, "bad args");
+  hipLaunchKernelGGL(adaln_fwd_kernel, dim3(gmr::grid_for(rows * D, 256)), dim3(256), 0, (hipStream_t)stream, rows, D,
+                     h0, ld0, t, t_const, S, lds, h1, ld1);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_adaln_bwd(int64_t rows, int32_t D, const float* h0, int64_t ld0, const float* dh1, int64_t ldd,
+                             const int32_t* t, const float* S, int64_t lds, float* dh0, int64_t ldo, float* prod,
+                             int64_t ldp, void* stream) {
+  GMR_ARG(h0 && dh1 && t && S && dh0 && prod && rows > 0, "bad args");
+  hipLaunchKernelGGL(adaln_bwd_kernel, dim3(gmr::grid_for(rows * D, 256)), dim3(256), 0, (hipStream_t)stream, rows, D,
+                     h0, ld0, dh1, ldd, t, S, lds, dh0, ldo, prod, ldp);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dropout_f32(int64_t rows, int32_t D, int32_t group, const float* x, int64_t ldx, float p_keep,
+                               const uint8_t* mask_in, uint8_t* mask_out, int64_t ldm, uint64_t seed, uint64_t step,
+                               float* y, int64_t ldy, void* stream) {
+  GMR_ARG(x && y && rows > 0 && D > 0 && group >= 1 && D % group == 0, "bad args");
+  GMR_ARG(p_keep > 0.f && p_keep <= 1.f, "p_keep in (0, 1]");
+  hipLaunchKernelGGL(dropout_kernel, dim3(gmr::grid_for(rows * D, 256)), dim3(256), 0, (hipStream_t)stream, rows, D,
+                     group, x, ldx, p_keep, mask_in, mask_out, ldm, seed, step, y, ldy);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_time_embedding(int32_t T, int32_t E, float* out, void* stream) {
+  GMR_ARG(out && T > 0 && E > 0, "bad args");
+  hipLaunchKernelGGL(time_embedding_kernel, dim3(gmr::grid_for((int64_t)T * E, 256)), dim3(256), 0,
+                     (hipStream_t)stream, T, E, out);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_silu_f32(int64_t n, const float* x, const float* dy, float* y, void* stream) {
+  GMR_ARG(x && y && n > 0, "bad args");
+  hipLaunchKernelGGL(silu_kernel, dim3(gmr::grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, x, dy, y);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_flip_total(const double* bce_kl, const float* cl, float w_cl, float* out4, void* stream) {
+  GMR_ARG(bce_kl && cl && out4, "bad args");
+  hipLaunchKernelGGL(flip_total_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, bce_kl, cl, w_cl, out4);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}

@@ -1,0 +1,697 @@
+"""GenRecV1 on MI355X — drop-in for models/genrecv1.py of the reference (GeneralRecommender API).
+
+Rows G1-G5 of SURVEY.md §8a:
+  * rec model (:16-427): user/item ID tables, modality projections (Linear+BN+LeakyReLU+Dropout),
+    gates (Linear+BN+Sigmoid), user_item_GCN on norm_adj and the rebuilt (edge-dropped) UI graph,
+    item_item_GCN on the kNN II graphs then R (U x I), gate_attention_fusion; calculate_loss =
+    BPR(log-sigmoid) + reg + 4 InfoNCE terms on B x B logits.  One fused forward and a
+    hand-derived backward: CSR SpMM (spmm.hip), fp32 MFMA GEMMs (gemm.hip), BN / fusion / content
+    row kernels (genrec.hip), transposed CSRs for the non-symmetric graphs (gengraph.hip), the
+    deterministic sorted scatter for the gathered rows;
+  * FlipInterestDiffusion (:460-648) + ModalDenoiseTransformer (:650-710): gendiff.hip +
+    transformer.py.
+
+Layout in HBM (N = U + I, d = 64): one rec slab [E0 = user_embedding; item_id_embedding (N x 64) |
+every other rec parameter under its reference name], the denoiser slab, N x 64 activation tables.
+BatchNorm running statistics are kept per module and updated in the reference's call order.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+from . import dist
+from . import kernels as K
+from .abstract_recommender import GeneralRecommender
+from .kernels import ptr, stream
+from .kmeans import kmeans_labels
+from .slab import Slab
+from .transformer import TransformerDenoiser
+
+BN_NAMES = ["image_residual_project_1", "image_modal_project_1", "text_residual_project_1",
+            "text_modal_project_1", "caculate_common_1", "gate_image_modal_1", "gate_text_modal_1",
+            "gate_audio_modal_1"]
+# BN call order of one forward (models/genrecv1.py:225-353) -> saved-statistics slot
+_BN_CALLS = ["image_residual_project_1", "image_modal_project_1", "gate_image_modal_1",
+             "text_residual_project_1", "text_modal_project_1", "gate_text_modal_1",
+             "caculate_common_1", "caculate_common_1", "gate_image_modal_1", "gate_text_modal_1"]
+ACT_NONE, ACT_LEAKY, ACT_SIGMOID, ACT_TANH = 0, 1, 2, 3
+POST_NONE, POST_RES, POST_MUL, POST_ROWDOT = 0, 1, 2, 3
+
+
+class _RecLoss(torch.autograd.Function):
+    """calculate_loss as an autograd node (external trainers call loss.backward())."""
+
+    @staticmethod
+    def forward(ctx, model, users, pos, neg, *params):
+        loss = model.rec_step(users, pos, neg)
+        ctx.model = model
+        return loss.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        m = ctx.model
+        return (None, None, None, None, *[m.grad_view(n) * g for n in m.param_names()])
+
+
+def _rec_init_twin(U, I, d, DV, DT):
+    """The reference constructor's RNG order (models/genrecv1.py:60-97, :155-222) on CPU torch
+    modules, to draw identical initial values under the caller's seed."""
+    out = {}
+    out["origin_weight"] = torch.ones(1)
+    out["generation_weight"] = torch.ones(1)
+    for n in ("img_weight", "txt_weight", "aud_weight"):
+        out[n] = torch.ones(1)
+    for n in ("img_weight", "txt_weight", "aud_weight"):
+        nn.init.normal_(out[n], mean=1.0, std=0.1)
+    ue, ie = nn.Embedding(U, d), nn.Embedding(I, d)
+    nn.init.xavier_uniform_(ue.weight)
+    nn.init.xavier_uniform_(ie.weight)
+    out["user_embedding_weight"], out["item_id_embedding_weight"] = ue.weight.data, ie.weight.data
+    out["fusion_weight"] = torch.ones(3)
+    out["res_scale"] = torch.ones(1)
+
+    def proj(din):
+        return nn.Sequential(nn.Linear(din, d), nn.BatchNorm1d(d), nn.LeakyReLU(0.2), nn.Dropout(0.1))
+
+    mods = {}
+    for mod, din in (("image", DV), ("text", DT)):
+        if din is None:
+            continue
+        mods[mod + "_residual_project"] = proj(din)
+        mods[mod + "_modal_project"] = proj(d)
+        nn.init.xavier_uniform_(mods[mod + "_residual_project"][0].weight)
+        nn.init.xavier_uniform_(mods[mod + "_modal_project"][0].weight)
+    cc = nn.Sequential(nn.Linear(d, d), nn.BatchNorm1d(d), nn.Tanh(), nn.Linear(d, 1, bias=False))
+    nn.init.xavier_uniform_(cc[0].weight)
+    nn.init.xavier_uniform_(cc[3].weight)
+    mods["caculate_common"] = cc
+    for g in ("gate_image_modal", "gate_text_modal", "gate_audio_modal"):
+        s = nn.Sequential(nn.Linear(d, d), nn.BatchNorm1d(d), nn.Sigmoid())
+        nn.init.xavier_uniform_(s[0].weight)
+        mods[g] = s
+    for name, m in mods.items():
+        for pn, p in m.named_parameters():
+            out[f"{name}_{pn.replace('.', '_')}"] = p.data
+    return out
+
+
+class GenRecV1(GeneralRecommender):
+    def __init__(self, config, dataloader):
+        super().__init__(config, dataloader)
+        c = config
+        self.config = config
+        self.latdim = int(c["embedding_size"])
+        if self.latdim != 64:
+            raise NotImplementedError("the gfx950 kernels are built for embedding_size = 64")
+        self.n_layers = int(c["n_layers"])
+        if self.n_layers != 1:
+            raise NotImplementedError("n_layers = 1 (GenRecV1.yaml) is the configured hot path")
+        self.keep_rate = float(c["keep_rate"])
+        self.sparse_temp = float(c["sparse_temp"])
+        self.temp = float(c["temperature"])
+        self.ssl_reg1, self.ssl_reg2 = float(c["ssl_reg1"]), float(c["ssl_reg2"])
+        self.gen_topk, self.rebuild_k = int(c["gen_topk"]), int(c["rebuild_k"])
+        self.d_emb_size, self.nhead, self.num_layers = int(c["d_emb_size"]), int(c["nhead"]), int(c["num_layers"])
+        self.steps = int(c["steps"])
+        self.flip_temp = float(c["flip_temp"])
+        self.bayesian_samplinge_schedule = bool(c["bayesian_samplinge_schedule"])
+        self.sampling_steps = int(c["sampling_steps"])
+        self.reg_weight = float(c["reg_weight"])
+        self.audio_modality = bool(c["audio_modality"])
+        if self.audio_modality:
+            raise NotImplementedError("audio_modality: the reference cannot run it (self.a_feat unset, genrecv1.py:46; "
+                                      "self.softmax undefined, :314) — see DESIGN.md")
+        if self.v_feat is None or self.t_feat is None:
+            raise NotImplementedError("GenRecV1's forward uses both the image and the text branch (:266-306)")
+        if not self.bayesian_samplinge_schedule:
+            raise NotImplementedError("bayesian_samplinge_schedule = True (GenRecV1.yaml) is the configured path")
+        self.seed = int((c["seed"][0] if isinstance(c["seed"], (list, tuple)) else c["seed"]) or 0)
+        U, I, d = self.n_users, self.n_items, 64
+        self.N = U + I
+        self.DV, self.DT = self.v_feat.shape[1], self.t_feat.shape[1]
+        dev = self.device
+        init = _rec_init_twin(U, I, d, self.DV, self.DT)
+        specs = [("E0", (self.N, d), None)]
+        for n, v in init.items():
+            if n in ("user_embedding_weight", "item_id_embedding_weight"):
+                continue
+            specs.append((n, tuple(v.shape), None))
+        self._pnames = [s[0] for s in specs[1:]]
+        self.rec_slab = Slab(specs, dev)
+        e0 = self.rec_slab.view("E0")
+        e0[:U].copy_(init["user_embedding_weight"])
+        e0[U:].copy_(init["item_id_embedding_weight"])
+        for n in self._pnames:
+            self.rec_slab.load(n, init[n])
+        self.user_embedding_weight = nn.Parameter(e0[:U])
+        self.user_embedding_weight.grad = self.rec_slab.gview("E0")[:U]
+        self.item_id_embedding_weight = nn.Parameter(e0[U:])
+        self.item_id_embedding_weight.grad = self.rec_slab.gview("E0")[U:]
+        for n in self._pnames:
+            setattr(self, n, self.rec_slab.parameter(n))
+        self.bn_state = {n: (torch.zeros(d, device=dev), torch.ones(d, device=dev)) for n in BN_NAMES}
+        # graphs: norm_adj (:54, :133-152), R (:55, :128-131) and R^T for the backward
+        tl = dataloader
+        self.user_ptr = torch.as_tensor(tl.uptr_np).to(dev)
+        self.user_items = torch.as_tensor(tl.uitems_np).to(dev)
+        self.norm_adj = K.bipartite_symnorm(U, I, self.user_ptr, self.user_items, self_loops=False, deg_eps=1e-7)
+        self.R = K.user_item_csr(U, I, self.user_ptr, self.user_items)
+        self.RT = K.csr_transpose(self.R)
+        self.image_UI_matrix = None
+        self.image_UI_matrix_T = None
+        self.image_II_matrix = None
+        self.text_II_matrix = None
+        self._ii_T = None
+        # generator (:99-115): the denoiser is constructed after the rec modules (same RNG stream)
+        self.denoise_in_dims = self.denoise_out_dims = I
+        self.denoise_model_image = TransformerDenoiser(I, I, self.d_emb_size, dev, nhead=self.nhead,
+                                                       num_layers=self.num_layers)
+        self.denoise_model_image.init_like_reference()
+        self.diffusion_model = FlipDiffusion(self)
+        self._w = None
+        self._step = 0
+        self.training_mode = True
+
+    # ================================================================= API pieces
+    def param_names(self):
+        return ["user_embedding_weight", "item_id_embedding_weight"] + self._pnames
+
+    def grad_view(self, name):
+        s, U = self.rec_slab, self.n_users
+        if name == "user_embedding_weight":
+            return s.gview("E0")[:U]
+        if name == "item_id_embedding_weight":
+            return s.gview("E0")[U:]
+        return s.gview(name)
+
+    def P(self, name):
+        return self.rec_slab.view(name)
+
+    def G(self, name):
+        return self.rec_slab.gview(name)
+
+    def optim_slabs(self):
+        return [self.rec_slab]
+
+    def train(self, mode=True):
+        super().train(mode)
+        self.training_mode = mode
+        self.denoise_model_image.train(mode)
+        return self
+
+    def getItemEmbeds(self):
+        return self.item_id_embedding_weight
+
+    def getUserEmbeds(self):
+        return self.user_embedding_weight
+
+    # ================================================================= graphs built by the trainer
+    def build_item_item_graphs(self, knn_k):
+        """GenRecV1Trainer._build_item_item_matrix (common/trainer.py:673-687) on the device."""
+        self.image_II_matrix = K.knn_graph(self.v_feat, knn_k)
+        self.text_II_matrix = K.knn_graph(self.t_feat, knn_k)
+        self._ii_T = (K.csr_transpose(self.image_II_matrix), K.csr_transpose(self.text_II_matrix))
+
+    def set_image_ui_matrix(self, csr):
+        self.image_UI_matrix = csr
+        self.image_UI_matrix_T = K.csr_transpose(csr)
+
+    def set_item_item_graphs(self, img, txt):
+        self.image_II_matrix, self.text_II_matrix = img, txt
+        self._ii_T = (K.csr_transpose(img), K.csr_transpose(txt))
+
+    # ================================================================= buffers
+    def _work(self, B):
+        if self._w is not None and self._w["B"] >= B:
+            return self._w
+        N, I, U, dev = self.N, self.n_items, self.n_users, self.device
+        f = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731
+        Bp = (B + 3) // 4 * 4
+        w = {"B": B, "A1": f(N, 64), "A2": f(N, 64), "C": f(N, 64),
+             "Zr": f(2, I, 64), "Xr": f(2, I, 64), "Zm": f(2, I, 64), "F": f(2, I, 64), "Zg": f(2, I, 64),
+             "Gt": f(2, I, 64), "Pm": f(2, I, 64), "MOD": f(2, N, 64), "Zc": f(2, N, 64), "a": f(2, N),
+             "Zp": f(2, N, 64), "PG": f(2, N, 64), "SIDE": f(N, 64), "alpha": f(N),
+             "stats": f(len(_BN_CALLS), 2, 64), "masks": torch.ones((4, I, 64), dtype=torch.uint8, device=dev),
+             "parts": torch.empty(max(int(_lib.load().gmr_bn_parts_doubles(N)), 4096), dtype=torch.float64,
+                                  device=dev),
+             "sums": f(128), "sqws": torch.empty(1024, dtype=torch.float64, device=dev),
+             # loss
+             "loss_bpr": f(B), "contrib": f(3 * B, 64), "contrib_s": f(2 * B, 64), "g": f(4, B, 64),
+             "nv": f(4, B, 64), "nrm": f(4, B), "raw": f(4, B, 64), "L": f(B, Bp), "rows": f(4, B), "loss": f(4),
+             # backward
+             "dC": f(N, 64), "dS": f(N, 64), "dM": f(2, N, 64), "da": f(2, N), "dPG": f(2, N, 64),
+             "dZ": f(N, 64), "T1": f(N, 64), "T2": f(N, 64), "dP": f(I, 64), "dF": f(I, 64), "dX": f(I, 64),
+             "dZi": f(I, 64)}
+        self._w = w
+        return w
+
+    # ================================================================= forward
+    def _bn(self, w, call, z, rows, act, train, y=None, keep=None, post=POST_NONE, aux=None, rs=None, out2=None,
+            rowdot=None):
+        name = _BN_CALLS[call]
+        rm, rv = self.bn_state[name]
+        st = w["stats"][call]
+        pre = name[:-2]
+        _lib.call("gmr_bn_fwd_f32", rows, ptr(z), K._ld(z), int(train), 1e-5, 0.1, ptr(rm), ptr(rv), ptr(w["parts"]),
+                  ptr(st[0]), ptr(st[1]), ptr(self.P(pre + "_1_weight")), ptr(self.P(pre + "_1_bias")), act, 0.2,
+                  ptr(keep), 64 if keep is not None else 0, 1.0 / 0.9, ptr(y), K._ld(y) if y is not None else 0, post,
+                  ptr(aux), K._ld(aux) if (aux is not None and aux.dim() == 2) else 0, ptr(rs), ptr(out2),
+                  K._ld(out2) if out2 is not None else 0, ptr(rowdot), stream())
+
+    def _linear(self, x, name, out, beta=0.0):
+        K.gemm(x, self.P(name + "_weight"), out, trans_b=True, epi=K.EPI_BIAS, bias=self.P(name + "_bias"), beta=beta)
+
+    def _modal_feature(self, w, m, train, masks=None):
+        """getImageFeats / getTextFeats (:225-239) -> w['F'][m] (and the saved BN inputs)."""
+        mod = ("image", "text")[m]
+        X = self.v_feat if m == 0 else self.t_feat
+        I = self.n_items
+        c0 = 3 * m
+        mk = w["masks"]
+        if train:
+            for j, site in enumerate(("residual", "modal")):
+                given = masks.get(f"{mod}_{site}_project_3") if masks else None
+                if given is not None:
+                    mk[2 * m + j].copy_(torch.as_tensor(given, dtype=torch.uint8))
+                else:
+                    _lib.call("gmr_keep_mask_u8", I * 64, 0.9, self.seed, self._mask_step(m, j), ptr(mk[2 * m + j]),
+                              stream())
+        self._linear(X, f"{mod}_residual_project_0", w["Zr"][m])
+        self._bn(w, c0, w["Zr"][m], I, ACT_LEAKY, train, y=w["Xr"][m], keep=mk[2 * m] if train else None)
+        self._linear(w["Xr"][m], f"{mod}_modal_project_0", w["Zm"][m])
+        self._bn(w, c0 + 1, w["Zm"][m], I, ACT_LEAKY, train, keep=mk[2 * m + 1] if train else None, post=POST_RES,
+                 aux=w["Xr"][m], rs=self.P("res_scale"), out2=w["F"][m])
+        return w["F"][m]
+
+    def _mask_step(self, m, j):
+        return (self._step * 8 + 2 * m + j) * 2 + (0 if self.training_mode else 1)
+
+    def _content(self, w):
+        """user_item_GCN on norm_adj and the rebuilt UI graph, softmax-weighted (:255-264, :332-336)."""
+        E = self.rec_slab.view("E0")
+        self.norm_adj.spmm(w["A1"], [(E,)])
+        self.image_UI_matrix.spmm(w["A2"], [(E,)])
+        _lib.call("gmr_gr_content_fwd", self.N, ptr(E), ptr(w["A1"]), ptr(w["A2"]), ptr(self.P("origin_weight")),
+                  ptr(self.P("generation_weight")), ptr(w["C"]), stream())
+        return w["C"]
+
+    def _forward(self, w, train, masks=None):
+        """GenRecV1.forward (:330-353): content -> C, side -> SIDE (train mode: BN batch statistics,
+        running-stat updates, dropout)."""
+        U, I, N = self.n_users, self.n_items, self.N
+        iE = self.rec_slab.view("E0")[U:]
+        self._content(w)
+        for m, (gate, ii) in enumerate((("gate_image_modal", self.image_II_matrix),
+                                        ("gate_text_modal", self.text_II_matrix))):
+            F = self._modal_feature(w, m, train, masks)
+            self._linear(F, gate + "_0", w["Zg"][m])
+            self._bn(w, 3 * m + 2, w["Zg"][m], I, ACT_SIGMOID, train, y=w["Gt"][m], post=POST_MUL, aux=iE,
+                     out2=w["Pm"][m])
+            MOD = w["MOD"][m]
+            ii.spmm(MOD[U:], [(w["Pm"][m],)])                 # item_item_GCN (n_layers = 1)
+            self.R.spmm(MOD[:U], [(MOD[U:],)])                 # users <- R @ items
+        wc2 = self.P("caculate_common_3_weight").view(64)
+        for m in range(2):
+            self._linear(w["MOD"][m], "caculate_common_0", w["Zc"][m])
+            self._bn(w, 6 + m, w["Zc"][m], N, ACT_TANH, train, post=POST_ROWDOT, aux=wc2, rowdot=w["a"][m])
+        for m, gate in enumerate(("gate_image_modal", "gate_text_modal")):
+            self._linear(w["C"], gate + "_0", w["Zp"][m])
+            self._bn(w, 8 + m, w["Zp"][m], N, ACT_SIGMOID, train, y=w["PG"][m])
+        _lib.call("gmr_gr_fusion_fwd", N, ptr(w["MOD"][0]), ptr(w["MOD"][1]), ptr(w["a"][0]), ptr(w["a"][1]),
+                  ptr(w["PG"][0]), ptr(w["PG"][1]), ptr(w["SIDE"]), ptr(w["alpha"]), stream())
+        return w["C"], w["SIDE"]
+
+    # ================================================================= fused rec step
+    def _nce(self, w, i1, i2, coef, rows):
+        """InfoNCE(nv[i1], nv[i2]) (:407-414): loss rows + gradients into g[i1], g[i2]."""
+        B = w["B"] if rows is None else rows.numel()
+        v1, v2 = w["nv"][i1][:B], w["nv"][i2][:B]
+        L = w["L"][:B, :B]
+        inv_t = 1.0 / self.temp
+        K.gemm(v1, v2, L, trans_b=True, alpha=inv_t)
+        _lib.call("gmr_nce_rows_f32", B, ptr(L), L.stride(0), coef, ptr(rows), stream())
+        K.gemm(L, v2, w["g"][i1][:B], alpha=inv_t, beta=1.0)
+        K.gemm(L, v1, w["g"][i2][:B], trans_a=True, alpha=inv_t, beta=1.0)
+
+    def rec_step(self, users, pos, neg, plan_bpr=None, plan_cl=None, norm_rows=None, reg_share=1.0, masks=None):
+        """calculate_loss (:355-405) and all rec-parameter gradients (into rec_slab.grad)."""
+        if self.image_UI_matrix is None:
+            return torch.zeros((), device=self.device)  # the reference returns 0 before the first rebuild (:363-364)
+        B = users.numel()
+        nr = float(norm_rows or B)
+        w = self._work(B)
+        U, I, N = self.n_users, self.n_items, self.N
+        s = self.rec_slab
+        E0 = s.view("E0")
+        if plan_bpr is None:
+            plan_bpr, plan_cl = self._plans(users, pos, neg)
+        C, SIDE = self._forward(w, True, masks)
+        # ---- losses
+        contrib, cs = w["contrib"][:3 * B], w["contrib_s"][:2 * B]
+        _lib.call("gmr_bpr_logsigmoid_f32", B, U, ptr(C), ptr(users), ptr(pos), ptr(neg), ptr(w["loss_bpr"]),
+                  ptr(contrib), 1.0 / nr, stream())
+        loss = w["loss"][:1]
+        _lib.call("gmr_sum_f32", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(loss), 0, stream())
+        _lib.call("gmr_sqnorm_f32", N * 64, ptr(E0), self.reg_weight * reg_share, ptr(loss), 1, ptr(w["sqws"]),
+                  stream())
+        # gathered views: 0 = C[users], 1 = C[U+pos], 2 = SIDE[users], 3 = SIDE[U+pos]
+        for j, (src, idx, off) in enumerate(((C, users, 0), (C, pos, U), (SIDE, users, 0), (SIDE, pos, U))):
+            K.gather_rows(src, idx, w["raw"][j][:B], off=off)
+            K.normalize_rows(w["raw"][j][:B], w["nv"][j][:B], w["nrm"][j][:B])
+        K.zero_(w["g"])
+        for k, (i1, i2, reg) in enumerate(((3, 1, self.ssl_reg1), (2, 0, self.ssl_reg1),
+                                           (0, 1, self.ssl_reg2), (0, 3, self.ssl_reg2))):
+            rows = w["rows"][k][:B]
+            self._nce(w, i1, i2, reg / nr, rows)
+            _lib.call("gmr_sum_f32", B, ptr(rows), reg / nr, ptr(loss), 1, stream())
+        K.normalize_rows_bwd(w["nv"][0][:B], w["nrm"][0][:B], w["g"][0][:B], contrib[:B], accumulate=True)
+        K.normalize_rows_bwd(w["nv"][1][:B], w["nrm"][1][:B], w["g"][1][:B], contrib[B:2 * B], accumulate=True)
+        K.normalize_rows_bwd(w["nv"][2][:B], w["nrm"][2][:B], w["g"][2][:B], cs[:B])
+        K.normalize_rows_bwd(w["nv"][3][:B], w["nrm"][3][:B], w["g"][3][:B], cs[B:])
+        dC, dS = w["dC"], w["dS"]
+        K.zero_(dC)
+        K.zero_(dS)
+        _lib.call("gmr_scatter_sorted_f32", plan_bpr.numel(), 64, ptr(plan_bpr), ptr(contrib), 64, ptr(dC), 64, stream())
+        _lib.call("gmr_scatter_sorted_f32", plan_cl.numel(), 64, ptr(plan_cl), ptr(cs), 64, ptr(dS), 64, stream())
+        self._backward(w, reg_share)
+        self._step += 1
+        return loss[0]
+
+    def _bn_bwd(self, w, call, z, rows, act, dy=None, mul=None, keep=None, da=None, dz=None, acc_dz=False):
+        name = _BN_CALLS[call]
+        pre = name[:-2]
+        st = w["stats"][call]
+        dv = self.G("caculate_common_3_weight").view(64) if da is not None else None
+        _lib.call("gmr_bn_bwd_f32", rows, ptr(z), K._ld(z), ptr(st[0]), ptr(st[1]), ptr(self.P(pre + "_1_weight")),
+                  ptr(self.P(pre + "_1_bias")), act, 0.2, ptr(keep), 64 if keep is not None else 0, 1.0 / 0.9,
+                  ptr(dy), K._ld(dy) if dy is not None else 0, ptr(mul), K._ld(mul) if mul is not None else 0,
+                  ptr(da), ptr(self.P("caculate_common_3_weight").view(64)) if da is not None else None,
+                  ptr(w["parts"]), ptr(w["sums"]), ptr(self.G(pre + "_1_weight")), ptr(self.G(pre + "_1_bias")),
+                  ptr(dv), 1, ptr(dz), K._ld(dz), int(acc_dz), stream())
+        return dz
+
+    def _linear_bwd(self, dz, x, name, dx=None, dx_beta=0.0):
+        """y = x W^T + b: dW += dz^T x, db += colsum(dz), dx (+)= dz W."""
+        K.gemm(dz, x, self.G(name + "_weight"), trans_a=True, beta=1.0)
+        K.colsum(dz, self.G(name + "_bias"), accumulate=True)
+        if dx is not None:
+            K.gemm(dz, self.P(name + "_weight"), dx, beta=dx_beta)
+
+    def _backward(self, w, reg_share):
+        U, I, N = self.n_users, self.n_items, self.N
+        s = self.rec_slab
+        s.zero_grad()
+        E0 = s.view("E0")
+        gE = s.gview("E0")
+        iE = E0[U:]
+        dC, dS, dM, dZ = w["dC"], w["dS"], w["dM"], w["dZ"]
+        _lib.call("gmr_gr_fusion_bwd", N, ptr(w["MOD"][0]), ptr(w["MOD"][1]), ptr(w["alpha"]), ptr(w["PG"][0]),
+                  ptr(w["PG"][1]), ptr(dS), ptr(dM[0]), ptr(dM[1]), ptr(w["da"][0]), ptr(w["da"][1]), ptr(w["dPG"][0]),
+                  ptr(w["dPG"][1]), stream())
+        # prefer gates on the content table (:344-345)
+        for m, gate in enumerate(("gate_image_modal", "gate_text_modal")):
+            self._bn_bwd(w, 8 + m, w["Zp"][m], N, ACT_SIGMOID, dy=w["dPG"][m], dz=dZ)
+            self._linear_bwd(dZ, w["C"], gate + "_0", dx=dC, dx_beta=1.0)
+        # attention scores (caculate_common on IMG / TXT, :313-323)
+        for m in range(2):
+            self._bn_bwd(w, 6 + m, w["Zc"][m], N, ACT_TANH, da=w["da"][m], dz=dZ)
+            self._linear_bwd(dZ, w["MOD"][m], "caculate_common_0", dx=dM[m], dx_beta=1.0)
+        # item_item_GCN branches (:266-306)
+        for m, (mod, gate) in enumerate((("image", "gate_image_modal"), ("text", "gate_text_modal"))):
+            d = dM[m]
+            self.RT.spmm(d[U:], [(d[:U],)], beta=1.0)                      # dP2 += R^T dU
+            self._ii_T[m].spmm(w["dP"], [(d[U:],)])                        # dP = II^T dP2
+            _lib.call("gmr_mul64_f32", I, ptr(w["dP"]), 64, ptr(w["Gt"][m]), 64, ptr(gE[U:]), 64, 1.0, 1, stream())
+            self._bn_bwd(w, 3 * m + 2, w["Zg"][m], I, ACT_SIGMOID, dy=w["dP"], mul=iE, dz=w["dZi"])
+            self._linear_bwd(w["dZi"], w["F"][m], gate + "_0", dx=w["dF"])
+            _lib.call("gmr_dot64_f32", I, ptr(w["Xr"][m]), 64, ptr(w["dF"]), 64, ptr(w["parts"]), 1.0,
+                      ptr(self.G("res_scale")), 1, stream())
+            mk = w["masks"]
+            self._bn_bwd(w, 3 * m + 1, w["Zm"][m], I, ACT_LEAKY, dy=w["dF"], keep=mk[2 * m + 1], dz=w["dZi"])
+            self._linear_bwd(w["dZi"], w["Xr"][m], f"{mod}_modal_project_0", dx=w["dX"])
+            _lib.call("gmr_axpy_dev_f32", I * 64, ptr(self.P("res_scale")), ptr(w["dF"]), ptr(w["dX"]), stream())
+            self._bn_bwd(w, 3 * m, w["Zr"][m], I, ACT_LEAKY, dy=w["dX"], keep=mk[2 * m], dz=w["dZi"])
+            X = self.v_feat if m == 0 else self.t_feat
+            self._linear_bwd(w["dZi"], X, f"{mod}_residual_project_0")
+        # content (user_item_GCN x 2, softmax weights) + regulariser
+        self.norm_adj.spmm(w["T1"], [(dC,)])
+        self.image_UI_matrix_T.spmm(w["T2"], [(dC,)])
+        _lib.call("gmr_gr_content_bwd", N, ptr(E0), ptr(w["A1"]), ptr(w["A2"]), ptr(dC), ptr(w["T1"]), ptr(w["T2"]),
+                  ptr(self.P("origin_weight")), ptr(self.P("generation_weight")), 2.0 * self.reg_weight * reg_share,
+                  ptr(w["parts"]), ptr(gE), ptr(self.G("origin_weight")), ptr(self.G("generation_weight")), stream())
+
+    def _plans(self, users, pos, neg):
+        B = users.numel()
+        dev = self.device
+        keys = torch.stack([users, pos, neg]).contiguous()
+        offs = torch.tensor([0, B], dtype=torch.int64, device=dev)
+        p2 = lambda n: 1 << max(1, (n - 1).bit_length())  # noqa: E731
+        pb = torch.empty((1, p2(3 * B)), dtype=torch.int64, device=dev)
+        pc = torch.empty((1, p2(2 * B)), dtype=torch.int64, device=dev)
+        ka = torch.tensor([0, self.n_users, self.n_users], dtype=torch.int32, device=dev)
+        _lib.call("gmr_sort_batch_keys", 1, ptr(keys), ptr(offs), ptr(ka), 3, B, ptr(pb), pb.shape[1], pb.shape[1],
+                  stream())
+        _lib.call("gmr_sort_batch_keys", 1, ptr(keys), ptr(offs), ptr(ka), 2, B, ptr(pc), pc.shape[1], pc.shape[1],
+                  stream())
+        return pb[0], pc[0]
+
+    # ================================================================= reference-facing API
+    def calculate_loss(self, interaction):
+        users, pos, neg = (interaction[i].to(torch.int32).contiguous() for i in range(3))
+        params = [getattr(self, n) for n in self.param_names()]
+        for p in params:
+            p.grad = None
+        return _RecLoss.apply(self, users, pos, neg, *params)
+
+    def getImageFeats(self):
+        w = self._work(1)
+        return self._modal_feature(w, 0, self.training_mode)
+
+    def getTextFeats(self):
+        w = self._work(1)
+        return self._modal_feature(w, 1, self.training_mode)
+
+    @torch.no_grad()
+    def forward_embeddings(self):
+        """content embeddings (the only part of forward full_sort_predict uses, :417-427)."""
+        w = self._work(1)
+        if self.image_UI_matrix is None:  # :419-421 scores are zeros before the first rebuild
+            K.zero_(w["C"])
+            return w["C"][:self.n_users], w["C"][self.n_users:]
+        C = self._content(w)
+        return C[:self.n_users], C[self.n_users:]
+
+    @torch.no_grad()
+    def forward(self, train=None):
+        """(content, side) like GenRecV1.forward; train defaults to the module mode."""
+        w = self._work(1)
+        return self._forward(w, self.training_mode if train is None else train)
+
+    @torch.no_grad()
+    def full_sort_predict(self, interaction):
+        user = interaction[0].to(torch.int32)
+        if self.image_UI_matrix is None:
+            return torch.zeros((user.numel(), self.n_items), device=self.device)  # :419-421
+        usr, itm = self.forward_embeddings()
+        ub = torch.empty((user.numel(), 64), device=self.device)
+        K.gather_rows(usr, user, ub)
+        scores = torch.empty((user.numel(), self.n_items), device=self.device)
+        K.gemm(ub, itm, scores, trans_b=True)
+        return scores
+
+    @torch.no_grad()
+    def topk_from_embeddings(self, usr, itm, users_i32, mask_rows, mask_cols, k, out_idx, scores_buf):
+        E = users_i32.numel()
+        ub = scores_buf.new_empty((E, 64))
+        K.gather_rows(usr, users_i32, ub)
+        sc = scores_buf[:E, :self.n_items]
+        K.gemm(ub, itm, sc, trans_b=True)
+        K.mask_scores(sc, mask_rows, mask_cols)
+        K.topk_rows(sc, k, out_idx)
+        return out_idx
+
+    def extra_state(self):
+        out = {"bn_state": {k: (v[0].cpu(), v[1].cpu()) for k, v in self.bn_state.items()}}
+        if self.image_UI_matrix is not None:
+            g = self.image_UI_matrix
+            out["image_UI_matrix"] = {"rowptr": g.rowptr.cpu(), "col": g.col.cpu(), "val": g.val.cpu()}
+        return out
+
+
+class FlipDiffusion:
+    """FlipInterestDiffusion (models/genrecv1.py:460-648) over device batches of users.
+
+    Batches are given as int32 user ids; x0 rows are densified from the train user CSR.  All draws
+    are Philox (seed, step); parity tests inject the reference's draws through `inject`."""
+
+    def __init__(self, model):
+        self.m = model
+        self.steps = model.steps
+        self.base_temp = model.flip_temp
+        self.sparse_temp = model.sparse_temp
+        self._w = None
+        self._parts = None
+
+    def _work(self, B):
+        if self._w is not None and self._w["B"] >= B:
+            return self._w
+        I = self.m.n_items
+        Ip = (I + 3) // 4 * 4
+        dev = self.m.device
+        f = lambda *s, dt=torch.float32: torch.empty(s, dtype=dt, device=dev)  # noqa: E731
+        self._w = {"B": B, "x0": f(B, Ip), "xt": f(B, Ip), "z": f(B, Ip), "dz": f(B, Ip), "probs": f(B, Ip),
+                   "tab": f(2 * self.steps + 2), "t": f(B, dt=torch.int32), "bce": f(B, dt=torch.float64),
+                   "kl": f(B, dt=torch.float64), "fe": f(I, 64), "o": f(2, B, 64), "nv": f(2, B, 64), "nrm": f(2, B),
+                   "L": f(B, (B + 3) // 4 * 4), "rows": f(B), "loss": f(4, dt=torch.float64), "lossf": f(2), "lossv": f(4),
+                   "topk": f(B, max(self.m.gen_topk, 1), dt=torch.int32)}
+        return self._w
+
+    def densify(self, users):
+        B = users.numel()
+        w = self._work(B)
+        I = self.m.n_items
+        x0 = w["x0"][:B, :I]
+        _lib.call("gmr_diff_densify", B, I, ptr(users), ptr(self.m.user_ptr), ptr(self.m.user_items), ptr(x0),
+                  x0.stride(0), stream())
+        return x0
+
+    def schedule(self, users):
+        w = self._work(users.numel())
+        _lib.call("gmr_flip_schedule", users.numel(), ptr(users), ptr(self.m.user_ptr), self.m.n_items, self.steps,
+                  ptr(w["tab"]), stream())
+        return w["tab"]
+
+    def p_sample(self, den, x0, tab, seed, step, inject=None, probs_out=None, q_steps=None):
+        """p_sample(steps = q_steps, bayesian) (:528-548): q_sample at t = q_steps - 1 (none when
+        q_steps = 0), then T model calls; the Bayesian step's coefficients are the q_sample tables at
+        that t (:541-542 re-index the q_sample tensors).  Returns the final x and the last probs."""
+        B, I = x0.shape
+        w = self._w
+        T = self.steps
+        qs = T if q_steps is None else int(q_steps)
+        if qs == 0:
+            raise NotImplementedError("p_sample with steps = 0 reads alpha tables left by an earlier call")
+        xt, z = w["xt"][:B, :I], w["z"][:B, :I]
+        inj = inject or {}
+        flip = inj.get("flip")
+        _lib.call("gmr_flip_qsample", B, I, ptr(x0), x0.stride(0), None, qs - 1, ptr(tab), T, self.base_temp,
+                  ptr(flip), flip.stride(0) if flip is not None else 0, seed, step * 16, ptr(xt), xt.stride(0), stream())
+        probs = probs_out if probs_out is not None else w["probs"][:B, :I]
+        for j, i in enumerate(reversed(range(T))):
+            den.forward(xt, t_const=i, T=T, out=z, seed=seed, step=step * 16 + 1 + j)
+            draws = inj.get("draws")
+            dr = draws[j] if draws is not None else None
+            _lib.call("gmr_flip_step", B, I, ptr(z), z.stride(0), ptr(tab), T, qs - 1, int(i == 0), ptr(dr),
+                      dr.stride(0) if dr is not None else 0, seed, step * 16 + 8 + j, ptr(xt), xt.stride(0),
+                      ptr(probs) if i == 0 else None, probs.stride(0), stream())
+        return xt, probs
+
+    def training_step(self, den, users, item_embeds, feats, seed, step, norm_rows=None, sched_users=None,
+                      inject=None):
+        """training_losses (:550-606) + the denoiser backward (only the BCE term carries gradient).
+        Returns the device loss vector [bce, kl, cl, total] (fp64; the loss of the rows held here,
+        normalised by norm_rows).  The BCE backward runs before the p_sample of the InfoNCE term
+        (which reuses the denoiser workspace); the reference's value is unchanged by the order."""
+        B = users.numel()
+        nr = float(norm_rows or B)
+        w = self._work(B)
+        I, T = self.m.n_items, self.steps
+        inj = inject or {}
+        x0 = self.densify(users)
+        tab = self.schedule(sched_users if sched_users is not None else users)
+        t = w["t"][:B]
+        if "t" in inj:
+            t.copy_(inj["t"])
+        else:
+            _lib.call("gmr_diff_sample_t", B, T, seed, step, ptr(t), stream())
+        xt, z, dz = w["xt"][:B, :I], w["z"][:B, :I], w["dz"][:B, :I]
+        flip = inj.get("flip1")
+        _lib.call("gmr_flip_qsample", B, I, ptr(x0), x0.stride(0), ptr(t), 0, ptr(tab), T, self.base_temp, ptr(flip),
+                  flip.stride(0) if flip is not None else 0, seed, step * 16 + 15, ptr(xt), xt.stride(0), stream())
+        den.forward(xt, t_rows=t, T=T, out=z, masks=inj.get("den_masks"), seed=seed, step=step * 16 + 14)
+        self.last_logits = z
+        _lib.call("gmr_flip_loss_rows", B, I, ptr(x0), x0.stride(0), ptr(z), z.stride(0), ptr(t), ptr(tab), T,
+                  1.0 / (nr * I), ptr(dz), dz.stride(0), ptr(w["bce"]), ptr(w["kl"]), stream())
+        den.backward(dz)
+        loss = w["loss"]
+        _lib.call("gmr_sum_f64", B, ptr(w["bce"]), 1.0 / (nr * I), ptr(loss[0:1]), 0, stream())
+        _lib.call("gmr_sum_f64", B, ptr(w["kl"]), 1.0 / nr, ptr(loss[1:2]), 0, stream())
+        # InfoNCE(x0 (iE * feats), p_sample(x0) (iE * feats)) — value only (:577-582)
+        gen, _ = self.p_sample(den, x0, tab, seed, step + 1, inject={"flip": inj.get("ps_flip"),
+                                                                     "draws": inj.get("ps_draws")})
+        cl = self.infonce_value(x0, gen, item_embeds, feats)
+        out = w["lossv"]
+        _lib.call("gmr_flip_total", ptr(loss), ptr(cl), 0.01, ptr(out), stream())
+        return out
+
+    def infonce_value(self, x0, gen, item_embeds, feats):
+        B, I = x0.shape
+        w = self._w
+        fe = w["fe"]
+        _lib.call("gmr_mul64_f32", I, ptr(item_embeds), K._ld(item_embeds), ptr(feats), K._ld(feats), ptr(fe), 64,
+                  1.0, 0, stream())
+        o = w["o"]
+        K.gemm(x0, fe, o[0][:B])
+        K.gemm(gen, fe, o[1][:B])
+        K.normalize_rows(o[0][:B], w["nv"][0][:B], w["nrm"][0][:B])
+        K.normalize_rows(o[1][:B], w["nv"][1][:B], w["nrm"][1][:B])
+        L = w["L"][:B, :B]
+        K.gemm(w["nv"][0][:B], w["nv"][1][:B], L, trans_b=True, alpha=1.0 / self.sparse_temp)
+        _lib.call("gmr_nce_rows_f32", B, ptr(L), L.stride(0), 0.0, ptr(w["rows"]), stream())
+        out = w["lossf"][:1]
+        _lib.call("gmr_sum_f32", B, ptr(w["rows"]), 1.0 / B, ptr(out), 0, stream())
+        return out
+
+    # ------------------------------------------------------------------ graph rebuild (trainer.py:736-789)
+    @torch.no_grad()
+    def rebuild_rows(self, den, users, out_topk, labels, ratio, seed, step, inject=None):
+        """One rebuild batch: p_sample(sampling_steps) -> gen_topk mask on the probabilities ->
+        InterestDebiase (labels given) -> top-rebuild_k of denoised * probs into out_topk
+        (ties -> lowest index).  Returns (denoised, probs) views of the work buffers."""
+        m = self.m
+        inj = inject or {}
+        B = users.numel()
+        I = m.n_items
+        x0 = self.densify(users)
+        tab = self.schedule(users)
+        w = self._w
+        probs = w["probs"][:B, :I]
+        xs, _ = self.p_sample(den, x0, tab, seed, step, inject=inj, probs_out=probs, q_steps=m.sampling_steps)
+        tk = w["topk"][:B, :m.gen_topk]
+        K.topk_rows(probs, m.gen_topk, tk)
+        dn = w["dz"][:B, :I]
+        _lib.call("gmr_gen_mask", B, I, m.gen_topk, ptr(tk), tk.stride(0), ptr(x0), ptr(xs), x0.stride(0), ptr(dn),
+                  dn.stride(0), stream())
+        self.gen_mask_topk = tk
+        if labels is not None:
+            self._debias(B, tk, x0, xs, dn, labels, ratio, seed, step, inj)
+        score = w["z"][:B, :I]
+        _lib.call("gmr_mul_f32", B * x0.stride(0), ptr(dn), ptr(probs), ptr(score), stream())
+        K.topk_rows(score, m.rebuild_k, out_topk)
+        return dn, probs
+
+    def _debias(self, B, tk, x0, xs, dn, labels, ratio, seed, step, inj):
+        """InterestDebiase.interest_query_debiase (interest_cluster.py:248-332)."""
+        I = self.m.n_items
+        kg = tk.shape[1]
+        maxp = B * kg
+        dev = self.m.device
+        if getattr(self, "_picks", None) is None or self._picks.shape[1] < maxp:
+            self._picks = torch.zeros((2, maxp, 2), dtype=torch.int32, device=dev)
+            self._npicks = torch.zeros(2, dtype=torch.int32, device=dev)
+        picks, npk = self._picks, self._npicks
+        if "dislike" in inj:  # parity: the reference's random.sample picks
+            cnt = []
+            for t, key in enumerate(("dislike", "like")):
+                pk = torch.as_tensor(np.asarray(inj[key]), dtype=torch.int32).reshape(-1, 2)
+                if pk.shape[0]:
+                    picks[t, :pk.shape[0]].copy_(pk)
+                cnt.append(pk.shape[0])
+            npk.copy_(torch.as_tensor(cnt, dtype=torch.int32))
+        else:
+            _lib.call("gmr_debias_select", B, kg, ptr(tk), tk.stride(0), ptr(x0), ptr(xs), x0.stride(0), float(ratio),
+                      seed, step, ptr(picks), picks.shape[1], ptr(npk), stream())
+        for t in range(2):
+            _lib.call("gmr_debias_apply", t, ptr(picks[t]), ptr(npk), picks.shape[1], ptr(x0), x0.stride(0), I,
+                      ptr(labels), ptr(dn), dn.stride(0), stream())

@@ -10,7 +10,7 @@ import torch
 
 from . import _lib
 
-EPI_NONE, EPI_BIAS, EPI_BIAS_TANH, EPI_LEAKY, EPI_POSTERIOR, EPI_DTANH, EPI_ROWSCALE_AUX = range(7)
+EPI_NONE, EPI_BIAS, EPI_BIAS_TANH, EPI_LEAKY, EPI_POSTERIOR, EPI_DTANH, EPI_ROWSCALE_AUX, EPI_BIAS_RELU, EPI_DRELU = range(9)
 
 _ws = {}
 
@@ -277,3 +277,64 @@ def eval_metrics(topk, pos_ptr, pos_items, ks, partials, out_sums):
     ks_t = ks
     _lib.call("gmr_eval_metrics", n, ptr(topk), _ld(topk), K, ptr(pos_ptr), ptr(pos_items), ks_t.numel(), ptr(ks_t),
               ptr(partials), ptr(out_sums), stream())
+
+
+# ----------------------------------------------------------------------------- GenRecV1 graphs
+def user_item_csr(n_users, n_items, user_ptr, user_items):
+    """R (U x I, binary) as a CSR over the train user CSR (models/genrecv1.py:128-131)."""
+    val = torch.ones(max(user_items.numel(), 1), dtype=torch.float32, device=user_ptr.device)[:user_items.numel()]
+    return CSR(user_ptr, user_items, val, n_cols=n_items, symmetric=False)
+
+
+def csr_transpose(a):
+    """A^T as a CSR (columns ascending per row), for the backward of non-symmetric SpMMs."""
+    dev = a.rowptr.device
+    nc = a.n_cols
+    trp = torch.empty(nc + 1, dtype=torch.int32, device=dev)
+    n = max(a.nnz, 1)
+    tcol = torch.empty(n, dtype=torch.int32, device=dev)
+    tval = torch.empty(n, dtype=torch.float32, device=dev)
+    scol = torch.empty(n, dtype=torch.int32, device=dev)
+    sval = torch.empty(n, dtype=torch.float32, device=dev)
+    ws = torch.empty(2 * nc, dtype=torch.int32, device=dev)
+    _lib.call("gmr_csr_transpose", a.n_rows, nc, a.nnz, ptr(a.rowptr), ptr(a.col), ptr(a.val), ptr(ws), ptr(trp),
+              ptr(tcol), ptr(tval), ptr(scol), ptr(sval), stream())
+    return CSR(trp, tcol[:a.nnz], tval[:a.nnz], n_cols=a.n_rows, symmetric=False)
+
+
+def csr_drop_edges(a, keep_rate, seed=0, step=0, keep=None):
+    """SpAdjDropEdge (models/genrecv1.py:443-457): each entry kept iff floor(u + keep_rate) >= 1,
+    kept values / keep_rate.  keep: optional 0/1 bytes per entry (CSR order) replacing the draws.
+    One host sync reads the kept count."""
+    dev = a.rowptr.device
+    orp = torch.empty(a.n_rows + 1, dtype=torch.int32, device=dev)
+    ws = torch.empty(a.n_rows, dtype=torch.int32, device=dev)
+    _lib.call("gmr_csr_drop_count", a.n_rows, ptr(a.rowptr), ptr(keep), float(keep_rate), int(seed), int(step),
+              ptr(ws), ptr(orp), stream())
+    nnz = int(orp[-1].item())
+    ocol = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    oval = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    _lib.call("gmr_csr_drop_write", a.n_rows, ptr(a.rowptr), ptr(a.col), ptr(a.val), ptr(keep), float(keep_rate),
+              int(seed), int(step), ptr(orp), ptr(ocol), ptr(oval), stream())
+    return CSR(orp, ocol[:nnz], oval[:nnz], n_cols=a.n_cols, symmetric=False)
+
+
+def knn_graph(feat, k):
+    """_build_knn_adj (common/trainer.py:682-687 -> utils/utils.py:184-197): cosine similarity on the
+    MFMA GEMM, per-row top-k, 'sym' normalisation.  Returns the I x I CSR."""
+    n, d = feat.shape
+    dev = feat.device
+    fn = torch.empty((n, d), dtype=torch.float32, device=dev)
+    normalize_rows(feat, fn)
+    sim = torch.empty((n, (n + 3) // 4 * 4), dtype=torch.float32, device=dev)[:, :n]
+    gemm(fn, fn, sim, trans_b=True)
+    ti = torch.empty((n, k), dtype=torch.int32, device=dev)
+    tv = torch.empty((n, k), dtype=torch.float32, device=dev)
+    topk_rows(sim, k, ti, tv)
+    del sim
+    rp = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(n * k, dtype=torch.int32, device=dev)
+    val = torch.empty(n * k, dtype=torch.float32, device=dev)
+    dis = torch.empty(n, dtype=torch.float32, device=dev)
+    _lib.call("gmr_knn_symnorm_csr", n, k, ptr(ti), k, ptr(tv), k, ptr(dis), ptr(rp), ptr(col), ptr(val), stream())
+    return CSR(rp, col, val, n_cols=n, symmetric=False)

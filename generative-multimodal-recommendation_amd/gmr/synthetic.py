@@ -13,7 +13,11 @@ SHAPES = {
     "baby": (19445, 7050, 160792, 4096, 384),
     "sports": (35598, 18357, 296337, 4096, 384),
     "tiny": (600, 400, 6000, 256, 64),
+    # TikTok-shaped (config 5; public GenRec-V1 statistics, shape only): image 128-d, text 768-d
+    "tiktok": (9319, 6710, 59541, 128, 768),
 }
+# feature value distributions: Amazon shapes as above; TikTok features N(0, 1)
+GAUSSIAN_FEATS = {"tiktok"}
 
 
 def make_interactions(n_users, n_items, n_inter, seed=0, zipf_s=0.8):
@@ -41,11 +45,13 @@ def make_interactions(n_users, n_items, n_inter, seed=0, zipf_s=0.8):
     return np.concatenate(users), np.concatenate(items), np.concatenate(labels)
 
 
-def make_features(n_items, dv, dt, seed=0):
+def make_features(n_items, dv, dt, seed=0, gaussian=False):
     rng = np.random.default_rng(seed + 1)
-    v = np.abs(rng.standard_normal((n_items, dv), dtype=np.float32))
+    v = rng.standard_normal((n_items, dv), dtype=np.float32)
     t = rng.standard_normal((n_items, dt), dtype=np.float32)
-    t /= np.linalg.norm(t, axis=1, keepdims=True)
+    if not gaussian:
+        v = np.abs(v)
+        t /= np.linalg.norm(t, axis=1, keepdims=True)
     return v, t
 
 
@@ -54,5 +60,5 @@ def make_dataset(config, shape="baby", seed=0):
     from .dataset import RecDataset
     U, I, n, dv, dt = SHAPES[shape]
     u, i, lb = make_interactions(U, I, n, seed)
-    v, t = make_features(I, dv, dt, seed)
+    v, t = make_features(I, dv, dt, seed, gaussian=shape in GAUSSIAN_FEATS)
     return RecDataset.from_arrays(config, u, i, lb, user_num=U, item_num=I, v_feat=v, t_feat=t)

@@ -309,3 +309,112 @@ class DiffMMTrainer(Trainer):
         dl = self._dloss.cpu().numpy() / max(steps, 1)
         self.logger.info(f"Diffusion Loss: Image={dl[0]:.4f}, Text={dl[1]:.4f}")
         return rec_loss, batches
+
+
+class GenRecV1Trainer(Trainer):
+    """common/trainer.py:588-820 — per epoch: diffusion training of the image denoiser (FlipInterest
+    diffusion over all users), the image UI-graph rebuild (p_sample, gen_topk mask, InterestDebiase,
+    rebuild_k top-k, SpAdjDropEdge), then the BPR/contrastive epoch.  The kNN item-item graphs and the
+    K-means interest clusters are built once at construction, on the device."""
+
+    # optimal cluster counts by dataset (trainer.py:632-648); other datasets use the TikTok values
+    OPTIMAL_K = {"tiktok": (18, 59), "baby": (6, 11), "sports": (9, 12)}
+
+    def __init__(self, config, model, mg=False):
+        super().__init__(config, model, mg)
+        lr = config["learning_rate"]
+        self.denoise_opt_image = FlatAdam([model.denoise_model_image.slab], lr=lr, weight_decay=0.0)
+        self.item_num, self.user_num = model.n_items, model.n_users
+        model.build_item_item_graphs(int(config["knn_k"] or 10))
+        self.multimodal_interest_space = None
+        self.debias = bool(config["OpenInterestDebiase"]) if "OpenInterestDebiase" in config else False
+        self.sample_ratio = float(config["sample_ratio"] if config["sample_ratio"] is not None else 0.1)
+        if self.debias:
+            self._init_interest_clustering()
+        self._perm = torch.empty(self.user_num, dtype=torch.int32, device=self.device)
+        self._users = torch.arange(self.user_num, dtype=torch.int32, device=self.device)
+        self._dloss = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self._one = torch.ones(1, dtype=torch.float32, device=self.device)
+        self._epoch_ctr = 0
+
+    def _init_interest_clustering(self):
+        """MultimodalCluster.multimodal_specific_cluster for image and text (trainer.py:611-671): labels by
+        device K-means; InterestDebiase consumes the image labels (interest_cluster.py:258-267)."""
+        from .kmeans import kmeans_labels
+        ik, tk = self.OPTIMAL_K.get(str(self.config["dataset"]), (18, 59))
+        m = self.model
+        self.logger.info("Performing Multimodal Clustering...")
+        img = kmeans_labels(m.v_feat, ik, seed=m.seed)
+        txt = kmeans_labels(m.t_feat, min(tk, 64), seed=m.seed + 1)
+        self.multimodal_interest_space = {"image_modal": img, "text_modal": txt}
+        self.logger.info("Multimodal Clustering Done.")
+
+    def diffusion_phase(self, epoch_idx):
+        """trainer.py:689-728: train the image denoiser over all users in shuffled batches.
+        Data parallel: a global step covers world x batch users; each rank takes a contiguous slice,
+        the schedule / pos_weight use the whole global batch (as the reference's batch)."""
+        m = self.model
+        m.train()
+        B = self.config["train_batch_size"]
+        U = self.user_num
+        W, r = dist.world(), dist.rank()
+        iE = m.rec_slab.view("E0")[m.n_users:]                # getItemEmbeds().detach() (:698)
+        feats_i = m.getImageFeats()                           # train mode: BN statistics + dropout (:699)
+        m.getTextFeats()                                      # :700 (its BN statistics update)
+        den = m.denoise_model_image
+        diff = m.diffusion_model
+        _lib.call("gmr_permutation", U, m.seed, 2000 + self._epoch_ctr, ptr(self._perm), stream())
+        K.zero_(self._dloss)
+        steps = 0
+        for g, lo in enumerate(range(0, U, B * W)):
+            hi = min(U, lo + B * W)
+            a, b = dist.shard(hi - lo, W, r)
+            users = self._perm[lo + a:lo + b]
+            step = ((self._epoch_ctr * 100000 + g) * W + r) * 4
+            if users.numel() > 0:
+                lv = diff.training_step(den, users, iE, feats_i, m.seed, step, norm_rows=hi - lo,
+                                        sched_users=self._perm[lo:hi])
+                _lib.call("gmr_axpy_dev_f32", 4, ptr(self._one), ptr(lv), ptr(self._dloss), stream())
+            else:
+                den.slab.zero_grad()
+            if W > 1:
+                dist.all_reduce_(den.slab.grad)
+            self.denoise_opt_image.step()
+            steps += 1
+        self._epoch_ctr += 1
+        return steps
+
+    @torch.no_grad()
+    def rebuild(self, chunk=None):
+        """trainer.py:730-789 on the device for users [lo, hi) of this rank; top-k rows all-gathered."""
+        m = self.model
+        U, I = self.user_num, self.item_num
+        kg, kr = m.gen_topk, m.rebuild_k
+        B = chunk or self.config["train_batch_size"]
+        dev = self.device
+        lo_r, hi_r, size = dist.padded_shard(U)
+        W = dist.world()
+        topk = torch.zeros((W * size, kr), dtype=torch.int32, device=dev)
+        den, diff = m.denoise_model_image, m.diffusion_model
+        labels = self.multimodal_interest_space["image_modal"] if self.debias else None
+        base = (self._epoch_ctr * 100000 + dist.rank()) * 1000
+        for j, lo in enumerate(range(lo_r, hi_r, B)):
+            hi = min(hi_r, lo + B)
+            diff.rebuild_rows(den, self._users[lo:hi],
+                              topk[lo - lo_r + dist.rank() * size:hi - lo_r + dist.rank() * size],
+                              labels, self.sample_ratio, m.seed, base + 4 * j)
+        dist.all_gather_rows_(topk, size)
+        uptr = torch.empty(U + 1, dtype=torch.int32, device=dev)
+        uitems = torch.empty(U * kr, dtype=torch.int32, device=dev)
+        K.topk_to_user_csr(topk[:U], uptr, uitems)
+        g = K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0)
+        g = K.csr_drop_edges(g, m.keep_rate, seed=m.seed, step=5000 + self._epoch_ctr)     # edgeDropper (:789)
+        m.set_image_ui_matrix(g)
+
+    def _train_epoch(self, train_data, epoch_idx, loss_func=None):
+        steps = self.diffusion_phase(epoch_idx)
+        self.rebuild()
+        rec_loss, batches = super()._train_epoch(train_data, epoch_idx)
+        dl = self._dloss.cpu().numpy() / max(steps, 1)
+        self.logger.info(f"Diffusion Loss: {dl[3]:.4f}")
+        return rec_loss, batches

@@ -7,7 +7,7 @@ import numpy as np
 import torch
 
 # model name -> module of this package (reference: importlib of models.<name.lower()>, utils.py:28-41)
-_MODELS = {"DiffMM": "diffmm", "DiffRec": "diffrec", "VBPR": "vbpr"}
+_MODELS = {"DiffMM": "diffmm", "DiffRec": "diffrec", "VBPR": "vbpr", "GenRecV1": "genrecv1"}
 
 
 def get_local_time():
@@ -22,10 +22,12 @@ def get_model(model_name):
 
 
 def get_trainer(model_name=None):
-    """DiffMM -> DiffMMTrainer, anything else -> Trainer (utils.py:44-58)."""
+    """DiffMM -> DiffMMTrainer, GenRecV1 -> GenRecV1Trainer, anything else -> Trainer (utils.py:44-58)."""
     mod = importlib.import_module(f"{__package__}.trainer")
     if model_name == "DiffMM":
         return mod.DiffMMTrainer
+    if model_name == "GenRecV1":
+        return mod.GenRecV1Trainer
     return mod.Trainer
 
 

@@ -37,6 +37,8 @@ extern "C" {
                                   c2 = rv2 ? rv2[m] : beta            p_sample posterior mean */
 #define GMR_EPI_DTANH 5        /* C = alpha*acc * (1 - aux[m,n]^2)      tanh backward      */
 #define GMR_EPI_ROWSCALE_AUX 6 /* C = alpha*acc + bias + rv1[m]*aux[m,n]                  */
+#define GMR_EPI_BIAS_RELU 7    /* C = relu(alpha*acc + bias)        TransformerDecoderLayer FF */
+#define GMR_EPI_DRELU 8        /* C = aux[m,n] > 0 ? alpha*acc : 0  ReLU (+ dropout) backward  */
 
 const char* gmr_last_error_string(void);
 int gmr_version(void);
@@ -217,6 +219,150 @@ int64_t gmr_eval_metrics_partials(int64_t n_users);
 int gmr_eval_metrics(int64_t n_users, const int32_t* topk, int64_t ld_topk, int32_t K, const int64_t* pos_ptr,
                      const int32_t* pos_items, int32_t n_ks, const int32_t* ks, double* partials, double* out_sums,
                      void* stream);
+
+/* ---------------------------------------------------------------- GenRecV1 rec step (models/genrecv1.py:225-427)
+ * Tables are rows x 64 fp32.  BatchNorm1d(64) (eps, momentum as nn.BatchNorm1d): train mode uses
+ * batch statistics and updates run_mean/run_var (unbiased var); eval mode uses them.  Fused:
+ * y = act(BN(z)) [* keep * keep_scale] (act 0 none, 1 leaky(slope), 2 sigmoid, 3 tanh) and the
+ * post op: 0 none, 1 out2 = rs[0]*aux + y (res_scale residual, :229), 2 out2 = aux*y (gate product,
+ * :268), 3 rowdot[r] = <y_r, aux[0:64]> (Linear(64, 1, bias=False), :88).
+ * Replaces nn.BatchNorm1d + activation + Dropout chains at genrecv1.py:84-89,155-164,166-222.
+ * parts: gmr_bn_parts_doubles(rows) doubles; mean/invstd: 64 floats each (saved for backward). */
+int64_t gmr_bn_parts_doubles(int64_t rows);
+int gmr_bn_fwd_f32(int64_t rows, const float* z, int64_t ldz, int32_t train, float eps, float momentum, float* run_mean,
+                   float* run_var, double* parts, float* mean, float* invstd, const float* w, const float* b,
+                   int32_t act, float slope, const uint8_t* keep, int64_t ld_keep, float keep_scale, float* y,
+                   int64_t ldy, int32_t post, const float* aux, int64_t ld_aux, const float* rs, float* out2,
+                   int64_t ld2, float* rowdot, void* stream);
+/* backward of the above (train mode): upstream = dy (* mul) or, for post 3, da[r] * v[c]; writes
+ * dz (accumulated if asked), dw/db (and dv for post 3; accumulated if asked); sums: 128 floats. */
+int gmr_bn_bwd_f32(int64_t rows, const float* z, int64_t ldz, const float* mean, const float* invstd, const float* w,
+                   const float* b, int32_t act, float slope, const uint8_t* keep, int64_t ld_keep, float keep_scale,
+                   const float* dy, int64_t lddy, const float* mul, int64_t ld_mul, const float* da, const float* v,
+                   double* parts, float* sums, float* dw, float* db, float* dv, int32_t accumulate_params, float* dz,
+                   int64_t lddz, int32_t accumulate_dz, void* stream);
+/* content = w0 (E + A1)/2 + w1 (E + A2)/2, w = softmax(origin_weight, generation_weight) (:255-264,:332-336)
+ * and its backward (T_k = A_k^T dC; dE += ... + reg2 E; d(ow, gw) accumulated); parts: gmr_gr_parts doubles */
+int64_t gmr_gr_parts(int64_t n);
+int gmr_gr_content_fwd(int64_t n, const float* E, const float* A1, const float* A2, const float* ow, const float* gw,
+                       float* C, void* stream);
+int gmr_gr_content_bwd(int64_t n, const float* E, const float* A1, const float* A2, const float* dC, const float* T1,
+                       const float* T2, const float* ow, const float* gw, float reg2, double* parts, float* dE,
+                       float* dow, float* dgw, void* stream);
+/* gate_attention_fusion + prefer gates (:309-353): SIDE = (PI (IMG-COM) + PT (TXT-COM) + COM)/4 */
+int gmr_gr_fusion_fwd(int64_t n, const float* IMG, const float* TXT, const float* aI, const float* aT,
+                      const float* PI, const float* PT, float* SIDE, float* alpha, void* stream);
+int gmr_gr_fusion_bwd(int64_t n, const float* IMG, const float* TXT, const float* alpha, const float* PI,
+                      const float* PT, const float* dSIDE, float* dIMG, float* dTXT, float* daI, float* daT,
+                      float* dPI, float* dPT, void* stream);
+/* out (+)= scale * a * b (rows x 64); out = sum(a * b) * scale (+ out), deterministic (parts >= 1024 doubles) */
+int gmr_mul64_f32(int64_t rows, const float* a, int64_t lda, const float* b, int64_t ldb, float* out, int64_t ldo,
+                  float scale, int32_t accumulate, void* stream);
+int gmr_dot64_f32(int64_t rows, const float* a, int64_t lda, const float* b, int64_t ldb, double* parts, float scale,
+                  float* out, int32_t accumulate, void* stream);
+/* InfoNCE rows on L = v1 v2^T / temp (B x B, in place; :407-414): loss[r] = lse(L_r) - L_rr and
+ * L <- coef (softmax - I) for the two gradient GEMMs (coef 0: loss only) */
+int gmr_nce_rows_f32(int64_t B, float* L, int64_t ld, float coef, float* loss, void* stream);
+/* BPR with log-sigmoid (:377-380) over one (U + I) x 64 table; contrib = [dU; dP; dN] */
+int gmr_bpr_logsigmoid_f32(int32_t B, int64_t U, const float* C, const int32_t* users, const int32_t* pos,
+                           const int32_t* neg, float* loss, float* contrib, float inv_norm, void* stream);
+
+/* y += alpha[0] x (device scalar); out = a * b (flat); Bernoulli(p_keep) keep bytes (nn.Dropout masks) */
+int gmr_axpy_dev_f32(int64_t n, const float* alpha, const float* x, float* y, void* stream);
+int gmr_mul_f32(int64_t n, const float* a, const float* b, float* out, void* stream);
+int gmr_keep_mask_u8(int64_t n, float p_keep, uint64_t seed, uint64_t step, uint8_t* out, void* stream);
+
+/* ---------------------------------------------------------------- GenRecV1 graphs (§8a G2, G6)
+ * CSR transpose (columns ascending in every output row, values carried); workspace 2*n_cols ints,
+ * stage_col/stage_val nnz entries.  Backward of the non-symmetric SpMMs (dropped UI graph, kNN, R). */
+int gmr_csr_transpose(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                      const float* val, int32_t* workspace, int32_t* t_rowptr, int32_t* t_col, float* t_val,
+                      int32_t* stage_col, float* stage_val, void* stream);
+/* SpAdjDropEdge (:443-457): keep e iff floor(u_e + keep_rate) >= 1 (Philox u, or keep[e]); values / keep_rate.
+ * Two calls: counts + out_rowptr (workspace n_rows ints), then the compaction. */
+int gmr_csr_drop_count(int64_t n_rows, const int32_t* rowptr, const uint8_t* keep, float keep_rate, uint64_t seed,
+                       uint64_t step, int32_t* workspace, int32_t* out_rowptr, void* stream);
+int gmr_csr_drop_write(int64_t n_rows, const int32_t* rowptr, const int32_t* col, const float* val,
+                       const uint8_t* keep, float keep_rate, uint64_t seed, uint64_t step, const int32_t* out_rowptr,
+                       int32_t* out_col, float* out_val, void* stream);
+/* kNN graph from per-row top-k (idx, sim) (utils/utils.py:184-197, 'sym'): deg = row sums of the
+ * kept sims (top-k order), w = d_r v d_c, d = deg^-1/2 (inf -> 0); rowptr n+1, col/val n*k */
+int gmr_knn_symnorm_csr(int64_t n, int32_t k, const int32_t* topi, int64_t ldi, const float* topv, int64_t ldv,
+                        float* dis_ws, int32_t* rowptr, int32_t* col, float* val, void* stream);
+/* rebuild (common/trainer.py:752-754): den = x0 with the gen_topk positions taken from xs */
+int gmr_gen_mask(int32_t B, int32_t I, int32_t k, const int32_t* topi, int64_t ldt, const float* x0, const float* xs,
+                 int64_t ld, float* den, void* stream);
+/* InterestDebiase (interest_cluster.py:186-332): exact-n uniform picks of 0->1 / 1->0 flips among the
+ * gen_topk positions (n = int(count * ratio)); picks[type][max_picks][2] = (row, item), n_picks[2];
+ * then the cluster rules (labels < 64) applied to den in place */
+int gmr_debias_select(int32_t B, int32_t k, const int32_t* topi, int64_t ldt, const float* x0, const float* xs,
+                      int64_t ld, float ratio, uint64_t seed, uint64_t step, int32_t* picks, int32_t max_picks,
+                      int32_t* n_picks, void* stream);
+int gmr_debias_apply(int32_t type, const int32_t* picks, const int32_t* n_picks, int32_t max_picks, const float* x0,
+                     int64_t ld0, int32_t I, const int32_t* labels, float* den, int64_t ldd, void* stream);
+/* K-means pieces (interest_cluster.py:60-79 — StandardScaler + KMeans): distances and centroid sums
+ * are GEMMs (gmr_gemm_f32) between these calls */
+int gmr_kmeans_standardize(int64_t n, int32_t d, const float* X, int64_t ldx, float* mean, float* scale, float* Y,
+                           int64_t ldy, float* sq, void* stream);
+int gmr_kmeans_pp_pick(int64_t n, const float* mind, uint64_t seed, uint64_t step, int32_t* out, void* stream);
+int gmr_kmeans_take_center(int32_t d, const float* X, int64_t ldx, const int32_t* idx, float* C, int64_t ldc,
+                           int32_t j, const float* xsq, float* csq, void* stream);
+int gmr_kmeans_min_dist(int64_t n, const float* xsq, const float* dots, const float* csq, int32_t j, float* mind,
+                        int32_t first, void* stream);
+int64_t gmr_kmeans_parts(int64_t n);
+int gmr_kmeans_assign(int64_t n, int32_t k, const float* dots, int64_t ldd, const float* csq, const float* xsq,
+                      int32_t* label, float* onehot_t, int64_t ldo, int32_t* changed, double* inertia_parts,
+                      void* stream);
+int gmr_kmeans_centroids(int32_t k, int32_t d, const float* sums, int64_t lds, const float* onehot_t, int64_t ldo,
+                         int64_t n, float* C, int64_t ldc, float* csq, void* stream);
+
+/* ---------------------------------------------------------------- GenRecV1 generation (§8a G4, G5)
+ * FlipInterestDiffusion (models/genrecv1.py:460-648).  tables = [gamma_cum (T) | eps_cum (T) |
+ * pos_weight | sparsity] from the batch users' history sizes (get_cum, :480-498). */
+int gmr_flip_schedule(int32_t B, const int32_t* users, const int32_t* user_ptr, int32_t I, int32_t T, float* tables,
+                      void* stream);
+/* q_sample (:512-526): x_t = x0 xor Bernoulli(sigmoid((a_t - u) temp)); flip (0/1 bytes) replaces the draws */
+int gmr_flip_qsample(int32_t B, int32_t I, const float* x0, int64_t ld0, const int32_t* t, int32_t t_const,
+                     const float* tables, int32_t T, float temp, const uint8_t* flip, int64_t ld_flip, uint64_t seed,
+                     uint64_t step, float* xt, int64_t ldt, void* stream);
+/* one p_sample step on the model logits (:536-548); probs may be NULL */
+int gmr_flip_step(int32_t B, int32_t I, const float* z, int64_t ldz, const float* tables, int32_t T, int32_t qi,
+                  int32_t last,
+                  const uint8_t* draws, int64_t ldd, uint64_t seed, uint64_t step, float* x, int64_t ldx, float* probs,
+                  int64_t ldp, void* stream);
+/* BCE(pos_weight) + curriculum KL rows (:550-627); dz = grad_scale * dBCE/dz (may alias z) */
+int gmr_flip_loss_rows(int32_t B, int32_t I, const float* x0, int64_t ld0, const float* z, int64_t ldz,
+                       const int32_t* t, const float* tables, int32_t T, float grad_scale, float* dz, int64_t lddz,
+                       double* bce_row, double* kl_row, void* stream);
+/* [bce, kl, cl, bce + kl + w_cl cl] (training_losses total, :604) */
+int gmr_flip_total(const double* bce_kl, const float* cl, float w_cl, float* out4, void* stream);
+/* ModalDenoiseTransformer rows (:650-710).  LayerNorm over D (64..1024) of s = a + keep*scale*b
+ * (b a matrix, or a broadcast row when ldb == 0; keep may be NULL), optional exact GELU after;
+ * saves s, mean, rstd.  Backward: dx (+)=, dw/db (+)= through parts (gmr_layernorm_parts_floats). */
+int gmr_layernorm_fwd(int64_t rows, int32_t D, const float* a, int64_t lda, const float* b, int64_t ldb,
+                      const uint8_t* keep, int64_t ld_keep, float keep_scale, const float* w, const float* bias,
+                      float eps, int32_t gelu, float* y, int64_t ldy, float* s_out, int64_t lds, float* mean,
+                      float* rstd, void* stream);
+int64_t gmr_layernorm_parts_floats(int64_t rows, int32_t D);
+int gmr_layernorm_bwd(int64_t rows, int32_t D, const float* s, int64_t lds, const float* mean, const float* rstd,
+                      const float* w, const float* bias, int32_t gelu, const float* dy, int64_t lddy, float* dx,
+                      int64_t lddx, int32_t accumulate_dx, float* parts, float* dw, float* db,
+                      int32_t accumulate_params, void* stream);
+/* adaLN (:702-703): h1 = h0 (1 + scale[t]) + shift[t], S = T x 2D [shift | scale]; backward writes
+ * dh0 and prod = dh1 * h0 (grouped column sums give dscale / dshift, gmr_colsum_f32) */
+int gmr_adaln_fwd(int64_t rows, int32_t D, const float* h0, int64_t ld0, const int32_t* t, int32_t t_const,
+                  const float* S, int64_t lds, float* h1, int64_t ld1, void* stream);
+int gmr_adaln_bwd(int64_t rows, int32_t D, const float* h0, int64_t ld0, const float* dh1, int64_t ldd,
+                  const int32_t* t, const float* S, int64_t lds, float* dh0, int64_t ldo, float* prod, int64_t ldp,
+                  void* stream);
+/* dropout with keep probability p_keep, one draw per (row, column / group) (group = head size for
+ * the attention-weight dropout of a length-1 sequence); mask_in replays a mask, mask_out records it */
+int gmr_dropout_f32(int64_t rows, int32_t D, int32_t group, const float* x, int64_t ldx, float p_keep,
+                    const uint8_t* mask_in, uint8_t* mask_out, int64_t ldm, uint64_t seed, uint64_t step, float* y,
+                    int64_t ldy, void* stream);
+/* sinusoidal time embedding table T x E (:692-696); SiLU (dy == NULL) or its backward */
+int gmr_time_embedding(int32_t T, int32_t E, float* out, void* stream);
+int gmr_silu_f32(int64_t n, const float* x, const float* dy, float* y, void* stream);
 
 /* ---------------------------------------------------------------- optimizer (torch.optim.Adam, trainer.py:125-142)
  * flat fp32 slabs; step_size = lr / (1 - b1^t), bias_correction2_sqrt = sqrt(1 - b2^t) */

@@ -180,3 +180,24 @@ def test_kmeans_labels_partition(G):
     lab, true = r["km_labels"], r["km_true"]
     pairs = set(zip(lab.tolist(), true.tolist()))
     assert len(pairs) == len(set(lab.tolist())) == len(set(true.tolist()))
+
+
+def test_init_matches_reference(G):
+    """Rec parameters drawn in the reference's constructor order under the same seed."""
+    from gmr.genrecv1 import _rec_init_twin  # CPU-only helper (no HIP call)
+    m = G["m"]
+    torch.manual_seed(999)
+    init = _rec_init_twin(int(m["U"]), int(m["I"]), 64, m["v_feat"].shape[1], m["t_feat"].shape[1])
+    for k, v in init.items():
+        assert np.array_equal(v.numpy(), m["p_" + k]), k
+
+
+def test_denoiser_init_order(G):
+    from gmr.transformer import _reference_init_twin
+    d = G["d"]
+    torch.manual_seed(4321)
+    twin = _reference_init_twin(int(d["I"]), 10, 8, int(d["n_layers"]), int(d["d_model"]), 0.2)
+    for n, p in twin.named_parameters():
+        assert np.array_equal(p.detach().numpy(), d["den_" + n.replace(".", "_")]), n
+
+
