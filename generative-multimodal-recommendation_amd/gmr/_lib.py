@@ -76,6 +76,49 @@ SIGNATURES = {
     "gmr_eval_metrics_partials": (I64, [I64]),
     "gmr_eval_metrics": (I32, [I64, P, I64, I32, P, P, I32, P, P, P, P]),
     "gmr_adam_f32": (I32, [I64, P, P, P, P, F32, F32, F32, F32, F32, F32, P]),
+    # GenRecV1
+    "gmr_bn_parts_doubles": (I64, [I64]),
+    "gmr_bn_fwd_f32": (I32, [I64, P, I64, I32, F32, F32, P, P, P, P, P, P, P, I32, F32, P, I64, F32, P, I64, I32, P, I64, P, P, I64, P, P]),
+    "gmr_bn_bwd_f32": (I32, [I64, P, I64, P, P, P, P, I32, F32, P, I64, F32, P, I64, P, I64, P, P, P, P, P, P, P, I32, P, I64, I32, P]),
+    "gmr_gr_parts": (I64, [I64]),
+    "gmr_gr_content_fwd": (I32, [I64, P, P, P, P, P, P, P]),
+    "gmr_gr_content_bwd": (I32, [I64, P, P, P, P, P, P, P, P, F32, P, P, P, P, P]),
+    "gmr_gr_fusion_fwd": (I32, [I64, P, P, P, P, P, P, P, P, P]),
+    "gmr_gr_fusion_bwd": (I32, [I64, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "gmr_mul64_f32": (I32, [I64, P, I64, P, I64, P, I64, F32, I32, P]),
+    "gmr_dot64_f32": (I32, [I64, P, I64, P, I64, P, F32, P, I32, P]),
+    "gmr_nce_rows_f32": (I32, [I64, P, I64, F32, P, P]),
+    "gmr_bpr_logsigmoid_f32": (I32, [I32, I64, P, P, P, P, P, P, F32, P]),
+    "gmr_axpy_dev_f32": (I32, [I64, P, P, P, P]),
+    "gmr_mul_f32": (I32, [I64, P, P, P, P]),
+    "gmr_keep_mask_u8": (I32, [I64, F32, U64, U64, P, P]),
+    "gmr_csr_transpose": (I32, [I64, I64, I64, P, P, P, P, P, P, P, P, P, P]),
+    "gmr_csr_drop_count": (I32, [I64, P, P, F32, U64, U64, P, P, P]),
+    "gmr_csr_drop_write": (I32, [I64, P, P, P, P, F32, U64, U64, P, P, P, P]),
+    "gmr_knn_symnorm_csr": (I32, [I64, I32, P, I64, P, I64, P, P, P, P, P]),
+    "gmr_gen_mask": (I32, [I32, I32, I32, P, I64, P, P, I64, P, P]),
+    "gmr_debias_select": (I32, [I32, I32, P, I64, P, P, I64, F32, U64, U64, P, I32, P, P]),
+    "gmr_debias_apply": (I32, [I32, P, P, I32, P, I64, I32, P, P, I64, P]),
+    "gmr_kmeans_standardize": (I32, [I64, I32, P, I64, P, P, P, I64, P, P]),
+    "gmr_kmeans_pp_pick": (I32, [I64, P, U64, U64, P, P]),
+    "gmr_kmeans_take_center": (I32, [I32, P, I64, P, P, I64, I32, P, P, P]),
+    "gmr_kmeans_min_dist": (I32, [I64, P, P, P, I32, P, I32, P]),
+    "gmr_kmeans_parts": (I64, [I64]),
+    "gmr_kmeans_assign": (I32, [I64, I32, P, I64, P, P, P, P, I64, P, P, P]),
+    "gmr_kmeans_centroids": (I32, [I32, I32, P, I64, P, I64, I64, P, I64, P, P]),
+    "gmr_flip_schedule": (I32, [I32, P, P, I32, I32, P, P]),
+    "gmr_flip_qsample": (I32, [I32, I32, P, I64, P, I32, P, I32, F32, P, I64, U64, U64, P, I64, P]),
+    "gmr_flip_step": (I32, [I32, I32, P, I64, P, I32, I32, I32, P, I64, U64, U64, P, I64, P, I64, P]),
+    "gmr_flip_loss_rows": (I32, [I32, I32, P, I64, P, I64, P, P, I32, F32, P, I64, P, P, P]),
+    "gmr_flip_total": (I32, [P, P, F32, P, P]),
+    "gmr_layernorm_fwd": (I32, [I64, I32, P, I64, P, I64, P, I64, F32, P, P, F32, I32, P, I64, P, I64, P, P, P]),
+    "gmr_layernorm_parts_floats": (I64, [I64, I32]),
+    "gmr_layernorm_bwd": (I32, [I64, I32, P, I64, P, P, P, P, I32, P, I64, P, I64, I32, P, P, P, I32, P]),
+    "gmr_adaln_fwd": (I32, [I64, I32, P, I64, P, I32, P, I64, P, I64, P]),
+    "gmr_adaln_bwd": (I32, [I64, I32, P, I64, P, I64, P, P, I64, P, I64, P, I64, P]),
+    "gmr_dropout_f32": (I32, [I64, I32, I32, P, I64, F32, P, P, I64, U64, U64, P, I64, P]),
+    "gmr_time_embedding": (I32, [I32, I32, P, P]),
+    "gmr_silu_f32": (I32, [I64, P, P, P, P]),
 }
 
 _lib = None
