@@ -38,7 +38,7 @@ __global__ void flip_schedule_kernel(int B, const int* __restrict__ users, const
   const float gstep = __fdiv_rn(__fsub_rn(ge, gs), (float)(T - 1));
   const float estep = __fdiv_rn(__fsub_rn(ee, es), (float)(T - 1));
   const int half = T / 2;
-  float gc = 1.f, ec = 1.f;
+  double gc = 1.0, ec = 1.0;  // ATen's CPU cumprod accumulates float in double (acc_type)
   for (int i = 0; i < T; ++i) {
     float g, e;
     if (i < half) {
@@ -49,10 +49,10 @@ __global__ void flip_schedule_kernel(int B, const int* __restrict__ users, const
       e = __fsub_rn(ee, __fmul_rn(estep, (float)(T - i - 1)));
     }
     e = fminf(e, 0.01f);
-    gc = __fmul_rn(gc, __fsub_rn(1.f, g));
-    ec = __fmul_rn(ec, __fsub_rn(1.f, e));
-    tab[i] = __fsub_rn(1.f, gc);
-    tab[T + i] = __fsub_rn(1.f, ec);
+    gc = __dmul_rn(gc, (double)__fsub_rn(1.f, g));
+    ec = __dmul_rn(ec, (double)__fsub_rn(1.f, e));
+    tab[i] = __fsub_rn(1.f, (float)gc);
+    tab[T + i] = __fsub_rn(1.f, (float)ec);
   }
   tab[2 * T] = __fdiv_rn(zeros, __fadd_rn((float)tot, 1e-8f));
   tab[2 * T + 1] = s;
@@ -156,8 +156,8 @@ __global__ void __launch_bounds__(256) flip_loss_kernel(int B, int I, const floa
 
 // ----------------------------------------------------------------- LayerNorm (one wave per row, D <= 1024)
 // s = a + keep * scale * b (b: matrix, or a broadcast vector when ldb == 0); y = LN(s) w + bias [-> GELU]
-template <int PER>  // floats per lane (D = 64 * PER)
-__global__ void __launch_bounds__(256) ln_fwd_kernel(int64_t rows, const float* __restrict__ a, int64_t lda,
+template <int PER>  // floats per lane (D = 64 * PER; PER 1 with Dsmall = 32 or 64)
+__global__ void __launch_bounds__(256) ln_fwd_kernel(int Dsmall, int64_t rows, const float* __restrict__ a, int64_t lda,
                                                      const float* __restrict__ bsrc, int64_t ldb,
                                                      const uint8_t* __restrict__ keep, int64_t ldk, float kscale,
                                                      const float* __restrict__ w, const float* __restrict__ bias,
@@ -167,17 +167,21 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(int64_t rows, const float* 
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int lane = threadIdx.x & 63;
-  constexpr int D = 64 * PER;
+  const int D = PER == 1 ? Dsmall : 64 * PER;  // PER == 1 also serves D = 32 (upper lanes idle)
+  const bool act = lane < D;
   float v[PER];
   float sum = 0.f;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int c = j * 64 + lane;
-    float x = a[r * lda + c];
-    if (bsrc) {
-      float bb = bsrc[(ldb ? r * ldb : 0) + c];
-      if (keep) bb = keep[r * ldk + c] ? bb * kscale : 0.f;
-      x += bb;
+    float x = 0.f;
+    if (act) {
+      x = a[r * lda + c];
+      if (bsrc) {
+        float bb = bsrc[(ldb ? r * ldb : 0) + c];
+        if (keep) bb = keep[r * ldk + c] ? bb * kscale : 0.f;
+        x += bb;
+      }
     }
     v[j] = x;
     sum += x;
@@ -186,10 +190,11 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(int64_t rows, const float* 
   float sq = 0.f;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    const float d = v[j] - mean;
+    const float d = act ? v[j] - mean : 0.f;
     sq += d * d;
   }
   const float rstd = 1.f / sqrtf(gmr::wave_sum(sq) / (float)D + eps);
+  if (!act) return;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int c = j * 64 + lane;
@@ -208,15 +213,17 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(int64_t rows, const float* 
 // dw/db column partials per block (rows blockIdx.x*RB .. ) -> part[blk][2*D]
 constexpr int kLnRowsPerBlock = 64;
 template <int PER>
-__global__ void __launch_bounds__(256) ln_bwd_kernel(int64_t rows, const float* __restrict__ s, int64_t lds,
+__global__ void __launch_bounds__(256) ln_bwd_kernel(int Dsmall, int64_t rows, const float* __restrict__ s, int64_t lds,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ w, const float* __restrict__ bias,
                                                      int gelu, const float* __restrict__ dy, int64_t lddy,
                                                      float* __restrict__ dx, int64_t lddx, int accumulate,
                                                      float* __restrict__ part) {
-  constexpr int D = 64 * PER;
-  __shared__ float red[4][2 * D];
+  constexpr int DM = 64 * PER;
+  const int D = PER == 1 ? Dsmall : DM;
+  __shared__ float red[4][2 * DM];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool act = lane < D;
   float pw[PER], pb[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) pw[j] = pb[j] = 0.f;
@@ -228,6 +235,10 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(int64_t rows, const float* 
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int c = j * 64 + lane;
+      if (!act) {
+        xh[j] = g[j] = 0.f;
+        continue;
+      }
       xh[j] = (s[r * lds + c] - mu) * rs;
       float d = dy[r * lddy + c];
       if (gelu) {
@@ -247,6 +258,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(int64_t rows, const float* 
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int c = j * 64 + lane;
+      if (!act) continue;
       float o = rs * (g[j] - s1 - xh[j] * s2);
       if (accumulate) o += dx[r * lddx + c];
       dx[r * lddx + c] = o;
@@ -254,12 +266,14 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(int64_t rows, const float* 
   }
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    red[wv][j * 64 + lane] = pw[j];
-    red[wv][D + j * 64 + lane] = pb[j];
+    red[wv][j * 64 + lane] = act ? pw[j] : 0.f;
+    red[wv][DM + j * 64 + lane] = act ? pb[j] : 0.f;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * D; c += 256)
-    part[(int64_t)blockIdx.x * 2 * D + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+  for (int c = threadIdx.x; c < 2 * D; c += 256) {
+    const int cc = c < D ? c : DM + (c - D);
+    part[(int64_t)blockIdx.x * 2 * D + c] = (red[0][cc] + red[1][cc]) + (red[2][cc] + red[3][cc]);
+  }
 }
 
 __global__ void ln_param_reduce_kernel(int P, int D, const float* __restrict__ part, float* __restrict__ dw,
@@ -401,13 +415,14 @@ extern "C" int gmr_layernorm_fwd(int64_t rows, int32_t D, const float* a, int64_
                                  const float* bias, float eps, int32_t gelu, float* y, int64_t ldy, float* s_out,
                                  int64_t lds, float* mean, float* rstd, void* stream) {
   GMR_ARG(a && w && bias && y && mean && rstd && rows > 0, "bad args");
-  GMR_ARG(D == 64 || D == 128 || D == 256 || D == 512 || D == 1024, "D must be 64..1024 (power of two)");
+  GMR_ARG(D == 32 || D == 64 || D == 128 || D == 256 || D == 512 || D == 1024, "D must be 32..1024 (power of two)");
   const dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
 #define GMR_LNF(P)                                                                                                \
-  hipLaunchKernelGGL(ln_fwd_kernel<P>, grid, dim3(256), 0, st, rows, a, lda, b, ldb, keep, ld_keep, keep_scale, w, \
-                     bias, eps, (int)gelu, y, ldy, s_out, lds, mean, rstd)
+  hipLaunchKernelGGL(ln_fwd_kernel<P>, grid, dim3(256), 0, st, (int)D, rows, a, lda, b, ldb, keep, ld_keep,        \
+                     keep_scale, w, bias, eps, (int)gelu, y, ldy, s_out, lds, mean, rstd)
   switch (D) {
+    case 32:
     case 64: GMR_LNF(1); break;
     case 128: GMR_LNF(2); break;
     case 256: GMR_LNF(4); break;
@@ -428,13 +443,14 @@ extern "C" int gmr_layernorm_bwd(int64_t rows, int32_t D, const float* s, int64_
                                  int64_t lddy, float* dx, int64_t lddx, int32_t accumulate_dx, float* parts, float* dw,
                                  float* db, int32_t accumulate_params, void* stream) {
   GMR_ARG(s && mean && rstd && w && bias && dy && dx && parts && dw && db && rows > 0, "bad args");
-  GMR_ARG(D == 64 || D == 128 || D == 256 || D == 512 || D == 1024, "D must be 64..1024 (power of two)");
+  GMR_ARG(D == 32 || D == 64 || D == 128 || D == 256 || D == 512 || D == 1024, "D must be 32..1024 (power of two)");
   hipStream_t st = (hipStream_t)stream;
   const int P = (int)((rows + kLnRowsPerBlock - 1) / kLnRowsPerBlock);
-#define GMR_LNB(PP)                                                                                              \
-  hipLaunchKernelGGL(ln_bwd_kernel<PP>, dim3(P), dim3(256), 0, st, rows, s, lds, mean, rstd, w, bias, (int)gelu, dy, \
-                     lddy, dx, lddx, (int)accumulate_dx, parts)
+#define GMR_LNB(PP)                                                                                                  \
+  hipLaunchKernelGGL(ln_bwd_kernel<PP>, dim3(P), dim3(256), 0, st, (int)D, rows, s, lds, mean, rstd, w, bias,         \
+                     (int)gelu, dy, lddy, dx, lddx, (int)accumulate_dx, parts)
   switch (D) {
+    case 32:
     case 64: GMR_LNB(1); break;
     case 128: GMR_LNB(2); break;
     case 256: GMR_LNB(4); break;

@@ -156,6 +156,9 @@ def check(rc, name="gmr"):
 
 
 def call(name, *args):
-    """Call an int-returning entry point and raise on a non-zero status."""
+    """Call an int-returning entry point and raise on a non-zero status (argument count checked:
+    ctypes would silently pass surplus arguments to a C function)."""
     fn = getattr(load(), name)
+    if len(args) != len(fn.argtypes):
+        raise TypeError(f"{name} takes {len(fn.argtypes)} arguments, got {len(args)}")
     return check(fn(*args), name)

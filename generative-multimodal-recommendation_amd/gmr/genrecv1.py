@@ -610,7 +610,6 @@ class FlipDiffusion:
         _lib.call("gmr_flip_qsample", B, I, ptr(x0), x0.stride(0), ptr(t), 0, ptr(tab), T, self.base_temp, ptr(flip),
                   flip.stride(0) if flip is not None else 0, seed, step * 16 + 15, ptr(xt), xt.stride(0), stream())
         den.forward(xt, t_rows=t, T=T, out=z, masks=inj.get("den_masks"), seed=seed, step=step * 16 + 14)
-        self.last_logits = z
         _lib.call("gmr_flip_loss_rows", B, I, ptr(x0), x0.stride(0), ptr(z), z.stride(0), ptr(t), ptr(tab), T,
                   1.0 / (nr * I), ptr(dz), dz.stride(0), ptr(w["bce"]), ptr(w["kl"]), stream())
         den.backward(dz)
@@ -661,8 +660,9 @@ class FlipDiffusion:
         tk = w["topk"][:B, :m.gen_topk]
         K.topk_rows(probs, m.gen_topk, tk)
         dn = w["dz"][:B, :I]
+        assert dn.stride(0) == x0.stride(0) == xs.stride(0)
         _lib.call("gmr_gen_mask", B, I, m.gen_topk, ptr(tk), tk.stride(0), ptr(x0), ptr(xs), x0.stride(0), ptr(dn),
-                  dn.stride(0), stream())
+                  stream())
         self.gen_mask_topk = tk
         if labels is not None:
             self._debias(B, tk, x0, xs, dn, labels, ratio, seed, step, inj)

@@ -130,3 +130,26 @@ def test_synthetic_recipe():
             assert (lab == 0).sum() == n - 2 and (lab == 1).sum() == 1 and (lab == 2).sum() == 1
     v, t = make_features(200, 32, 16)
     assert (v >= 0).all() and np.allclose(np.linalg.norm(t, axis=1), 1, atol=1e-5)
+
+
+def test_every_abi_call_site_matches_its_signature():
+    """Static check of every _lib.call("gmr_...", ...) in the package: the argument count equals the
+    ctypes signature (a surplus argument would silently shift the stream pointer)."""
+    import ast
+    import glob
+
+    from gmr import _lib
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "generative-multimodal-recommendation_amd", "gmr")
+    bad = []
+    for f in glob.glob(os.path.join(pkg, "*.py")):
+        for node in ast.walk(ast.parse(open(f).read())):
+            if (isinstance(node, ast.Call) and isinstance(node.func, ast.Attribute) and node.func.attr == "call"
+                    and node.args and isinstance(node.args[0], ast.Constant) and str(node.args[0].value).startswith("gmr_")):
+                name = node.args[0].value
+                if any(isinstance(a, ast.Starred) for a in node.args):
+                    continue
+                want = len(_lib.SIGNATURES[name][1])
+                if len(node.args) - 1 != want:
+                    bad.append(f"{os.path.basename(f)}:{node.lineno} {name}: {len(node.args) - 1} args, signature {want}")
+    assert not bad, bad
