@@ -26,6 +26,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "train users/sec + full-rank eval users/sec, DiffMM Amazon-baby, 1/2/4/8 MI355X"
+MODELS = {"diffmm": "DiffMM", "genrecv1": "GenRecV1"}
+DEFAULT_SHAPE = {"diffmm": "baby", "genrecv1": "tiktok"}
+STEP_DESC = {"diffmm": "one DiffMMTrainer epoch (diffusion train + graph rebuild + BPR/contrastive)",
+             "genrecv1": "one GenRecV1Trainer epoch (flip-diffusion train of the transformer denoiser + "
+                         "graph rebuild with interest debiasing + BPR/contrastive)"}
 HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFS = 157.3
 
@@ -38,13 +43,13 @@ def log(*a):
 def setup(args):
     from gmr.configurator import Config
     from gmr.dataloader import EvalDataLoader, TrainDataLoader
-    from gmr.diffmm import DiffMM
     from gmr.quick_start import popularity_groups
     from gmr.synthetic import make_dataset
-    from gmr.trainer import DiffMMTrainer
-    from gmr.utils import init_seed
+    from gmr.utils import get_model, get_trainer, init_seed
 
-    cfg = Config("DiffMM", "baby", {"synthetic": args.shape, "save_recommended_topk": False, "epochs": 1})
+    name = MODELS[args.model]
+    cfg = Config(name, "tiktok" if args.shape == "tiktok" else "baby",
+                 {"synthetic": args.shape, "save_recommended_topk": False, "epochs": 1})
     init_seed(999)
     t0 = time.time()
     ds = make_dataset(cfg, args.shape, seed=0)
@@ -53,28 +58,30 @@ def setup(args):
     cfg["pop_items"], cfg["warm_users"] = pop, warm
     tl = TrainDataLoader(cfg, tr, batch_size=cfg["train_batch_size"], shuffle=True)
     vl = EvalDataLoader(cfg, va, additional_dataset=tr, batch_size=cfg["eval_batch_size"])
-    model = DiffMM(cfg, tl)
-    trainer = DiffMMTrainer(cfg, model)
+    model = get_model(name)(cfg, tl)
+    trainer = get_trainer(name)(cfg, model)
     torch.cuda.synchronize()
     log(f"setup {time.time() - t0:.1f}s: U={ds.user_num} I={ds.item_num} train={len(tr)} valid users={vl.pr_end}")
     return cfg, ds, tr, tl, vl, model, trainer
 
 
-def pmc_traffic():
-    """HBM bytes per launch per kernel class from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, made by scripts/pmc_traffic.sh on the same workload)."""
+def pmc_traffic(model="diffmm"):
+    """HBM bytes per launch per kernel class from the newest committed PMC summary of this workload
+    (profiles/*_pmc_traffic.json for DiffMM, *_pmc_traffic_<model>.json otherwise; made by
+    scripts/pmc_traffic.sh on the same command)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    pat = "*_pmc_traffic.json" if model == "diffmm" else f"*_pmc_traffic_{model}.json"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)))
     if not files:
         return {}, None
     with open(files[-1]) as f:
         return json.load(f), os.path.relpath(files[-1], ROOT)
 
 
-def summarize_probe(p):
+def summarize_probe(p, model="diffmm"):
     """Aggregate HIP-event timings per kernel class into roofline objects."""
     out = {}
-    pmc, pmc_src = pmc_traffic()
+    pmc, pmc_src = pmc_traffic(model)
     for tag, recs in p.items():
         if not recs:
             continue
@@ -177,16 +184,78 @@ def cpu_baseline(model, tl, budget_s=30.0):
                       f"extrapolated to {n_bpr} BPR + {n_dif} diffusion + {n_dif} p_sample batches = {epoch:.1f}s/epoch"}
 
 
+def cpu_baseline_genrec(model, tl, trainer):
+    """Oracle (oracle/genrec_ref.py, torch-CPU fp32) timed on the host: one BPR step, one diffusion
+    batch (training_losses fwd+bwd incl. its p_sample) and one rebuild p_sample batch at the shape,
+    extrapolated to a GenRecV1Trainer epoch (train users/s)."""
+    from oracle import genrec_ref, graph_ref, model_ref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    U, I, B = model.n_users, model.n_items, 2048
+    N = U + I
+    s = model.rec_slab
+    p = {n: s.view(n).cpu().clone().requires_grad_(True) for n in model._pnames}
+    p["user_embedding_weight"] = s.view("E0")[:U].cpu().clone().requires_grad_(True)
+    p["item_id_embedding_weight"] = s.view("E0")[U:].cpu().clone().requires_grad_(True)
+    feats = {"image": model.v_feat.cpu(), "text": model.t_feat.cpu()}
+    rows = np.repeat(np.arange(U), np.diff(tl.uptr_np))
+    rng = np.random.default_rng(0)
+    sp = lambda c, n, m: model_ref.sparse_from_csr(*c, n, m)  # noqa: E731
+    graphs = {"norm_adj": sp(graph_ref.norm_adj_csr(U, I, rows, tl.uitems_np), N, N),
+              "R": sp(genrec_ref.user_item_csr(U, I, rows, tl.uitems_np), U, I)}
+    ui = graph_ref.ui_adj_csr(U, I, np.repeat(np.arange(U), 10), rng.integers(0, I, 10 * U))
+    graphs["ui_img"] = sp(genrec_ref.drop_edges_csr(*ui, rng.random(len(ui[1])) < 0.5), N, N)
+    for key, f in (("ii_img", feats["image"]), ("ii_txt", feats["text"])):
+        graphs[key] = sp(genrec_ref.knn_graph_csr(f.numpy(), 10)[0], I, I)
+    state = {n: (torch.zeros(64), torch.ones(64)) for n in
+             ["image_residual_project_1", "image_modal_project_1", "text_residual_project_1", "text_modal_project_1",
+              "caculate_common_1", "gate_image_modal_1", "gate_text_modal_1"]}
+    users = torch.as_tensor(rng.integers(0, U, B))
+    pos, neg = torch.as_tensor(rng.integers(0, I, B)), torch.as_tensor(rng.integers(0, I, B))
+    t0 = time.time()
+    genrec_ref.calculate_loss(p, feats, graphs, state, users, pos, neg).backward()
+    t_bpr = time.time() - t0
+    den = model.denoise_model_image
+    w = {n: den.v(n).cpu().clone().requires_grad_(True) for n in den.names}
+    w["input_proj_weight"] = den.v("input_proj_weight").cpu().contiguous().clone().requires_grad_(True)
+    x0 = torch.zeros(B, I)
+    for b in range(B):
+        x0[b, tl.uitems_np[tl.uptr_np[b]:tl.uptr_np[b + 1]]] = 1.0
+    g, e = genrec_ref.flip_schedule(x0)
+    ts = rng.integers(0, 5, B)
+    flips = [(torch.rand(B, I) < 0.4).float().numpy() for _ in range(2)]
+    draws = [(torch.rand(B, I) < 0.3).float().numpy() for _ in range(5)]
+    t0 = time.time()
+    total = genrec_ref.training_losses(w, x0, ts, flips[0], p["item_id_embedding_weight"].detach(), torch.randn(I, 64),
+                                       flips[1], draws, g, e, den.L)[0]
+    total.backward()
+    t_dif = time.time() - t0
+    t0 = time.time()
+    with torch.no_grad():
+        genrec_ref.p_sample({k: v.detach() for k, v in w.items()}, x0, g, e, flips[0], draws, den.L)
+    t_ps = time.time() - t0
+    n_bpr = -(-tl.n_inter // B)
+    n_dif = -(-U // B)
+    epoch = t_bpr * n_bpr + (t_dif + t_ps) * n_dif
+    return {"value": round(U / epoch, 2), "unit": "users/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (torch-CPU fp32 restatement of GenRecV1): 1 BPR+InfoNCE step (B=2048, fwd+bwd) = "
+                      f"{t_bpr:.2f}s, 1 diffusion batch (training_losses incl. its p_sample, fwd+bwd) = {t_dif:.2f}s, "
+                      f"1 rebuild p_sample batch = {t_ps:.2f}s; extrapolated to {n_bpr} BPR + {n_dif} diffusion + "
+                      f"{n_dif} rebuild batches = {epoch:.1f}s/epoch"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--shape", default="baby")
+    ap.add_argument("--model", default="diffmm", choices=sorted(MODELS))
+    ap.add_argument("--shape", default=None, help="synthetic shape (default: baby for DiffMM, tiktok for GenRecV1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eval-passes", type=int, default=3)
     ap.add_argument("--no-probe", action="store_true", help="no HIP-event probes (A/B timing only)")
     args = ap.parse_args()
+    args.shape = args.shape or DEFAULT_SHAPE[args.model]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -231,7 +300,7 @@ def main():
         trainer._use_graphs = graphs
         if probed:
             raw = K.probe_end()
-            probe_all = summarize_probe(raw)
+            probe_all = summarize_probe(raw, args.model)
             if os.environ.get("GMR_PROBE_REPORT"):
                 report_shapes(raw)
         log(f"warmup epoch {i}: {time.time() - t0:.3f}s")
@@ -247,7 +316,7 @@ def main():
         trainer._train_epoch(tl, args.warmup + i)
     barrier()
     dt = max_over_ranks(time.time() - t0)
-    live = summarize_probe(K.probe_end()) if not args.no_probe else {}
+    live = summarize_probe(K.probe_end(), args.model) if not args.no_probe else {}
     train_ups = U * args.steps / dt
 
     # full-rank evaluation passes (valid split)
@@ -266,13 +335,13 @@ def main():
             roof["probe_scope"] = ("timed epochs, launches outside the BPR-step HIP graphs" if graphs and dominant in live
                                    else "timed epochs" if dominant in live else "last warmup epoch (eager)")
         line = {
-            "metric": METRIC, "value": round(train_ups, 1), "unit": "users/s", "n_gpus": world,
+            "metric": METRIC if args.model == "diffmm" else
+            "train users/sec + full-rank eval users/sec, GenRecV1 TikTok-shaped (config 5)", "value": round(train_ups, 1), "unit": "users/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 2),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic (Amazon-baby shape, SURVEY.md 8d recipe; random-init weights)",
-            "config": {"workload": f"DiffMM {args.shape}-shaped synthetic: {U} users x {model.n_items} items, "
-                                   f"{tl.n_inter} train interactions; step = one DiffMMTrainer epoch "
-                                   "(diffusion train + graph rebuild + BPR/contrastive)",
+            "data": f"synthetic ({args.shape} shape, SURVEY.md 8d recipe; random-init weights)",
+            "config": {"workload": f"{MODELS[args.model]} {args.shape}-shaped synthetic: {U} users x {model.n_items} "
+                                   f"items, {tl.n_inter} train interactions; step = {STEP_DESC[args.model]}",
                        "global_batch": cfg["train_batch_size"], "eval_batch": cfg["eval_batch_size"],
                        "parallelism": f"dp{world}"},
             "eval_users_per_s": round(eval_ups, 1), "eval_recall@20": res.get("recall@20"),
@@ -280,7 +349,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             try:
-                line["cpu_baseline"] = cpu_baseline(model, tl)
+                line["cpu_baseline"] = (cpu_baseline(model, tl) if args.model == "diffmm"
+                                        else cpu_baseline_genrec(model, tl, trainer))
             except Exception as e:  # noqa: BLE001
                 line["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(line), flush=True)

@@ -243,6 +243,33 @@ __global__ void __launch_bounds__(1024) colsum_kernel(int64_t rows, int64_t cols
   }
 }
 
+// few column blocks (cols <= 64 * 32): rows split over blockIdx.y into fixed-order partials, then
+// a second pass adds the partials in split order (deterministic)
+constexpr int kColSplits = 32;
+__global__ void __launch_bounds__(256) colsum_split_kernel(int64_t rows, int64_t cols, const float* __restrict__ x,
+                                                           int64_t ld, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t rc = (rows + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = (int64_t)blockIdx.y * rc, r1 = r0 + rc < rows ? r0 + rc : rows;
+  float s = 0.f;
+  if (c < cols)
+    for (int64_t r = r0 + w; r < r1; r += 4) s += x[r * ld + c];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < cols) part[(int64_t)blockIdx.y * cols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+__global__ void colsum_split_fin_kernel(int64_t cols, int S, const float* __restrict__ part, float* __restrict__ out,
+                                        int accumulate) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int j = 0; j < S; ++j) s += part[(int64_t)j * cols + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
 // generic fallback (many groups): one group per blockIdx.y
 __global__ void __launch_bounds__(256) colsum_grouped_kernel(int64_t rows, int64_t cols, const float* __restrict__ x,
                                                              int64_t ld, const int* __restrict__ group,
@@ -584,6 +611,22 @@ extern "C" int gmr_diff_time_bwd(int32_t T, int32_t E, int32_t H, const float* S
   GMR_ARG((size_t)T * E * sizeof(float) <= 60000, "T * E too large for the LDS staging");
   hipLaunchKernelGGL(time_bwd_e_kernel, dim3(1), dim3(1024), sizeof(float) * (size_t)T * E, st, T, E, H, S, W1, ld_w1,
                      col_off, temb, d_emb_W, d_emb_b, accumulate);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int64_t gmr_colsum_split_floats(int64_t cols) { return (int64_t)kColSplits * cols; }
+
+extern "C" int gmr_colsum_split_f32(int64_t rows, int64_t cols, const float* x, int64_t ld, float* out,
+                                   int32_t accumulate, float* workspace, int64_t workspace_floats, void* stream) {
+  GMR_ARG(x && out && workspace && rows > 0 && cols > 0, "bad args");
+  GMR_ARG(workspace_floats >= (int64_t)kColSplits * cols, "workspace too small (gmr_colsum_split_floats)");
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned gx = (unsigned)((cols + 63) / 64);
+  hipLaunchKernelGGL(colsum_split_kernel, dim3(gx, kColSplits), dim3(256), 0, st, rows, cols, x, ld, workspace);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(colsum_split_fin_kernel, dim3(gmr::grid_for(cols, 256)), dim3(256), 0, st, cols, kColSplits,
+                     workspace, out, (int)accumulate);
   GMR_LAUNCHED();
   return GMR_OK;
 }

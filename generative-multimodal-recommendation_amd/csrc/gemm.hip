@@ -392,9 +392,13 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
     // measured on MI355X (scripts/gemm_bench.py): 256^2 tiles win the long-K products of the
     // denoiser (M >= 2048, N >= 1000, K >= 4096; one 16-wave block per CU), 128^2 the wide
     // K ~ 1000 ones, 64^2 (with split-K) the skinny N = 64 / K = 64 products and the TN updates.
+    // The 2048 x 512 x 512 transformer products (GenRecV1) run best on 64^2 tiles without split-K,
+    // their K = 6710 input projection on 128^2, the K = 256 output projection on 256^2.
     const bool tn = trans_a && !trans_b;
     if (!tn && M >= 2048 && N >= 1000 && K >= 4096) tile = 256;
+    else if (!tn && M >= 2048 && N >= 4096 && K >= 256 && K <= 512) tile = 256;
     else if (!tn && M * N >= (int64_t)8 << 20 && K >= 512) tile = 128;
+    else if (!tn && M * N >= (int64_t)1 << 20 && K >= 4096) tile = 128;
     else tile = 64;
   }
   const int bm = tile == 256128 ? 256 : tile == 128256 ? 128 : tile;
@@ -404,7 +408,7 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   int splits = split_k;
   if (splits <= 0) {  // auto: aim for >= 512 workgroups on 256 CUs
     splits = 1;
-    while (tm * tn * splits < 512 && K / (splits * 2) >= 256 && splits < 16) splits *= 2;
+    while (tm * tn * splits < 512 && K / (splits * 2) >= 512 && splits < 16) splits *= 2;
   }
   int64_t kps = (K + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;

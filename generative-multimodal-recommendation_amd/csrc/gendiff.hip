@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(int Dsmall, int64_t rows, c
 
 // dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy w (dy through GELU first);
 // dw/db column partials per block (rows blockIdx.x*RB .. ) -> part[blk][2*D]
-constexpr int kLnRowsPerBlock = 64;
+constexpr int kLnRowsPerBlock = 8;
 template <int PER>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(int Dsmall, int64_t rows, const float* __restrict__ s, int64_t lds,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -276,12 +276,21 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(int Dsmall, int64_t rows, c
   }
 }
 
-__global__ void ln_param_reduce_kernel(int P, int D, const float* __restrict__ part, float* __restrict__ dw,
-                                       float* __restrict__ db, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * D) return;
+// column c of the P x 2D partials: 16 part groups per column (fixed order), 64 columns per block
+__global__ void __launch_bounds__(1024) ln_param_reduce_kernel(int P, int D, const float* __restrict__ part,
+                                                               float* __restrict__ dw, float* __restrict__ db,
+                                                               int accumulate) {
+  __shared__ double red[16][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   double s = 0.0;
-  for (int p = 0; p < P; ++p) s += part[(int64_t)p * 2 * D + c];
+  if (c < 2 * D)
+    for (int p = g; p < P; p += 16) s += part[(int64_t)p * 2 * D + c];
+  red[g][cl] = s;
+  __syncthreads();
+  if (g != 0 || c >= 2 * D) return;
+  s = 0.0;
+  for (int j = 0; j < 16; ++j) s += red[j][cl];
   float* o = c < D ? dw + c : db + (c - D);
   *o = (float)s + (accumulate ? *o : 0.f);
 }
@@ -459,7 +468,7 @@ extern "C" int gmr_layernorm_bwd(int64_t rows, int32_t D, const float* s, int64_
   }
 #undef GMR_LNB
   GMR_LAUNCHED();
-  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(gmr::grid_for(2 * D, 256)), dim3(256), 0, st, P, D, parts, dw, db,
+  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(gmr::grid_for(2 * D, 64)), dim3(1024), 0, st, P, D, parts, dw, db,
                      (int)accumulate_params);
   GMR_LAUNCHED();
   return GMR_OK;

@@ -134,28 +134,65 @@ __device__ __forceinline__ bool edge_kept(int64_t e, const uint8_t* keep, float 
   return floorf(u + keep_rate) >= 1.f;
 }
 
-__global__ void drop_count_kernel(int n_rows, const int* __restrict__ rowptr, const uint8_t* __restrict__ keep,
-                                  float keep_rate, uint64_t seed, uint64_t step, int* __restrict__ cnt) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n_rows) return;
-  int c = 0;
-  for (int e = rowptr[r]; e < rowptr[r + 1]; ++e) c += edge_kept(e, keep, keep_rate, seed, step) ? 1 : 0;
-  cnt[r] = c;
+// position of column c in row r (columns ascending; present by symmetry)
+__device__ __forceinline__ int find_in_row(const int* __restrict__ rowptr, const int* __restrict__ col, int r, int c) {
+  int lo = rowptr[r], hi = rowptr[r + 1] - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (col[mid] < c) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
 }
 
-__global__ void drop_write_kernel(int n_rows, const int* __restrict__ rowptr, const int* __restrict__ col,
-                                  const float* __restrict__ val, const uint8_t* __restrict__ keep, float keep_rate,
-                                  uint64_t seed, uint64_t step, const int* __restrict__ orp, int* __restrict__ ocol,
-                                  float* __restrict__ oval) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+// keep flag of entry e = (r, c); transposed: the flag of (c, r) of a structurally symmetric matrix,
+// so the result is (A with its entries dropped)^T built directly from A
+__device__ __forceinline__ bool kept_entry(int r, int e, const int* __restrict__ rowptr, const int* __restrict__ col,
+                                           int transposed, const uint8_t* keep, float keep_rate, uint64_t seed,
+                                           uint64_t step) {
+  const int src = transposed ? find_in_row(rowptr, col, col[e], r) : e;
+  return edge_kept(src, keep, keep_rate, seed, step);
+}
+
+// one wave per row: ballot of the kept entries
+__global__ void __launch_bounds__(256) drop_count_kernel(int n_rows, const int* __restrict__ rowptr,
+                                                         const int* __restrict__ col, int transposed,
+                                                         const uint8_t* __restrict__ keep, float keep_rate,
+                                                         uint64_t seed, uint64_t step, int* __restrict__ cnt) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= n_rows) return;
+  const int lane = threadIdx.x & 63;
+  int c = 0;
+  for (int e0 = rowptr[r]; e0 < rowptr[r + 1]; e0 += 64) {
+    const int e = e0 + lane;
+    const bool k = e < rowptr[r + 1] && kept_entry(r, e, rowptr, col, transposed, keep, keep_rate, seed, step);
+    c += __popcll(__ballot(k));
+  }
+  if (lane == 0) cnt[r] = c;
+}
+
+__global__ void __launch_bounds__(256) drop_write_kernel(int n_rows, const int* __restrict__ rowptr,
+                                                         const int* __restrict__ col, const float* __restrict__ val,
+                                                         int transposed, const uint8_t* __restrict__ keep,
+                                                         float keep_rate, uint64_t seed, uint64_t step,
+                                                         const int* __restrict__ orp, int* __restrict__ ocol,
+                                                         float* __restrict__ oval) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n_rows) return;
+  const int lane = threadIdx.x & 63;
   int o = orp[r];
-  for (int e = rowptr[r]; e < rowptr[r + 1]; ++e)
-    if (edge_kept(e, keep, keep_rate, seed, step)) {
-      ocol[o] = col[e];
-      oval[o] = val[e] / keep_rate;
-      ++o;
+  for (int e0 = rowptr[r]; e0 < rowptr[r + 1]; e0 += 64) {
+    const int e = e0 + lane;
+    const bool k = e < rowptr[r + 1] && kept_entry(r, e, rowptr, col, transposed, keep, keep_rate, seed, step);
+    const unsigned long long m = __ballot(k);
+    if (k) {
+      const int pos = o + __popcll(m & ((1ull << lane) - 1ull));
+      const int src = transposed ? find_in_row(rowptr, col, col[e], r) : e;
+      ocol[pos] = col[e];
+      oval[pos] = val[src] / keep_rate;
     }
+    o += __popcll(m);
+  }
 }
 
 // ----------------------------------------------------------------- kNN graph ('sym')
@@ -214,9 +251,26 @@ __device__ __forceinline__ int cand_type(const float* x0, const float* xs, int64
   return -1;
 }
 
+// candidate keys: UINT64_MAX unless position j (row j / k, pick j % k) flipped with the given type
+__global__ void debias_keys_kernel(int B, int k, const int* __restrict__ topi, int64_t ldt, const float* __restrict__ x0,
+                                   const float* __restrict__ xs, int64_t ld, uint64_t seed, uint64_t step,
+                                   unsigned long long* __restrict__ keys) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B * k) return;
+  const int b = j / k, i = topi[(int64_t)b * ldt + j % k];
+  const int ty = cand_type(x0, xs, ld, b, i);
+  for (int type = 0; type < 2; ++type) {
+    unsigned long long key = ~0ull;
+    if (ty == type) {
+      const uint4 r = gmr::Philox::gen(seed, step * 2 + type, (uint64_t)j);
+      key = ((unsigned long long)r.x << 32) | (unsigned)j;
+    }
+    keys[(int64_t)type * B * k + j] = key;
+  }
+}
+
 __global__ void __launch_bounds__(kSel) debias_select_kernel(int B, int k, const int* __restrict__ topi, int64_t ldt,
-                                                             const float* __restrict__ x0, const float* __restrict__ xs,
-                                                             int64_t ld, float ratio, uint64_t seed, uint64_t step,
+                                                             const unsigned long long* __restrict__ keys, float ratio,
                                                              int* __restrict__ picks, int max_picks,
                                                              int* __restrict__ n_picks) {
   __shared__ int hist[256];
@@ -227,15 +281,16 @@ __global__ void __launch_bounds__(kSel) debias_select_kernel(int B, int k, const
   const int t = threadIdx.x;
   const int n = B * k;
   for (int type = 0; type < 2; ++type) {
+    const unsigned long long* kk = keys + (int64_t)type * n;
     if (t == 0) s_cnt = 0;
     __syncthreads();
     int c = 0;
-    for (int j = t; j < n; j += kSel) c += cand_type(x0, xs, ld, j / k, topi[(int64_t)(j / k) * ldt + j % k]) == type;
+    for (int j = t; j < n; j += kSel) c += kk[j] != ~0ull;
     atomicAdd(&s_cnt, c);
     __syncthreads();
     const int total = s_cnt;
     const int need = (int)((float)total * ratio);
-    // radix select of the need-th smallest key among this type's candidates
+    // radix select of the need-th smallest key among this type's candidates (keys are distinct)
     unsigned long long prefix = 0ull;
     int remaining = need;
     if (need > 0) {
@@ -244,11 +299,8 @@ __global__ void __launch_bounds__(kSel) debias_select_kernel(int B, int k, const
         __syncthreads();
         const unsigned long long hi_mask = pass == 7 ? 0ull : (~0ull << (8 * (pass + 1)));
         for (int j = t; j < n; j += kSel) {
-          const int b = j / k, i = topi[(int64_t)b * ldt + j % k];
-          if (cand_type(x0, xs, ld, b, i) != type) continue;
-          const uint4 r = gmr::Philox::gen(seed, step * 2 + type, (uint64_t)j);
-          const unsigned long long key = ((unsigned long long)r.x << 32) | (unsigned)j;
-          if ((key & hi_mask) != prefix) continue;
+          const unsigned long long key = kk[j];
+          if (key == ~0ull || (key & hi_mask) != prefix) continue;
           atomicAdd(&hist[(key >> (8 * pass)) & 255], 1);
         }
         __syncthreads();
@@ -267,20 +319,16 @@ __global__ void __launch_bounds__(kSel) debias_select_kernel(int B, int k, const
         __syncthreads();
       }
     }
-    // emit every candidate with key <= the need-th smallest key (keys are distinct)
     if (t == 0) s_out = 0;
     __syncthreads();
     if (need > 0)
       for (int j = t; j < n; j += kSel) {
-        const int b = j / k, i = topi[(int64_t)b * ldt + j % k];
-        if (cand_type(x0, xs, ld, b, i) != type) continue;
-        const uint4 r = gmr::Philox::gen(seed, step * 2 + type, (uint64_t)j);
-        const unsigned long long key = ((unsigned long long)r.x << 32) | (unsigned)j;
-        if (key <= prefix) {
+        const unsigned long long key = kk[j];
+        if (key != ~0ull && key <= prefix) {
           const int o = atomicAdd(&s_out, 1);
           if (o < max_picks) {
-            picks[(type * max_picks + o) * 2] = b;
-            picks[(type * max_picks + o) * 2 + 1] = i;
+            picks[(type * max_picks + o) * 2] = j / k;
+            picks[(type * max_picks + o) * 2 + 1] = topi[(int64_t)(j / k) * ldt + j % k];
           }
         }
       }
@@ -524,13 +572,14 @@ extern "C" int gmr_csr_transpose(int64_t n_rows, int64_t n_cols, int64_t nnz, co
   return GMR_OK;
 }
 
-extern "C" int gmr_csr_drop_count(int64_t n_rows, const int32_t* rowptr, const uint8_t* keep, float keep_rate,
-                                  uint64_t seed, uint64_t step, int32_t* workspace, int32_t* out_rowptr, void* stream) {
-  GMR_ARG(rowptr && workspace && out_rowptr && n_rows > 0, "bad args");
+extern "C" int gmr_csr_drop_count(int64_t n_rows, const int32_t* rowptr, const int32_t* col, int32_t transposed,
+                                  const uint8_t* keep, float keep_rate, uint64_t seed, uint64_t step,
+                                  int32_t* workspace, int32_t* out_rowptr, void* stream) {
+  GMR_ARG(rowptr && col && workspace && out_rowptr && n_rows > 0, "bad args");
   GMR_ARG(keep_rate > 0.f && keep_rate <= 1.f, "keep_rate in (0, 1]");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(drop_count_kernel, dim3(gmr::grid_for(n_rows, 256)), dim3(256), 0, st, (int)n_rows, rowptr, keep,
-                     keep_rate, seed, step, workspace);
+  hipLaunchKernelGGL(drop_count_kernel, dim3(gmr::grid_for(n_rows, 4)), dim3(256), 0, st, (int)n_rows, rowptr, col,
+                     (int)transposed, keep, keep_rate, seed, step, workspace);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, n_rows, workspace, out_rowptr);
   GMR_LAUNCHED();
@@ -538,11 +587,13 @@ extern "C" int gmr_csr_drop_count(int64_t n_rows, const int32_t* rowptr, const u
 }
 
 extern "C" int gmr_csr_drop_write(int64_t n_rows, const int32_t* rowptr, const int32_t* col, const float* val,
-                                  const uint8_t* keep, float keep_rate, uint64_t seed, uint64_t step,
-                                  const int32_t* out_rowptr, int32_t* out_col, float* out_val, void* stream) {
+                                  int32_t transposed, const uint8_t* keep, float keep_rate, uint64_t seed,
+                                  uint64_t step, const int32_t* out_rowptr, int32_t* out_col, float* out_val,
+                                  void* stream) {
   GMR_ARG(rowptr && col && val && out_rowptr && out_col && out_val && n_rows > 0, "bad args");
-  hipLaunchKernelGGL(drop_write_kernel, dim3(gmr::grid_for(n_rows, 256)), dim3(256), 0, (hipStream_t)stream,
-                     (int)n_rows, rowptr, col, val, keep, keep_rate, seed, step, out_rowptr, out_col, out_val);
+  hipLaunchKernelGGL(drop_write_kernel, dim3(gmr::grid_for(n_rows, 4)), dim3(256), 0, (hipStream_t)stream,
+                     (int)n_rows, rowptr, col, val, (int)transposed, keep, keep_rate, seed, step, out_rowptr, out_col,
+                     out_val);
   GMR_LAUNCHED();
   return GMR_OK;
 }
@@ -572,10 +623,15 @@ extern "C" int gmr_gen_mask(int32_t B, int32_t I, int32_t k, const int32_t* topi
 
 extern "C" int gmr_debias_select(int32_t B, int32_t k, const int32_t* topi, int64_t ldt, const float* x0,
                                  const float* xs, int64_t ld, float ratio, uint64_t seed, uint64_t step,
-                                 int32_t* picks, int32_t max_picks, int32_t* n_picks, void* stream) {
-  GMR_ARG(topi && x0 && xs && picks && n_picks && B > 0 && k > 0 && max_picks > 0, "bad args");
-  hipLaunchKernelGGL(debias_select_kernel, dim3(1), dim3(kSel), 0, (hipStream_t)stream, B, k, topi, ldt, x0, xs, ld,
-                     ratio, seed, step, picks, max_picks, n_picks);
+                                 uint64_t* keys_ws, int32_t* picks, int32_t max_picks, int32_t* n_picks,
+                                 void* stream) {
+  GMR_ARG(topi && x0 && xs && keys_ws && picks && n_picks && B > 0 && k > 0 && max_picks > 0, "bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(debias_keys_kernel, dim3(gmr::grid_for((int64_t)B * k, 256)), dim3(256), 0, st, B, k, topi, ldt,
+                     x0, xs, ld, seed, step, (unsigned long long*)keys_ws);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(debias_select_kernel, dim3(1), dim3(kSel), 0, st, B, k, topi, ldt,
+                     (const unsigned long long*)keys_ws, ratio, picks, max_picks, n_picks);
   GMR_LAUNCHED();
   return GMR_OK;
 }

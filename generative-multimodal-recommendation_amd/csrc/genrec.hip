@@ -76,20 +76,34 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(int64_t rows, const float
   }
 }
 
-__global__ void bn_finalize_kernel(int P, const double* __restrict__ part, int64_t rows, float eps, float momentum,
-                                   int train, float* __restrict__ run_mean, float* __restrict__ run_var,
-                                   float* __restrict__ mean_out, float* __restrict__ invstd_out) {
-  const int c = threadIdx.x;
-  if (c >= 64) return;
+// 1024 threads: column c = t & 63 summed by 16 groups (parts g, g+16, ...) then the 16 group sums in
+// order — a fixed reduction order with a 16-long dependent chain instead of P
+__global__ void __launch_bounds__(1024) bn_finalize_kernel(int P, const double* __restrict__ part, int64_t rows,
+                                                           float eps, float momentum, int train,
+                                                           float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                           float* __restrict__ mean_out, float* __restrict__ invstd_out) {
+  __shared__ double rs[16][64], rq[16][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
   if (!train) {
-    mean_out[c] = run_mean[c];
-    invstd_out[c] = 1.f / sqrtf(run_var[c] + eps);
+    if (g == 0) {
+      mean_out[c] = run_mean[c];
+      invstd_out[c] = 1.f / sqrtf(run_var[c] + eps);
+    }
     return;
   }
   double s = 0.0, q = 0.0;
-  for (int p = 0; p < P; ++p) {
+  for (int p = g; p < P; p += 16) {
     s += part[(int64_t)p * 128 + c];
     q += part[(int64_t)p * 128 + 64 + c];
+  }
+  rs[g][c] = s;
+  rq[g][c] = q;
+  __syncthreads();
+  if (g != 0) return;
+  s = q = 0.0;
+  for (int j = 0; j < 16; ++j) {
+    s += rs[j][c];
+    q += rq[j][c];
   }
   const double n = (double)rows;
   const double mean = s / n;
@@ -216,16 +230,29 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(int64_t rows, BnBwdI
 }
 
 // dw += sum dv*xhat; db += sum dv; dvec += sum da*a; sums = [mean dv | mean dv*xhat]
-__global__ void bn_bwd_finalize_kernel(int P, const double* __restrict__ part, int64_t rows, float* __restrict__ dw,
-                                       float* __restrict__ db, float* __restrict__ dvec, float* __restrict__ sums,
-                                       int accumulate) {
-  const int c = threadIdx.x;
-  if (c >= 64) return;
+// (1024 threads, 16 part groups per column, fixed order)
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(int P, const double* __restrict__ part, int64_t rows,
+                                                               float* __restrict__ dw, float* __restrict__ db,
+                                                               float* __restrict__ dvec, float* __restrict__ sums,
+                                                               int accumulate) {
+  __shared__ double r0[16][64], r1[16][64], r2[16][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  for (int p = 0; p < P; ++p) {
+  for (int p = g; p < P; p += 16) {
     s0 += part[(int64_t)p * 192 + c];
     s1 += part[(int64_t)p * 192 + 64 + c];
     s2 += part[(int64_t)p * 192 + 128 + c];
+  }
+  r0[g][c] = s0;
+  r1[g][c] = s1;
+  r2[g][c] = s2;
+  __syncthreads();
+  if (g != 0) return;
+  s0 = s1 = s2 = 0.0;
+  for (int j = 0; j < 16; ++j) {
+    s0 += r0[j][c];
+    s1 += r1[j][c];
+    s2 += r2[j][c];
   }
   if (dw) dw[c] = (float)s1 + (accumulate ? dw[c] : 0.f);
   if (db) db[c] = (float)s0 + (accumulate ? db[c] : 0.f);
@@ -311,16 +338,31 @@ __global__ void __launch_bounds__(256) content_bwd_part_kernel(int64_t n, const 
         (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]);
 }
 
-// softmax backward onto the two weight parameters (accumulated into their grads)
-__global__ void content_bwd_weights_kernel(int P, const double* __restrict__ part, const float* __restrict__ ow,
-                                           const float* __restrict__ gw, float* __restrict__ dow,
-                                           float* __restrict__ dgw) {
-  if (threadIdx.x != 0) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int p = 0; p < P; ++p) {
-    s1 += part[2 * p];
-    s2 += part[2 * p + 1];
+// fixed-order block reduction of P doubles (stride st, offset o): thread t sums t, t+256, ...; tree in LDS
+__device__ __forceinline__ double block_sum_parts(int P, const double* __restrict__ part, int st, int o,
+                                                  double* red) {
+  double s = 0.0;
+  for (int p = threadIdx.x; p < P; p += 256) s += part[(int64_t)p * st + o];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
   }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// softmax backward onto the two weight parameters (accumulated into their grads)
+__global__ void __launch_bounds__(256) content_bwd_weights_kernel(int P, const double* __restrict__ part,
+                                                                  const float* __restrict__ ow,
+                                                                  const float* __restrict__ gw,
+                                                                  float* __restrict__ dow, float* __restrict__ dgw) {
+  __shared__ double red[256];
+  const double s1 = block_sum_parts(P, part, 2, 0, red);
+  const double s2 = block_sum_parts(P, part, 2, 1, red);
+  if (threadIdx.x != 0) return;
   float w0, w1;
   softmax2v(ow, gw, w0, w1);
   const double dot = w0 * s1 + w1 * s2;
@@ -446,12 +488,11 @@ __global__ void __launch_bounds__(256) dot_part_kernel(int64_t rows, const float
   if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ void sum_parts_kernel(int P, const double* __restrict__ part, float scale, float* __restrict__ out,
-                                 int accumulate) {
-  if (threadIdx.x != 0) return;
-  double s = 0.0;
-  for (int p = 0; p < P; ++p) s += part[p];
-  out[0] = (float)(s * scale) + (accumulate ? out[0] : 0.f);
+__global__ void __launch_bounds__(256) sum_parts_kernel(int P, const double* __restrict__ part, float scale,
+                                                        float* __restrict__ out, int accumulate) {
+  __shared__ double red[256];
+  const double s = block_sum_parts(P, part, 1, 0, red);
+  if (threadIdx.x == 0) out[0] = (float)(s * scale) + (accumulate ? out[0] : 0.f);
 }
 
 // ----------------------------------------------------------------- losses
@@ -559,7 +600,7 @@ extern "C" int gmr_bn_fwd_f32(int64_t rows, const float* z, int64_t ldz, int32_t
     hipLaunchKernelGGL(bn_stats_kernel, dim3(P), dim3(256), 0, st, rows, z, ldz, parts);
     GMR_LAUNCHED();
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(64), 0, st, P, parts, rows, eps, momentum, (int)train, run_mean,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(1024), 0, st, P, parts, rows, eps, momentum, (int)train, run_mean,
                      run_var, mean, invstd);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(bn_apply_kernel, rows16(rows), dim3(256), 0, st, rows, z, ldz, mean, invstd, w, b, (int)act, slope,
@@ -583,7 +624,7 @@ extern "C" int gmr_bn_bwd_f32(int64_t rows, const float* z, int64_t ldz, const f
   const int P = parts_for(rows);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(P), dim3(256), 0, st, rows, p, parts);
   GMR_LAUNCHED();
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(64), 0, st, P, parts, rows, dw, db, dv, sums,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(1024), 0, st, P, parts, rows, dw, db, dv, sums,
                      (int)accumulate_params);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(bn_bwd_apply_kernel, rows16(rows), dim3(256), 0, st, rows, p, sums, dz, lddz, (int)accumulate_dz);
@@ -611,7 +652,7 @@ extern "C" int gmr_gr_content_bwd(int64_t n, const float* E, const float* A1, co
   const int P = gmr::grid_for(n * 16, 256, 1024);
   hipLaunchKernelGGL(content_bwd_part_kernel, dim3(P), dim3(256), 0, st, n, E, A1, A2, dC, parts);
   GMR_LAUNCHED();
-  hipLaunchKernelGGL(content_bwd_weights_kernel, dim3(1), dim3(64), 0, st, P, parts, ow, gw, dow, dgw);
+  hipLaunchKernelGGL(content_bwd_weights_kernel, dim3(1), dim3(256), 0, st, P, parts, ow, gw, dow, dgw);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(content_bwd_combine_kernel, rows16(n), dim3(256), 0, st, n, dC, T1, T2, ow, gw, E, reg2, dE);
   GMR_LAUNCHED();
@@ -657,7 +698,7 @@ extern "C" int gmr_dot64_f32(int64_t rows, const float* a, int64_t lda, const fl
   const int P = gmr::grid_for(rows * 16, 256, 1024);
   hipLaunchKernelGGL(dot_part_kernel, dim3(P), dim3(256), 0, st, rows, a, lda, b, ldb, parts);
   GMR_LAUNCHED();
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, st, P, parts, scale, out, (int)accumulate);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, st, P, parts, scale, out, (int)accumulate);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -10,6 +10,8 @@
 // Columns are sorted inside each row, so the CSR equals the reference's coalesced COO.
 // Item rows are filled through atomically claimed slots, then each row is put in user order
 // by its own workgroup (rank count / LDS bitmap), so the build is deterministic.
+#include <algorithm>
+
 #include "gmr_common.h"
 
 namespace {
@@ -57,6 +59,58 @@ __global__ void user_rows_kernel(int U, const int* __restrict__ uptr, const int*
     const int it = uitems[e];
     col[o++] = U + it;
     col[rowptr[U + it] + atomicAdd(&fill[it], 1)] = u;
+  }
+}
+
+// LDS-privatised variants for I <= kLdsItems: each block counts its users' items in LDS and
+// touches every global counter once (the rebuilt graphs send most users to a few popular items,
+// where one global atomic per entry serialises on the same address).
+constexpr int kLdsItems = 8192;
+constexpr int kPrivBlocks = 64;
+__global__ void __launch_bounds__(1024) count_items_priv_kernel(int U, int I, const int* __restrict__ uptr,
+                                                                const int* __restrict__ uitems, int* __restrict__ cnt) {
+  __shared__ int hist[kLdsItems];
+  const int t = threadIdx.x;
+  for (int i = t; i < I; i += 1024) hist[i] = 0;
+  __syncthreads();
+  const int uc = (U + gridDim.x - 1) / gridDim.x;
+  const int u0 = blockIdx.x * uc, u1 = min(U, u0 + uc);
+  const int e0 = u0 < U ? uptr[u0] : 0, e1 = u0 < U ? uptr[u1] : 0;
+  for (int e = e0 + t; e < e1; e += 1024) atomicAdd(&hist[uitems[e]], 1);
+  __syncthreads();
+  for (int i = t; i < I; i += 1024)
+    if (hist[i]) atomicAdd(&cnt[i], hist[i]);
+}
+
+__global__ void __launch_bounds__(1024) user_rows_priv_kernel(int U, int I, const int* __restrict__ uptr,
+                                                              const int* __restrict__ uitems, int sl,
+                                                              const int* __restrict__ rowptr, int* __restrict__ col,
+                                                              int* __restrict__ fill) {
+  __shared__ int base[kLdsItems];
+  __shared__ int loc[kLdsItems];
+  const int t = threadIdx.x;
+  for (int i = t; i < I; i += 1024) {
+    base[i] = 0;
+    loc[i] = 0;
+  }
+  __syncthreads();
+  const int uc = (U + gridDim.x - 1) / gridDim.x;
+  const int u0 = blockIdx.x * uc, u1 = min(U, u0 + uc);
+  const int e0 = u0 < U ? uptr[u0] : 0, e1 = u0 < U ? uptr[u1] : 0;
+  for (int e = e0 + t; e < e1; e += 1024) atomicAdd(&base[uitems[e]], 1);
+  __syncthreads();
+  for (int i = t; i < I; i += 1024)
+    if (base[i]) base[i] = atomicAdd(&fill[i], base[i]);
+  __syncthreads();
+  // user rows (in place) + item-row slots claimed from the block's reserved ranges
+  for (int u = u0 + t; u < u1; u += 1024) {
+    int o = rowptr[u];
+    if (sl) col[o++] = u;
+    for (int e = uptr[u]; e < uptr[u + 1]; ++e) {
+      const int it = uitems[e];
+      col[o++] = U + it;
+      col[rowptr[U + it] + base[it] + atomicAdd(&loc[it], 1)] = u;
+    }
   }
 }
 
@@ -118,19 +172,21 @@ __global__ void __launch_bounds__(kSortThreads) item_sort_kernel(int U, const in
   }
 }
 
-// one wave per row: values in fp64, rounded once to fp32
-__global__ void values_kernel(int N, const int* __restrict__ rowptr, const int* __restrict__ col, double eps,
-                              float* __restrict__ val) {
+// d[r] = (deg_r + eps)^-1/2 in fp64, once per node
+__global__ void dis_kernel(int N, const int* __restrict__ rowptr, double eps, double* __restrict__ dis) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < N) dis[r] = pow((double)(rowptr[r + 1] - rowptr[r]) + eps, -0.5);
+}
+
+// one wave per row: values d_r * d_c in fp64, rounded once to fp32
+__global__ void values_kernel(int N, const int* __restrict__ rowptr, const int* __restrict__ col,
+                              const double* __restrict__ dis, float* __restrict__ val) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= N) return;
   const int lane = threadIdx.x & 63;
   const int beg = rowptr[r], end = rowptr[r + 1];
-  const double dr = pow((double)(end - beg) + eps, -0.5);
-  for (int e = beg + lane; e < end; e += 64) {
-    const int c = col[e];
-    const double dc = pow((double)(rowptr[c + 1] - rowptr[c]) + eps, -0.5);
-    val[e] = (float)(dr * dc);
-  }
+  const double dr = dis[r];
+  for (int e = beg + lane; e < end; e += 64) val[e] = (float)(dr * dis[col[e]]);
 }
 
 // sort the k items of each user (insertion sort, k <= 64) and write uptr = u*k
@@ -159,7 +215,9 @@ extern "C" int64_t gmr_bipartite_nnz(int64_t n_users, int64_t n_items, int64_t n
   return 2 * n_user_items + (self_loops ? n_users + n_items : 0);
 }
 
-extern "C" int64_t gmr_bipartite_workspace_ints(int64_t n_users, int64_t n_items) { return 2 * n_items; }
+extern "C" int64_t gmr_bipartite_workspace_ints(int64_t n_users, int64_t n_items) {
+  return 2 * n_items + 2 * (n_users + n_items) + 2;  // counters | fp64 d (8-byte aligned)
+}
 
 extern "C" int gmr_bipartite_symnorm_build(int64_t n_users, int64_t n_items, const int32_t* user_ptr,
                                            const int32_t* user_items, int64_t n_user_items, int32_t self_loops,
@@ -175,15 +233,24 @@ extern "C" int gmr_bipartite_symnorm_build(int64_t n_users, int64_t n_items, con
   int* cnt = workspace;
   hipError_t e = hipMemsetAsync(workspace, 0, sizeof(int) * 2 * (size_t)I, st);
   if (e != hipSuccess) return gmr::hip_status(__func__, e);
+  const bool priv = I <= kLdsItems;
+  const int pblocks = (int)std::min<int64_t>(kPrivBlocks, std::max<int64_t>(1, n_user_items / 2048));
   if (n_user_items > 0) {
-    hipLaunchKernelGGL(count_items_kernel, dim3(gmr::grid_for(n_user_items, 256)), dim3(256), 0, st, n_user_items,
-                       user_items, cnt);
+    if (priv)
+      hipLaunchKernelGGL(count_items_priv_kernel, dim3(pblocks), dim3(1024), 0, st, U, I, user_ptr, user_items, cnt);
+    else
+      hipLaunchKernelGGL(count_items_kernel, dim3(gmr::grid_for(n_user_items, 256)), dim3(256), 0, st, n_user_items,
+                         user_items, cnt);
     GMR_LAUNCHED();
   }
   hipLaunchKernelGGL(rowptr_kernel, dim3(1), dim3(1024), 0, st, U, I, user_ptr, cnt, sl, rowptr);
   GMR_LAUNCHED();
-  hipLaunchKernelGGL(user_rows_kernel, dim3(gmr::grid_for(U, 256)), dim3(256), 0, st, U, user_ptr, user_items, sl, rowptr,
-                     col, workspace + I);
+  if (priv)
+    hipLaunchKernelGGL(user_rows_priv_kernel, dim3(pblocks), dim3(1024), 0, st, U, I, user_ptr, user_items, sl, rowptr,
+                       col, workspace + I);
+  else
+    hipLaunchKernelGGL(user_rows_kernel, dim3(gmr::grid_for(U, 256)), dim3(256), 0, st, U, user_ptr, user_items, sl,
+                       rowptr, col, workspace + I);
   GMR_LAUNCHED();
   const size_t dyn = sizeof(uint32_t) * (size_t)((U + 31) / 32);
   if (dyn > 65536) {
@@ -192,7 +259,10 @@ extern "C" int gmr_bipartite_symnorm_build(int64_t n_users, int64_t n_items, con
   }
   hipLaunchKernelGGL(item_sort_kernel, dim3(I), dim3(kSortThreads), dyn, st, U, rowptr, col, sl);
   GMR_LAUNCHED();
-  hipLaunchKernelGGL(values_kernel, dim3(gmr::grid_for(N, 4)), dim3(256), 0, st, N, rowptr, col, deg_eps, val);
+  double* dis = reinterpret_cast<double*>(workspace + 2 * (int64_t)I + ((2 * (int64_t)I) & 1));
+  hipLaunchKernelGGL(dis_kernel, dim3(gmr::grid_for(N, 256)), dim3(256), 0, st, N, rowptr, deg_eps, dis);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(values_kernel, dim3(gmr::grid_for(N, 4)), dim3(256), 0, st, N, rowptr, col, dis, val);
   GMR_LAUNCHED();
   return GMR_OK;
 }

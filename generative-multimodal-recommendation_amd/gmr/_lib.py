@@ -76,6 +76,8 @@ SIGNATURES = {
     "gmr_eval_metrics_partials": (I64, [I64]),
     "gmr_eval_metrics": (I32, [I64, P, I64, I32, P, P, I32, P, P, P, P]),
     "gmr_adam_f32": (I32, [I64, P, P, P, P, F32, F32, F32, F32, F32, F32, P]),
+    "gmr_colsum_split_floats": (I64, [I64]),
+    "gmr_colsum_split_f32": (I32, [I64, I64, P, I64, P, I32, P, I64, P]),
     # GenRecV1
     "gmr_bn_parts_doubles": (I64, [I64]),
     "gmr_bn_fwd_f32": (I32, [I64, P, I64, I32, F32, F32, P, P, P, P, P, P, P, I32, F32, P, I64, F32, P, I64, I32, P, I64, P, P, I64, P, P]),
@@ -93,11 +95,11 @@ SIGNATURES = {
     "gmr_mul_f32": (I32, [I64, P, P, P, P]),
     "gmr_keep_mask_u8": (I32, [I64, F32, U64, U64, P, P]),
     "gmr_csr_transpose": (I32, [I64, I64, I64, P, P, P, P, P, P, P, P, P, P]),
-    "gmr_csr_drop_count": (I32, [I64, P, P, F32, U64, U64, P, P, P]),
-    "gmr_csr_drop_write": (I32, [I64, P, P, P, P, F32, U64, U64, P, P, P, P]),
+    "gmr_csr_drop_count": (I32, [I64, P, P, I32, P, F32, U64, U64, P, P, P]),
+    "gmr_csr_drop_write": (I32, [I64, P, P, P, I32, P, F32, U64, U64, P, P, P, P]),
     "gmr_knn_symnorm_csr": (I32, [I64, I32, P, I64, P, I64, P, P, P, P, P]),
     "gmr_gen_mask": (I32, [I32, I32, I32, P, I64, P, P, I64, P, P]),
-    "gmr_debias_select": (I32, [I32, I32, P, I64, P, P, I64, F32, U64, U64, P, I32, P, P]),
+    "gmr_debias_select": (I32, [I32, I32, P, I64, P, P, I64, F32, U64, U64, P, P, I32, P, P]),
     "gmr_debias_apply": (I32, [I32, P, P, I32, P, I64, I32, P, P, I64, P]),
     "gmr_kmeans_standardize": (I32, [I64, I32, P, I64, P, P, P, I64, P, P]),
     "gmr_kmeans_pp_pick": (I32, [I64, P, U64, U64, P, P]),

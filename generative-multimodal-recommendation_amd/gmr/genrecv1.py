@@ -213,9 +213,10 @@ class GenRecV1(GeneralRecommender):
         self.text_II_matrix = K.knn_graph(self.t_feat, knn_k)
         self._ii_T = (K.csr_transpose(self.image_II_matrix), K.csr_transpose(self.text_II_matrix))
 
-    def set_image_ui_matrix(self, csr):
+    def set_image_ui_matrix(self, csr, transpose=None):
+        """The rebuilt, edge-dropped UI graph and its transpose (backward of A2 = ui @ E)."""
         self.image_UI_matrix = csr
-        self.image_UI_matrix_T = K.csr_transpose(csr)
+        self.image_UI_matrix_T = transpose if transpose is not None else K.csr_transpose(csr)
 
     def set_item_item_graphs(self, img, txt):
         self.image_II_matrix, self.text_II_matrix = img, txt
@@ -690,8 +691,10 @@ class FlipDiffusion:
                 cnt.append(pk.shape[0])
             npk.copy_(torch.as_tensor(cnt, dtype=torch.int32))
         else:
+            if getattr(self, "_keys", None) is None or self._keys.numel() < 2 * maxp:
+                self._keys = torch.empty(2 * maxp, dtype=torch.int64, device=dev)
             _lib.call("gmr_debias_select", B, kg, ptr(tk), tk.stride(0), ptr(x0), ptr(xs), x0.stride(0), float(ratio),
-                      seed, step, ptr(picks), picks.shape[1], ptr(npk), stream())
+                      seed, step, ptr(self._keys), ptr(picks), picks.shape[1], ptr(npk), stream())
         for t in range(2):
             _lib.call("gmr_debias_apply", t, ptr(picks[t]), ptr(npk), picks.shape[1], ptr(x0), x0.stride(0), I,
                       ptr(labels), ptr(dn), dn.stride(0), stream())

@@ -253,6 +253,11 @@ def mask_scores(scores, rows, cols, fill=-1e10):
 
 def colsum(x, out, group=None, n_groups=1, accumulate=False):
     rows, cols = x.shape
+    if group is None and cols <= 2048 and rows >= 1024:  # few column blocks: split the rows too
+        ws = workspace(32 * cols, x.device, tag="colsum")
+        _lib.call("gmr_colsum_split_f32", rows, cols, ptr(x), _ld(x), ptr(out), int(accumulate), ptr(ws), ws.numel(),
+                  stream())
+        return out
     _lib.call("gmr_colsum_f32", rows, cols, ptr(x), _ld(x), ptr(group), n_groups, ptr(out), int(accumulate),
               stream())
     return out
@@ -302,20 +307,21 @@ def csr_transpose(a):
     return CSR(trp, tcol[:a.nnz], tval[:a.nnz], n_cols=a.n_rows, symmetric=False)
 
 
-def csr_drop_edges(a, keep_rate, seed=0, step=0, keep=None):
+def csr_drop_edges(a, keep_rate, seed=0, step=0, keep=None, transposed=False):
     """SpAdjDropEdge (models/genrecv1.py:443-457): each entry kept iff floor(u + keep_rate) >= 1,
     kept values / keep_rate.  keep: optional 0/1 bytes per entry (CSR order) replacing the draws.
-    One host sync reads the kept count."""
+    transposed (structurally symmetric a only): the transpose of the dropped matrix, from the same
+    draws.  One host sync reads the kept count."""
     dev = a.rowptr.device
     orp = torch.empty(a.n_rows + 1, dtype=torch.int32, device=dev)
     ws = torch.empty(a.n_rows, dtype=torch.int32, device=dev)
-    _lib.call("gmr_csr_drop_count", a.n_rows, ptr(a.rowptr), ptr(keep), float(keep_rate), int(seed), int(step),
-              ptr(ws), ptr(orp), stream())
+    _lib.call("gmr_csr_drop_count", a.n_rows, ptr(a.rowptr), ptr(a.col), int(transposed), ptr(keep), float(keep_rate),
+              int(seed), int(step), ptr(ws), ptr(orp), stream())
     nnz = int(orp[-1].item())
     ocol = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
     oval = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
-    _lib.call("gmr_csr_drop_write", a.n_rows, ptr(a.rowptr), ptr(a.col), ptr(a.val), ptr(keep), float(keep_rate),
-              int(seed), int(step), ptr(orp), ptr(ocol), ptr(oval), stream())
+    _lib.call("gmr_csr_drop_write", a.n_rows, ptr(a.rowptr), ptr(a.col), ptr(a.val), int(transposed), ptr(keep),
+              float(keep_rate), int(seed), int(step), ptr(orp), ptr(ocol), ptr(oval), stream())
     return CSR(orp, ocol[:nnz], oval[:nnz], n_cols=a.n_cols, symmetric=False)
 
 

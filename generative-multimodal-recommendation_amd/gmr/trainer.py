@@ -408,8 +408,10 @@ class GenRecV1Trainer(Trainer):
         uitems = torch.empty(U * kr, dtype=torch.int32, device=dev)
         K.topk_to_user_csr(topk[:U], uptr, uitems)
         g = K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0)
-        g = K.csr_drop_edges(g, m.keep_rate, seed=m.seed, step=5000 + self._epoch_ctr)     # edgeDropper (:789)
-        m.set_image_ui_matrix(g)
+        st = 5000 + self._epoch_ctr                                                      # edgeDropper (:789)
+        gd = K.csr_drop_edges(g, m.keep_rate, seed=m.seed, step=st)
+        gt = K.csr_drop_edges(g, m.keep_rate, seed=m.seed, step=st, transposed=True)    # same draws, transposed
+        m.set_image_ui_matrix(gd, gt)
 
     def _train_epoch(self, train_data, epoch_idx, loss_func=None):
         steps = self.diffusion_phase(epoch_idx)

@@ -239,8 +239,7 @@ class TransformerDenoiser:
             if given is not None:
                 mbuf.copy_(given[l])
             else:  # draw the residual-branch dropout mask (mask only: the LN kernel applies it)
-                _lib.call("gmr_dropout_f32", B, D, 1, ptr(b), K._ld(b) if ldb else 0, keep, None, ptr(mbuf),
-                          mbuf.stride(0), seed, self._site_step(step, l, site), ptr(self._ws["dB"][:B]), D, stream())
+                _lib.call("gmr_keep_mask_u8", B * D, keep, seed, self._site_step(step, l, site), ptr(mbuf), stream())
         _lib.call("gmr_layernorm_fwd", B, D, ptr(a), K._ld(a), ptr(b), ldb, ptr(mbuf), mbuf.stride(0) if mbuf is not None
                   else 0, 1.0 / keep, ptr(wt), ptr(bs), 1e-5, 0, ptr(y), K._ld(y), ptr(s), D, ptr(mean), ptr(rstd),
                   stream())

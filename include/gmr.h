@@ -159,6 +159,12 @@ int gmr_sum_f64(int64_t n, const double* x, double scale, double* out, int32_t a
 int gmr_colsum_f32(int64_t rows, int64_t cols, const float* x, int64_t ld, const int32_t* group, int32_t n_groups,
                    float* out, int32_t accumulate, void* stream);
 
+/* column sums over few columns with the rows split 32 ways (fixed-order partials; workspace
+ * gmr_colsum_split_floats(cols) floats) — bias gradients of the B x 512 transformer products */
+int64_t gmr_colsum_split_floats(int64_t cols);
+int gmr_colsum_split_f32(int64_t rows, int64_t cols, const float* x, int64_t ld, float* out, int32_t accumulate,
+                         float* workspace, int64_t workspace_floats, void* stream);
+
 /* ---------------------------------------------------------------- BPR epoch sampler (dataloader.py:218-275)
  * shuffled interactions + one rejection-sampled negative from `all_items` per interaction */
 int gmr_sample_epoch(int64_t n_inter, const int32_t* inter_user, const int32_t* inter_item, const int32_t* user_rowptr,
@@ -279,12 +285,14 @@ int gmr_csr_transpose(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t
                       const float* val, int32_t* workspace, int32_t* t_rowptr, int32_t* t_col, float* t_val,
                       int32_t* stage_col, float* stage_val, void* stream);
 /* SpAdjDropEdge (:443-457): keep e iff floor(u_e + keep_rate) >= 1 (Philox u, or keep[e]); values / keep_rate.
- * Two calls: counts + out_rowptr (workspace n_rows ints), then the compaction. */
-int gmr_csr_drop_count(int64_t n_rows, const int32_t* rowptr, const uint8_t* keep, float keep_rate, uint64_t seed,
-                       uint64_t step, int32_t* workspace, int32_t* out_rowptr, void* stream);
+ * Two calls: counts + out_rowptr (workspace n_rows ints), then the compaction.  transposed = 1 on a
+ * structurally symmetric matrix gives (dropped A)^T directly (entry (r, c) takes the flag of (c, r)). */
+int gmr_csr_drop_count(int64_t n_rows, const int32_t* rowptr, const int32_t* col, int32_t transposed,
+                       const uint8_t* keep, float keep_rate, uint64_t seed, uint64_t step, int32_t* workspace,
+                       int32_t* out_rowptr, void* stream);
 int gmr_csr_drop_write(int64_t n_rows, const int32_t* rowptr, const int32_t* col, const float* val,
-                       const uint8_t* keep, float keep_rate, uint64_t seed, uint64_t step, const int32_t* out_rowptr,
-                       int32_t* out_col, float* out_val, void* stream);
+                       int32_t transposed, const uint8_t* keep, float keep_rate, uint64_t seed, uint64_t step,
+                       const int32_t* out_rowptr, int32_t* out_col, float* out_val, void* stream);
 /* kNN graph from per-row top-k (idx, sim) (utils/utils.py:184-197, 'sym'): deg = row sums of the
  * kept sims (top-k order), w = d_r v d_c, d = deg^-1/2 (inf -> 0); rowptr n+1, col/val n*k */
 int gmr_knn_symnorm_csr(int64_t n, int32_t k, const int32_t* topi, int64_t ldi, const float* topv, int64_t ldv,
@@ -296,8 +304,8 @@ int gmr_gen_mask(int32_t B, int32_t I, int32_t k, const int32_t* topi, int64_t l
  * gen_topk positions (n = int(count * ratio)); picks[type][max_picks][2] = (row, item), n_picks[2];
  * then the cluster rules (labels < 64) applied to den in place */
 int gmr_debias_select(int32_t B, int32_t k, const int32_t* topi, int64_t ldt, const float* x0, const float* xs,
-                      int64_t ld, float ratio, uint64_t seed, uint64_t step, int32_t* picks, int32_t max_picks,
-                      int32_t* n_picks, void* stream);
+                      int64_t ld, float ratio, uint64_t seed, uint64_t step, uint64_t* keys_ws /* 2*B*k */,
+                      int32_t* picks, int32_t max_picks, int32_t* n_picks, void* stream);
 int gmr_debias_apply(int32_t type, const int32_t* picks, const int32_t* n_picks, int32_t max_picks, const float* x0,
                      int64_t ld0, int32_t I, const int32_t* labels, float* den, int64_t ldd, void* stream);
 /* K-means pieces (interest_cluster.py:60-79 — StandardScaler + KMeans): distances and centroid sums

@@ -33,6 +33,15 @@ SHAPES = [
     ("cl_dp1_u (NN,N=64)", 2048, 64, 19445, 0, 0, 60),
     ("dout+=G f^T (NT,K=64)", 2048, 7050, 64, 0, 1, 40),
     ("train_Z (NN,N=64)", 2048, 64, 7050, 0, 0, 40),
+    # GenRecV1 ModalDenoiseTransformer (B = 2048, D = 512, I = 6710 TikTok); calls per epoch ~ 5 batches
+    ("tf_lin (NT)", 2048, 512, 512, 0, 1, 5 * 6 * 4 * 6),
+    ("tf_dX (NN)", 2048, 512, 512, 0, 0, 5 * 6 * 4),
+    ("tf_dW (TN)", 512, 512, 2048, 1, 0, 5 * 6 * 4),
+    ("tf_in (NT)", 2048, 512, 6710, 0, 1, 5 * 11),
+    ("tf_out (NT)", 2048, 6710, 256, 0, 1, 5 * 11),
+    ("tf_dg (NN)", 2048, 256, 6710, 0, 0, 5),
+    ("tf_dWout (TN)", 6710, 256, 2048, 1, 0, 5),
+    ("tf_dWin (TN)", 512, 6710, 2048, 1, 0, 5),
 ]
 
 
@@ -50,17 +59,18 @@ def run(args):
         C = torch.empty((M, r4(N)), device=dev)[:, :N]
         best = None
         for tile in args.tiles:
+          for split in args.splits:
             for _ in range(3):
-                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=args.split)
+                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=split)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(args.reps):
-                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=args.split)
+                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=split)
             e.record()
             torch.cuda.synchronize()
             us = 1e3 * s.elapsed_time(e) / args.reps
             tf = 2.0 * M * N * Kd / (us * 1e-6) / 1e12
-            print(f"{name:26s} {tile:7d} {us:9.1f} {tf:7.1f} {us * calls / 1e3:9.2f}")
+            print(f"{name:26s} {tile:7d} s{split:<2d} {us:9.1f} {tf:7.1f} {us * calls / 1e3:9.2f}")
             best = us if best is None else min(best, us)
         tot_ms += best * calls / 1e3
     print(f"total GEMM ms/epoch (best tile per shape): {tot_ms:.1f}")
@@ -70,8 +80,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="0,64,128,256,256128,128256")
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--split", type=int, default=0)
+    ap.add_argument("--splits", default="0")
     ap.add_argument("--only", default="", help="substring filter on shape names")
     a = ap.parse_args()
     a.tiles = [int(t) for t in a.tiles.split(",")]
+    a.splits = [int(t) for t in a.splits.split(",")]
     run(a)

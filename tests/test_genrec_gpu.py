@@ -128,6 +128,17 @@ def test_drop_edges_statistics(M):
     assert np.array_equal(d.col.cpu().numpy(), d2.col.cpu().numpy())  # deterministic per (seed, step)
 
 
+def test_drop_edges_transposed(M):
+    """transposed=True on the symmetric rebuilt graph equals the transpose of the dropped graph."""
+    from gmr import kernels as K
+    _, ui = M
+    d = K.csr_drop_edges(ui, 0.5, seed=4, step=2)
+    dt = K.csr_drop_edges(ui, 0.5, seed=4, step=2, transposed=True)
+    ref = K.csr_transpose(d)
+    for x, y in zip(_csr_np(dt), _csr_np(ref)):
+        assert np.array_equal(x, y)
+
+
 def _inject_masks(m, prefix):
     return {k: v for k, v in masks_of(m, prefix).items()}
 

@@ -74,6 +74,21 @@ def test_bipartite_build_large_hubs(K, self_loops):
     assert np.array_equal(csr.val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
 
 
+def test_bipartite_build_many_items(K):
+    """I above the LDS-privatised counting limit (8192 items): global-atomic path."""
+    rng = _rng(6)
+    U, I = 2000, 9000
+    rows = np.repeat(np.arange(U), 4)
+    p = 1.0 / np.arange(1, I + 1) ** 1.1
+    cols = rng.choice(I, size=rows.size, p=p / p.sum())
+    want = graph_ref.ui_adj_csr(U, I, rows, cols)
+    uptr, uitems = _user_csr(U, I, rows, cols)
+    csr = K.bipartite_symnorm(U, I, _dev(uptr), _dev(uitems), 1, 0.0)
+    assert np.array_equal(csr.rowptr.cpu().numpy(), want[0])
+    assert np.array_equal(csr.col.cpu().numpy(), want[1])
+    assert np.array_equal(csr.val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
+
+
 SPMM_SEGS = [64, 128, 512, 2048]  # segment plans (short, default) and blocked plans
 
 
