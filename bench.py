@@ -78,6 +78,13 @@ def pmc_traffic(model="diffmm"):
         return json.load(f), os.path.relpath(files[-1], ROOT)
 
 
+def spmm_kernel_name():
+    from gmr import kernels as K
+    if K.SPMM_SEG_NNZ & K.SPMM_LANE_PLAN:
+        return f"spmm_lane_kernel (CSR, XCD column slices, lane group per row, L={K.SPMM_SEG_NNZ & 0xFFFF})"
+    return "spmm_seg_kernel (CSR, wave/segment)"
+
+
 def summarize_probe(p, model="diffmm"):
     """Aggregate HIP-event timings per kernel class into roofline objects."""
     out = {}
@@ -105,7 +112,7 @@ def summarize_probe(p, model="diffmm"):
             out[tag] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "launches": len(recs),
                         "avg_us": round(1e3 * tot_ms / len(recs), 2), "total_ms": round(tot_ms, 3),
-                        "algorithmic_per_launch": byts / len(recs), "kernel": "spmm_seg_kernel (CSR, wave/segment)"}
+                        "algorithmic_per_launch": byts / len(recs), "kernel": spmm_kernel_name()}
     for tag, o in out.items():
         if tag in pmc:
             o["traffic"] = round(pmc[tag]["traffic_per_launch"])

@@ -10,6 +10,9 @@
 //     wave gathers 64/(16*nb) neighbour rows per instruction.  Single-segment rows
 //     are written directly; hub rows (popular items) write per-segment partials that
 //     a second pass adds in segment order, so results are deterministic.
+#include <algorithm>
+#include <cstdlib>
+
 #include "gmr_common.h"
 
 namespace {
@@ -429,15 +432,183 @@ __global__ void __launch_bounds__(kBlkThreads) spmm_blk_kernel(const int* __rest
   }
 }
 
+// ----------------------------------------------------------------------------------------
+// Lane plan (seg_nnz = GMR_SPMM_LANE_PLAN | L, L = 32, 64 or 128).  The graph-conv adjacencies
+// average ~9 nnz per row with Zipf hub rows of thousands.  The wave-per-segment kernel above
+// launches one wave per row and gathers whole 64*NB-float rows of X, which at d = 128 (13.6 MB at
+// baby) do not fit one XCD's 4 MB L2, so most gathers are served by the Infinity Cache
+// (DESIGN.md 5.1).  Here
+//   * X is cut into S column slices of W = 4*LPR floats (W = 16 for d = 64 and 128, 32 for
+//     d = 256); slice s is served by XCD s (S = 8) or by XCDs s and s + 4 (S = 4, each taking
+//     every other work item): an XCD gathers only its slice, which stays in its L2 (1.7 MB at
+//     baby), and one gather instruction fetches 64/LPR neighbour rows;
+//   * a lane group of LPR lanes owns one row of degree <= L and walks it 8 entries at a time,
+//     the col/val words of the next 8 in flight while the current gathers land; the plan orders
+//     rows by descending degree, so the groups of a wave make (nearly) equal trip counts;
+//   * a row of degree > L (a hub) takes a whole 256-thread workgroup: its lane groups stride
+//     over 8-entry batches and their sums meet in a fixed butterfly + LDS order;
+//   * the grid is a bounded number of workgroups per XCD that loop over the work, so few waves
+//     are launched.  One launch, no partial buffer; every row is summed in a fixed order
+//     wherever it lands, so results are deterministic.
+// Plan: hdr {n_hub, n_short, 0, L}, then n_rows x int4 {row, beg, end, 0}: hub rows (longest
+// first by power of two), then the others by descending degree (rows of one class in any order).
+constexpr int kLaneThreads = 256;
+constexpr int kLaneMaxBuckets = 160;
+
+__device__ __forceinline__ int lane_bucket(int deg, int L, int HB) {
+  return deg > L ? 30 - (31 - __clz(deg)) : HB + (L - deg);
+}
+
+__global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__ rowptr, int n_rows, int L, int HB,
+                                                         int* __restrict__ plan) {
+  __shared__ int s_cnt[kLaneMaxBuckets], s_off[kLaneMaxBuckets];
+  const int t = threadIdx.x, nbk = HB + L + 1;
+  for (int i = t; i < nbk; i += 1024) s_cnt[i] = 0;
+  __syncthreads();
+  for (int r = t; r < n_rows; r += 1024) atomicAdd(&s_cnt[lane_bucket(rowptr[r + 1] - rowptr[r], L, HB)], 1);
+  __syncthreads();
+  if (t == 0) {
+    int o = 0, n_hub = 0;
+    for (int b = 0; b < nbk; ++b) {
+      s_off[b] = o;
+      o += s_cnt[b];
+      if (b == HB - 1) n_hub = o;
+    }
+    plan[0] = n_hub;
+    plan[1] = n_rows - n_hub;
+    plan[2] = 0;
+    plan[3] = L;
+  }
+  __syncthreads();
+  int4* desc = reinterpret_cast<int4*>(plan + kPlanHdr);
+  for (int r = t; r < n_rows; r += 1024) {
+    const int beg = rowptr[r], end = rowptr[r + 1];
+    desc[atomicAdd(&s_off[lane_bucket(end - beg, L, HB)], 1)] = make_int4(r, beg, end, 0);
+  }
+}
+
+template <int LPR>
+__global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __restrict__ col,
+                                                                  const float* __restrict__ val,
+                                                                  const int* __restrict__ plan, int S, int wpx, Src src,
+                                                                  float alpha, float beta, float* __restrict__ y,
+                                                                  int64_t ldy) {
+  constexpr int NW = kLaneThreads / 64;  // waves per workgroup
+  constexpr int NG = 64 / LPR;           // lane groups per wave
+  constexpr int EB = 8;                  // entries per batch
+  constexpr int EPL = EB / LPR;          // col/val words per lane per batch
+  __shared__ float4 s_red[NW][LPR];
+  const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+  const int slice = xcd % S, part = xcd / S, P = 8 / S;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = lane / LPR, sub = lane % LPR, gbase = grp * LPR;
+  const int n_hub = plan[0], n_short = plan[1];
+  const int4* __restrict__ desc = reinterpret_cast<const int4*>(plan + kPlanHdr);
+  const int c0 = slice * 4 * LPR;  // first column of the slice
+  const int blk = c0 >> 6, cin = (c0 & 63) + sub * 4;
+  const float* lo = src.lo[blk] + cin;
+  const float* hi = src.hi[blk] + cin;
+  const int64_t ldl = src.ld_lo[blk], ldh = src.ld_hi[blk], split = src.split;
+  float* yc = y + c0 + sub * 4;
+
+  // sum over the batches at e0, e0 + step, ... below end (e0, end and step are uniform in the group)
+  auto walk = [&](int e0, int end, int step) -> float4 {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int cc[EPL];
+    float vv[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+      const int i = e0 + q * LPR + sub;
+      cc[q] = i < end ? col[i] : 0;
+      vv[q] = i < end ? val[i] : 0.f;
+    }
+    for (int e = e0; e < end; e += step) {
+      float4 xs[EB];
+      float vs[EB];
+#pragma unroll
+      for (int u = 0; u < EB; ++u) {
+        const int c = __shfl(cc[u / LPR], gbase + u % LPR);
+        vs[u] = __shfl(vv[u / LPR], gbase + u % LPR);
+        xs[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e + u < end)
+          xs[u] = *reinterpret_cast<const float4*>(c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh);
+      }
+      const int en = e + step;
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {  // the next batch's indices travel while the gathers land
+        const int i = en + q * LPR + sub;
+        cc[q] = i < end ? col[i] : 0;
+        vv[q] = i < end ? val[i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < EB; ++u) acc = gmr::f4_fma(vs[u], xs[u], acc);
+    }
+    return acc;
+  };
+  auto store = [&](int row, float4 acc) {
+    float* yp = yc + (int64_t)row * ldy;
+    float4 o = gmr::f4_scale(alpha, acc);
+    if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
+    *reinterpret_cast<float4*>(yp) = o;
+  };
+
+  const int wg = part * wpx + k, n_wg = P * wpx;
+  // hub rows: one workgroup each; group partials meet in a fixed butterfly + LDS order
+  for (int hb = wg; hb < n_hub; hb += n_wg) {
+    const int4 d = desc[hb];
+    float4 acc = walk(d.y + (wid * NG + grp) * EB, d.z, NW * NG * EB);
+#pragma unroll
+    for (int m = LPR; m < 64; m <<= 1) acc = gmr::f4_add(acc, gmr::shfl_xor_f4(acc, m));
+    if (grp == 0) s_red[wid][sub] = acc;
+    __syncthreads();
+    if (threadIdx.x < LPR) {
+      float4 s = s_red[0][sub];
+#pragma unroll
+      for (int q = 1; q < NW; ++q) s = gmr::f4_add(s, s_red[q][sub]);
+      store(d.x, s);
+    }
+    __syncthreads();
+  }
+  // short rows: NG consecutive (equal-degree) rows per wave and pass; the next descriptor is in
+  // flight while the current row is walked
+  const int stride = n_wg * NW * NG;
+  int base = (wg * NW + wid) * NG;
+  int4 d = base + grp < n_short ? desc[n_hub + base + grp] : make_int4(-1, 0, 0, 0);
+  for (; base < n_short; base += stride) {
+    const int nb = base + stride + grp;
+    const int4 dn = nb < n_short ? desc[n_hub + nb] : make_int4(-1, 0, 0, 0);
+    const float4 acc = walk(d.y, d.z, EB);
+    if (d.x >= 0) store(d.x, acc);
+    d = dn;
+  }
+}
+
 }  // namespace
 
+static inline int lane_l(int32_t seg_nnz) {  // longest short row of a lane plan, 0 if seg_nnz is invalid
+  const int L = seg_nnz & 0xFFFF;
+  return (seg_nnz & ~0xFFFF) == GMR_SPMM_LANE_PLAN && (L == 32 || L == 64 || L == 128) ? L : 0;
+}
+static inline int lane_hb(int L) { return L == 32 ? 26 : L == 64 ? 25 : 24; }  // hub buckets = 31 - log2(L)
+
+static int lane_wpx_cap() {  // workgroups per XCD of a lane-plan launch (GMR_SPMM_WPX overrides, for tuning)
+  static const int cap = [] {
+    const char* s = getenv("GMR_SPMM_WPX");
+    const int v = s ? atoi(s) : 0;
+    return v > 0 && v <= 1024 ? v : 512;
+  }();
+  return cap;
+}
+
 extern "C" int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_nnz) {
+  if (seg_nnz & GMR_SPMM_LANE_PLAN) return lane_l(seg_nnz) ? kPlanHdr + 4 * n_rows : -1;
   if (seg_nnz <= 0) return -1;
   if (seg_nnz >= 512) return kPlanHdr + 2 * (blk_max_blocks(n_rows, nnz, seg_nnz) + 1);
   return kPlanHdr + 4 * plan_max_seg(n_rows, nnz, seg_nnz) + 3 * plan_max_fix(n_rows, nnz, seg_nnz);
 }
 
 extern "C" int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t seg_nnz) {
+  if (seg_nnz & GMR_SPMM_LANE_PLAN) return lane_l(seg_nnz) ? 1 : -1;  // hub rows are combined in LDS
   if (seg_nnz <= 0) return -1;
   if (seg_nnz >= 512) return 1;  // the blocked variant combines in LDS
   return 2 * ((nnz + seg_nnz - 1) / seg_nnz) + 2;
@@ -447,6 +618,15 @@ extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_
                                    int32_t* plan, void* stream) {
   GMR_ARG(rowptr && plan, "null pointer");
   GMR_ARG(n_rows > 0 && n_rows < (1ll << 31) && nnz >= 0 && nnz < (1ll << 31), "bad size");
+  if (seg_nnz & GMR_SPMM_LANE_PLAN) {
+    const int L = lane_l(seg_nnz);
+    GMR_ARG(L, "lane plans take seg_nnz = GMR_SPMM_LANE_PLAN | 32, 64 or 128");
+    GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
+    hipLaunchKernelGGL(lane_plan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, (int)n_rows, L,
+                       lane_hb(L), plan);
+    GMR_LAUNCHED();
+    return GMR_OK;
+  }
   GMR_ARG((seg_nnz >= 64 && seg_nnz < 512 && seg_nnz % 64 == 0) || (seg_nnz >= 512 && seg_nnz <= 8192),
           "seg_nnz: a multiple of 64 below 512 (segment plan) or 512..8192 (blocked plan)");
   GMR_ARG(n_rows < (1 << 30), "n_rows too large");
@@ -478,7 +658,7 @@ extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const
                                 const float* const* x_lo, const int64_t* ld_lo, const float* const* x_hi,
                                 const int64_t* ld_hi, int64_t split, float alpha, float beta, float* y, int64_t ldy,
                                 int32_t flags, void* stream) {
-  GMR_ARG(rowptr && col && val && plan && y && x_lo && ld_lo, "null pointer");
+  GMR_ARG(rowptr && (nnz == 0 || (col && val)) && plan && y && x_lo && ld_lo, "null pointer");
   GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "n_blocks must be 1, 2 or 4");
   GMR_ARG(n_rows > 0 && nnz >= 0 && ldy >= 64 * n_blocks && ldy % 4 == 0, "bad shape");
   GMR_ARG(((uintptr_t)y & 15) == 0, "y must be 16-byte aligned");
@@ -495,6 +675,23 @@ extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const
     GMR_ARG(s.ld_lo[b] % 4 == 0 && s.ld_hi[b] % 4 == 0, "source ld must be a multiple of 4");
   }
   hipStream_t st0 = (hipStream_t)stream;
+  if (seg_nnz & GMR_SPMM_LANE_PLAN) {
+    GMR_ARG(lane_l(seg_nnz), "bad lane plan seg_nnz");
+    GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
+    const int lpr = n_blocks == 4 ? 8 : 4;  // lanes per row: a slice is 4 * lpr columns
+    const int S = 16 * n_blocks / lpr;      // column slices: 4 (d = 64), 8 (d = 128, 256)
+    const int64_t waves = (n_rows + 64 / lpr - 1) / (64 / lpr) / (8 / S) + 1;  // one pass over the rows
+    const int wpx = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, lane_wpx_cap()));
+    const dim3 grid((unsigned)(8 * wpx));
+    if (lpr == 8)
+      hipLaunchKernelGGL(spmm_lane_kernel<8>, grid, dim3(kLaneThreads), 0, st0, col, val, plan, S, wpx, s, alpha,
+                         beta, y, ldy);
+    else
+      hipLaunchKernelGGL(spmm_lane_kernel<4>, grid, dim3(kLaneThreads), 0, st0, col, val, plan, S, wpx, s, alpha,
+                         beta, y, ldy);
+    GMR_LAUNCHED();
+    return GMR_OK;
+  }
   if (seg_nnz >= 512) {
     const int64_t mb = blk_max_blocks(n_rows, nnz, seg_nnz);
     const int rp = 8 / (2 * n_blocks);

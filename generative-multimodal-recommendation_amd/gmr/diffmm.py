@@ -160,7 +160,7 @@ class DiffMM(GeneralRecommender):
              "partials": f(int(_lib.load().gmr_dmm_final_bwd_partials(N))),
              "logits_u": f(B, (U + 3) // 4 * 4), "lse_u": f(B), "P1_u": f(B, 64),
              "logits_i": f(B, (I + 3) // 4 * 4), "lse_i": f(B), "P1_i": f(B, 64),
-             "part_cl": f(self.norm_adj.partial.shape[0], self.norm_adj.partial.shape[1]),
+             "part_cl": torch.zeros_like(self.norm_adj.partial),  # hub-row scratch of the side-stream product
              "contrib_bpr": f(3 * B, 64), "contrib_cl": f(2 * B, 128),
              "loss_bpr": f(B), "loss_cu": f(B), "loss_ci": f(B), "loss": f(4),
              "sqws": torch.empty(1024, dtype=torch.float64, device=dev)}

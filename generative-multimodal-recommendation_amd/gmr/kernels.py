@@ -142,11 +142,13 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
 
 
 # ----------------------------------------------------------------------------- SpMM
-# SpMM plan: 64..448 = segment plan (wave per <= seg_nnz segment), 512..8192 = blocked plan
-# (see include/gmr.h).  The segment plan at 128 measured fastest on the DiffMM graphs
-# (scripts/spmm_bench.py).
-SPMM_SEG_NNZ = 128
+# SpMM plan: 64..448 = segment plan (wave per <= seg_nnz segment), 512..8192 = blocked plan,
+# SPMM_LANE_PLAN | L = lane plan (XCD column slices, lane group per row)
+# (see include/gmr.h).  The lane plan with L = 32 measured fastest on the DiffMM graphs
+# (scripts/spmm_bench.py, profiles/r01_spmm_lane_bench.txt).
 SPMM_NO_SPLIT_ROWS = 1
+SPMM_LANE_PLAN = 1 << 16  # | L (32, 64, 128): lane plan (include/gmr.h)
+SPMM_SEG_NNZ = SPMM_LANE_PLAN | 32
 
 
 class CSR:
@@ -164,7 +166,7 @@ class CSR:
         words = _lib.load().gmr_spmm_plan_words(self.n_rows, self.nnz, seg_nnz)
         self.plan = torch.empty(words, dtype=torch.int32, device=dev)
         prow = _lib.load().gmr_spmm_partial_rows(self.n_rows, self.nnz, seg_nnz)
-        self.partial = torch.empty((prow, 256), dtype=torch.float32, device=dev)
+        self.partial = torch.zeros((prow, 256), dtype=torch.float32, device=dev)
         _lib.call("gmr_spmm_plan_build", ptr(rowptr), self.n_rows, self.nnz, seg_nnz, ptr(self.plan), stream())
         hdr = (ctypes.c_int32 * 4)()
         _lib.call("gmr_spmm_plan_info", ptr(self.plan), hdr, stream())  # one sync per graph build

@@ -11,8 +11,9 @@ import csv
 import json
 import sys
 
-CLASSES = {"gemm": ("gemm_kernel", "splitk_reduce_kernel"), "spmm": ("spmm_seg_kernel", "spmm_fix_kernel")}
-PRIMARY = {"gemm": "gemm_kernel", "spmm": "spmm_seg_kernel"}
+CLASSES = {"gemm": ("gemm_kernel", "splitk_reduce_kernel"),
+           "spmm": ("spmm_seg_kernel", "spmm_fix_kernel", "spmm_lane_kernel", "spmm_blk_kernel")}
+PRIMARY = {"gemm": ("gemm_kernel",), "spmm": ("spmm_seg_kernel", "spmm_lane_kernel", "spmm_blk_kernel")}
 
 
 def load(path, counter):
@@ -33,7 +34,7 @@ def main():
     for cls, names in CLASSES.items():
         f = sum(v for n, v in fetch if n in names) * 1024 * 2
         w = sum(v for n, v in write if n in names) * 1024
-        launches = sum(1 for n, _ in fetch if n == PRIMARY[cls])
+        launches = sum(1 for n, _ in fetch if n in PRIMARY[cls])
         res[cls] = {"launches": launches, "fetch_bytes": f, "write_bytes": w,
                     "traffic_per_launch": (f + w) / max(launches, 1)}
     print(json.dumps(res, indent=1))

@@ -1,7 +1,7 @@
 """SpMM microbenchmark on the baby-shaped DiffMM graphs (HIP events, 1 process).
 
 python scripts/spmm_bench.py [--segs 128,64,32] [--reps 50]
-Times gmr_spmm_csr_f32 for norm_adj (no self loops) and a rebuilt UI graph (top-1 per user +
+Times gmr_spmm_csr_f32 (graph-replayed reps) for norm_adj (no self loops) and a rebuilt UI graph (top-1 per user +
 self loops) at 1, 2 and 4 column blocks, per plan segment length, checks every variant against
 the first, and prints GB/s with the SURVEY.md 8(d) byte formula.
 """
@@ -63,9 +63,17 @@ def main():
                 blocks = [(X[:, 64 * b:64 * b + 64],) for b in range(nb)]
                 for _ in range(3):
                     g.spmm(Y, blocks)
+                torch.cuda.synchronize()
+                # the reps are replayed from a HIP graph: back-to-back launches without the Python
+                # call overhead, which is longer than these kernels
+                cg = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(cg):
+                    for _ in range(args.reps):
+                        g.spmm(Y, blocks)
+                cg.replay()
+                torch.cuda.synchronize()
                 s.record()
-                for _ in range(args.reps):
-                    g.spmm(Y, blocks)
+                cg.replay()
                 e.record()
                 torch.cuda.synchronize()
                 us = 1e3 * s.elapsed_time(e) / args.reps

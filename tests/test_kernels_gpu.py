@@ -89,7 +89,7 @@ def test_bipartite_build_many_items(K):
     assert np.array_equal(csr.val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
 
 
-SPMM_SEGS = [64, 128, 512, 2048]  # segment plans (short, default) and blocked plans
+SPMM_SEGS = [64, 128, 512, 2048, (1 << 16) | 32, (1 << 16) | 64, (1 << 16) | 128]  # segment, blocked, lane plans
 
 
 @pytest.mark.parametrize("seg", SPMM_SEGS)
@@ -133,6 +133,37 @@ def test_spmm_split_sources(K, seg):
     want0 = A @ np.concatenate([uE, F[:, :64]]).astype(np.float64)
     want1 = A @ np.concatenate([uE, F[:, 64:]]).astype(np.float64)
     np.testing.assert_allclose(out.cpu().numpy(), np.concatenate([want0, want1], 1), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("seg", [128, (1 << 16) | 32, (1 << 16) | 128])
+def test_spmm_empty_runs_and_repeat(K, seg):
+    """Long runs of empty rows, a tiny and an empty matrix,
+    and repeated products: bit-identical
+    results across calls."""
+    rng = _rng(4)
+    for n, nnz_rows in ((700, 3), (700, 0), (4000, 600)):
+        deg = np.zeros(n, dtype=np.int64)
+        live = rng.choice(n, size=nnz_rows, replace=False)
+        deg[live] = rng.integers(1, 400, size=nnz_rows)
+        rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+        col = rng.integers(0, n, size=int(rp[-1])).astype(np.int32)
+        val = rng.standard_normal(col.size).astype(np.float32)
+        csr = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=seg)
+        X = rng.standard_normal((n, 128)).astype(np.float32)
+        Xd = _dev(X)
+        Y0 = rng.standard_normal((n, 128)).astype(np.float32)
+        blocks = [(Xd[:, :64],), (Xd[:, 64:],)]
+        outs = []
+        for _ in range(3):
+            Yd = _dev(Y0)
+            csr.spmm(Yd, blocks, alpha=1.5, beta=-0.5)
+            outs.append(Yd.cpu().numpy())
+        A = np.zeros((n, n))
+        np.add.at(A, (np.repeat(np.arange(n), np.diff(rp)), col), val.astype(np.float64))  # duplicates add
+        want = 1.5 * (A @ X.astype(np.float64)) - 0.5 * Y0
+        np.testing.assert_allclose(outs[0], want, rtol=1e-5, atol=1e-4)
+        for o in outs[1:]:
+            assert np.array_equal(o.view(np.uint32), outs[0].view(np.uint32))
 
 
 GEMM_CASES = [
