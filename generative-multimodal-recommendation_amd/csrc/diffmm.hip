@@ -9,6 +9,8 @@
 //   M       = w0 * E_img + w1 * E_txt       N x 64
 //   Emb     = M + adj@M + ris * norm(M)     N x 64   (forward_MM output)
 // Reference: models/diffmm.py:129-258.
+#include <algorithm>
+
 #include "gmr_common.h"
 
 namespace {
@@ -653,6 +655,262 @@ __global__ void sum_f64_kernel(int64_t n, const double* __restrict__ x, double s
 extern "C" int gmr_sum_f64(int64_t n, const double* x, double scale, double* out, int32_t accumulate, void* stream) {
   GMR_ARG(x && out && n >= 0, "bad args");
   hipLaunchKernelGGL(sum_f64_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n, x, scale, out, accumulate);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+// ============================================================================ K8 fused InfoNCE
+// contrastLoss (models/diffmm.py:251-258) forward + backward without the B x n logit matrix.
+// P = gathered view-1 rows (B x 64, ldp), T = view-2 table (n x 64, ldt), t = 1/temp, k = coef t:
+//   E_ij = exp(t <P_i, T_j>),   z_i = sum_j E_ij,   loss_i = log z_i - t <P_i, T_node(i)>
+//   dP_i = k (sum_j E_ij T_j / z_i - T_node(i)),    dT_j = k sum_i (E_ij / z_i) P_i
+// (the -k P_i term of table row node(i) goes through the sorted scatter with the sparse terms).
+// Rows pass: a wave owns 32 rows i, the workgroup's 4 waves share 32-row blocks of T staged in
+// LDS.  S^T = T_blk P^T runs on the f32 matrix cores (v_mfma_f32_32x32x2_f32; k order
+// d = 32u + 16h + s so both fragments are float4 reads), E = exp in registers, then
+// U^T += T_blk^T E^T takes the exp'd accumulator itself as the B operand: its rows j sit in the
+// registers, so MFMA step e pairs with j = (e&3) + 8(e>>2) + 4h and only T[j][d] is read (LDS).
+// The grid splits j into chunks; the finalise pass adds the per-chunk (U_i, z_i) in chunk order.
+// Table pass: the same with the roles swapped (a wave owns 32 table rows, the workgroup shares
+// blocks of P and r_i = k / z_i); per-row-chunk partials of dT are added in chunk order.
+// Every sum has a fixed order: deterministic.
+namespace {
+
+constexpr int kClLd = 68;  // LDS row stride of a staged 32 x 64 block (floats): conflict-free b128 rows
+typedef float clx16 __attribute__((ext_vector_type(16)));
+
+// two float4 per thread stage a 32 x 64 block: rows r0 .. r0 + 31 of src, zero at and past r_end
+__device__ __forceinline__ void cl_load(float4 (&st)[2], const float* __restrict__ src, int64_t ld, int r0,
+                                        int r_end) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int idx = threadIdx.x + 256 * q, r = idx >> 4, c4 = (idx & 15) * 4;
+    st[q] = r0 + r < r_end ? ld4(src + (int64_t)(r0 + r) * ld + c4) : f4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+__device__ __forceinline__ void cl_store(const float4 (&st)[2], float* dst) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int idx = threadIdx.x + 256 * q;
+    st4(dst + (idx >> 4) * kClLd + (idx & 15) * 4, st[q]);
+  }
+}
+// 32 x 32 dot tile: rows = the staged block (A operand), columns = the lane's register fragment (B)
+__device__ __forceinline__ clx16 cl_dot(const float* blk, const float4 (&fr)[2][4], int l32, int h) {
+  clx16 s;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) s[e] = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 a = ld4(blk + l32 * kClLd + 32 * u + 16 * h + 4 * q);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, fr[u][q].x, s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, fr[u][q].y, s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, fr[u][q].z, s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, fr[u][q].w, s, 0, 0, 0);
+    }
+  return s;
+}
+// y^T (64 x 32) += blk^T (64 x 32) X, X (32 x 32) in the accumulator registers (row (e&3)+8(e>>2)+4h)
+__device__ __forceinline__ void cl_acc(const float* blk, const clx16& X, clx16& y0, clx16& y1, int l32, int h) {
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int r = (e & 3) + 8 * (e >> 2) + 4 * h;
+    y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(blk[r * kClLd + l32], X[e], y0, 0, 0, 0);
+    y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(blk[r * kClLd + 32 + l32], X[e], y1, 0, 0, 0);
+  }
+}
+// the lane's 64-float column of y^T: registers 4g .. 4g+3 hold d = 8g + 4h + 0..3 (+32 in y1)
+__device__ __forceinline__ void cl_put(float* dst, const clx16& y0, const clx16& y1, int h) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    st4(dst + 8 * g + 4 * h, f4(y0[4 * g], y0[4 * g + 1], y0[4 * g + 2], y0[4 * g + 3]));
+    st4(dst + 32 + 8 * g + 4 * h, f4(y1[4 * g], y1[4 * g + 1], y1[4 * g + 2], y1[4 * g + 3]));
+  }
+}
+__device__ __forceinline__ void cl_frag(float4 (&fr)[2][4], const float* __restrict__ src, int64_t ld, int row,
+                                        int n_rows, int h) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      fr[u][q] = row < n_rows ? ld4(src + (int64_t)row * ld + 32 * u + 16 * h + 4 * q) : f4(0.f, 0.f, 0.f, 0.f);
+}
+
+__global__ void __launch_bounds__(256) cl_rows_kernel(int B, int n, const float* __restrict__ P, int64_t ldp,
+                                                      const float* __restrict__ T, int64_t ldt, float inv_t, int chunk,
+                                                      float* __restrict__ part_u, float* __restrict__ part_z) {
+  __shared__ __attribute__((aligned(16))) float s_blk[2][32 * kClLd];
+  const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const int i = blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + l32;  // the lane's row (a column of S^T)
+  const int c = blockIdx.y, j0 = c * chunk, j1 = min(n, j0 + chunk);
+  float4 fr[2][4];
+  cl_frag(fr, P, ldp, i, B, h);
+  clx16 y0, y1;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) y0[e] = y1[e] = 0.f;
+  float z = 0.f;
+  float4 st[2];
+  cl_load(st, T, ldt, j0, j1);
+  cl_store(st, s_blk[0]);
+  __syncthreads();
+  int cur = 0;
+  for (int j = j0; j < j1; j += 32) {
+    const bool more = j + 32 < j1;
+    if (more) cl_load(st, T, ldt, j + 32, j1);
+    const float* blk = s_blk[cur];
+    clx16 s = cl_dot(blk, fr, l32, h);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int r = (e & 3) + 8 * (e >> 2) + 4 * h;
+      s[e] = j + r < j1 ? expf(inv_t * s[e]) : 0.f;
+      z += s[e];
+    }
+    cl_acc(blk, s, y0, y1, l32, h);
+    if (more) cl_store(st, s_blk[cur ^ 1]);
+    __syncthreads();
+    cur ^= 1;
+  }
+  z += __shfl_xor(z, 32);
+  if (i < B) {
+    cl_put(part_u + ((int64_t)c * B + i) * 64, y0, y1, h);
+    if (h == 0) part_z[(int64_t)c * B + i] = z;
+  }
+}
+
+// one wave per row i, lane = d: chunk partials in order, loss, dense dP row, r_i = k / z_i
+__global__ void __launch_bounds__(256) cl_finalize_kernel(int B, int nc, const float* __restrict__ part_u,
+                                                          const float* __restrict__ part_z, const float* __restrict__ CLN,
+                                                          const int* __restrict__ nodes, int64_t node_off, float inv_t,
+                                                          float coef, float* __restrict__ loss,
+                                                          float* __restrict__ contrib, int64_t ld_contrib,
+                                                          float* __restrict__ r_out) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), d = threadIdx.x & 63;
+  if (i >= B) return;
+  float u = 0.f, z = 0.f;
+  for (int c = 0; c < nc; ++c) {
+    u += part_u[((int64_t)c * B + i) * 64 + d];
+    z += part_z[(int64_t)c * B + i];
+  }
+  const int64_t t = node_off + nodes[i];
+  const float p1 = CLN[t * 128 + d], p2 = CLN[t * 128 + 64 + d];
+  const float dot = gmr::wave_sum(p1 * p2);
+  const float k = coef * inv_t;
+  float* o = contrib + (int64_t)i * ld_contrib;
+  o[d] = k * (u / z - p2);
+  o[64 + d] = -k * p1;
+  if (d == 0) {
+    loss[i] = logf(z) - dot * inv_t;
+    r_out[i] = k / z;
+  }
+}
+
+__global__ void __launch_bounds__(256) cl_table_kernel(int B, int n, const float* __restrict__ P, int64_t ldp,
+                                                       const float* __restrict__ r, const float* __restrict__ T,
+                                                       int64_t ldt, float inv_t, int chunk, float* __restrict__ part_t) {
+  __shared__ __attribute__((aligned(16))) float s_blk[2][32 * kClLd];
+  __shared__ float s_r[2][32];
+  const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const int j = blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + l32;  // the lane's table row
+  const int c = blockIdx.y, i0 = c * chunk, i1 = min(B, i0 + chunk);
+  float4 fr[2][4];
+  cl_frag(fr, T, ldt, j, n, h);
+  clx16 y0, y1;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) y0[e] = y1[e] = 0.f;
+  float4 st[2];
+  float sr = 0.f;
+  cl_load(st, P, ldp, i0, i1);
+  if (threadIdx.x < 32) sr = i0 + (int)threadIdx.x < i1 ? r[i0 + threadIdx.x] : 0.f;
+  cl_store(st, s_blk[0]);
+  if (threadIdx.x < 32) s_r[0][threadIdx.x] = sr;
+  __syncthreads();
+  int cur = 0;
+  for (int i = i0; i < i1; i += 32) {
+    const bool more = i + 32 < i1;
+    if (more) {
+      cl_load(st, P, ldp, i + 32, i1);
+      if (threadIdx.x < 32) sr = i + 32 + (int)threadIdx.x < i1 ? r[i + 32 + threadIdx.x] : 0.f;
+    }
+    const float* blk = s_blk[cur];
+    clx16 s = cl_dot(blk, fr, l32, h);  // S' (rows i of the block x the wave's 32 table rows)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s[e] = s_r[cur][(e & 3) + 8 * (e >> 2) + 4 * h] * expf(inv_t * s[e]);
+    cl_acc(blk, s, y0, y1, l32, h);  // dT^T += P_blk^T (r E)
+    if (more) {
+      cl_store(st, s_blk[cur ^ 1]);
+      if (threadIdx.x < 32) s_r[cur ^ 1][threadIdx.x] = sr;
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (j < n) cl_put(part_t + ((int64_t)c * n + j) * 64, y0, y1, h);
+}
+
+__global__ void cl_table_reduce_kernel(int n, int nc, const float* __restrict__ part_t, float* __restrict__ dT,
+                                       int64_t ld) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (int64_t)n * 16) return;
+  const int64_t j = g >> 4;
+  const int c4 = (int)(g & 15) * 4;
+  float4 s = ld4(part_t + j * 64 + c4);
+  for (int c = 1; c < nc; ++c) s = gmr::f4_add(s, ld4(part_t + ((int64_t)c * n + j) * 64 + c4));
+  st4(dT + j * ld + c4, s);
+}
+
+struct ClPlan {
+  int nca, chunk_a, ncb, chunk_b;
+};
+// chunk the j (rows pass) and i (table pass) ranges for ~1024 workgroups each, in 32-row blocks
+ClPlan cl_plan(int64_t B, int64_t n) {
+  ClPlan p;
+  const int64_t rb = (B + 127) / 128, tb = (n + 127) / 128;
+  int64_t want = std::max<int64_t>(1, std::min<int64_t>((1024 + rb - 1) / rb, (n + 31) / 32));
+  p.chunk_a = (int)(((n + want - 1) / want + 31) / 32 * 32);
+  p.nca = (int)((n + p.chunk_a - 1) / p.chunk_a);
+  want = std::max<int64_t>(1, std::min<int64_t>((1024 + tb - 1) / tb, (B + 31) / 32));
+  p.chunk_b = (int)(((B + want - 1) / want + 31) / 32 * 32);
+  p.ncb = (int)((B + p.chunk_b - 1) / p.chunk_b);
+  return p;
+}
+
+}  // namespace
+
+extern "C" int64_t gmr_contrast_workspace_floats(int32_t B, int64_t n) {
+  if (B <= 0 || n <= 0) return -1;
+  const ClPlan p = cl_plan(B, n);
+  return (int64_t)p.nca * B * 65 + B + (int64_t)p.ncb * n * 64;
+}
+
+extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int64_t ldp, const float* T, int64_t ldt,
+                                      const float* CLN, const int32_t* nodes, int64_t node_off, float inv_temp,
+                                      float coef, float* loss, float* contrib, int64_t ld_contrib, float* dT,
+                                      int64_t ld_dt, float* workspace, int64_t workspace_floats, void* stream) {
+  GMR_ARG(P && T && CLN && nodes && loss && contrib && dT && workspace, "null pointer");
+  GMR_ARG(B > 0 && n > 0 && n < (1ll << 31), "bad size");
+  GMR_ARG(ldp >= 64 && ldt >= 64 && ld_contrib >= 128 && ld_dt >= 64 && ldp % 4 == 0 && ldt % 4 == 0 &&
+              ld_dt % 4 == 0,
+          "bad leading dimension");
+  GMR_ARG((((uintptr_t)P | (uintptr_t)T | (uintptr_t)dT) & 15) == 0, "P, T and dT must be 16-byte aligned");
+  GMR_ARG(workspace_floats >= gmr_contrast_workspace_floats(B, n), "workspace too small");
+  const ClPlan p = cl_plan(B, n);
+  float* part_u = workspace;
+  float* part_z = part_u + (int64_t)p.nca * B * 64;
+  float* r = part_z + (int64_t)p.nca * B;
+  float* part_t = r + B;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(cl_rows_kernel, dim3((unsigned)((B + 127) / 128), (unsigned)p.nca), dim3(256), 0, st, B, (int)n,
+                     P, ldp, T, ldt, inv_temp, p.chunk_a, part_u, part_z);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(cl_finalize_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, p.nca, part_u, part_z, CLN,
+                     nodes, node_off, inv_temp, coef, loss, contrib, ld_contrib, r);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(cl_table_kernel, dim3((unsigned)((n + 127) / 128), (unsigned)p.ncb), dim3(256), 0, st, B, (int)n,
+                     P, ldp, r, T, ldt, inv_temp, p.chunk_b, part_t);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(cl_table_reduce_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n, p.ncb, part_t,
+                     dT, ld_dt);
   GMR_LAUNCHED();
   return GMR_OK;
 }

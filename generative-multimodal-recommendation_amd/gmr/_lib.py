@@ -49,6 +49,8 @@ SIGNATURES = {
     "gmr_bpr_fwd_bwd": (I32, [I32, I64, P, P, P, P, P, P, F32, P]),
     "gmr_row_softmax_f32": (I32, [I64, I64, P, I64, F32, P, P]),
     "gmr_contrast_rows": (I32, [I32, P, P, I64, P, F32, F32, P, P, I64, P]),
+    "gmr_contrast_workspace_floats": (I64, [I32, I64]),
+    "gmr_contrast_fused_f32": (I32, [I32, I64, P, I64, P, I64, P, P, I64, F32, F32, P, P, I64, P, I64, P, I64, P]),
     "gmr_gather_rows_f32": (I32, [I32, I32, P, I64, P, I64, P, I64, P]),
     "gmr_scatter_sorted_f32": (I32, [I32, I32, P, P, I64, P, I64, P]),
     "gmr_sort_batch_keys": (I32, [I64, P, P, P, I32, I64, P, I64, I32, P]),

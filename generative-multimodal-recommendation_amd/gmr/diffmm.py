@@ -9,7 +9,7 @@ Data layout in HBM (N = U + I, d = 64):
               adjacency is streamed once per two 64-wide products
 The BPR/contrastive step (calculate_loss, diffmm.py:203-258) runs as one fused forward and
 a hand-derived backward: 12 CSR SpMM launches (the reference issues 22), fp32 MFMA GEMMs for
-the projections and InfoNCE logits, and deterministic sorted scatter-adds.
+the projections, the fused MFMA InfoNCE (no B x n logits), and deterministic sorted scatter-adds.
 """
 import numpy as np
 import torch
@@ -158,8 +158,7 @@ class DiffMM(GeneralRecommender):
              "DG": f(N, 128), "T3": f(N, 128), "Tcl": f(N, 128), "Ri": f(N, 128), "Rt": f(N, 128),
              "OutI": f(N, 128), "OutT": f(N, 128), "dNF": f(I, 128),
              "partials": f(int(_lib.load().gmr_dmm_final_bwd_partials(N))),
-             "logits_u": f(B, (U + 3) // 4 * 4), "lse_u": f(B), "P1_u": f(B, 64),
-             "logits_i": f(B, (I + 3) // 4 * 4), "lse_i": f(B), "P1_i": f(B, 64),
+             "P1_u": f(B, 64), "P1_i": f(B, 64),
              "part_cl": torch.zeros_like(self.norm_adj.partial),  # hub-row scratch of the side-stream product
              "contrib_bpr": f(3 * B, 64), "contrib_cl": f(2 * B, 128),
              "loss_bpr": f(B), "loss_cu": f(B), "loss_ci": f(B), "loss": f(4),
@@ -209,21 +208,15 @@ class DiffMM(GeneralRecommender):
 
     # ================================================================= fused rec step
     def _contrast(self, w, nodes, off, n_table, slot0, loss_out, B, norm, slot="u"):
-        """InfoNCE of CLN[:, :64] (view 1) vs CLN[:, 64:] (view 2) for the gathered nodes."""
+        """InfoNCE of CLN[:, :64] (view 1) vs CLN[:, 64:] (view 2) for the gathered nodes
+        (contrastLoss, diffmm.py:251-258): one fused MFMA pass over the table for the loss rows and
+        dP, one for the dense table gradient (gmr_contrast_fused_f32) - no B x n logits in HBM."""
         CLN, P1 = w["CLN"], w["P1_" + slot][:B]
-        inv_t = 1.0 / self.temp
-        coef = self.ssl_reg / norm
-        table = CLN[off:off + n_table, 64:]
-        L = w["logits_" + slot][:B, :n_table]
-        lse = w["lse_" + slot]
         K.gather_rows(CLN[:, :64], nodes, P1, off=off)
-        K.gemm(P1, table, L, trans_b=True, alpha=inv_t)                         # logits / temp
-        _lib.call("gmr_row_softmax_f32", B, n_table, ptr(L), L.stride(0), coef, ptr(lse), stream())
         contrib = w["contrib_cl"][slot0:slot0 + B]
-        K.gemm(L, table, contrib[:, :64], alpha=inv_t)                          # dp1 (dense part)
-        K.gemm(L, P1, w["dCLN"][off:off + n_table, 64:], trans_a=True, alpha=inv_t)  # d table
-        _lib.call("gmr_contrast_rows", B, ptr(CLN), ptr(nodes), off, ptr(lse), inv_t, coef, ptr(loss_out),
-                  ptr(contrib), contrib.stride(0), stream())
+        ws = K.contrast_workspace(B, n_table, self.device, "cl_" + slot)
+        K.contrast_fused(P1, CLN[off:off + n_table, 64:], CLN, nodes, off, 1.0 / self.temp, self.ssl_reg / norm,
+                         loss_out, contrib, w["dCLN"][off:off + n_table, 64:], ws)
 
     def rec_step(self, users, pos, neg, plan_bpr=None, plan_cl=None, norm_rows=None, reg_share=1.0):
         """Loss of calculate_loss (cl_method 0) and all rec-parameter gradients (into rec_slab.grad).

@@ -253,6 +253,20 @@ def mask_scores(scores, rows, cols, fill=-1e10):
               stream())
 
 
+def contrast_workspace(B, n, device, tag):
+    return workspace(int(_lib.load().gmr_contrast_workspace_floats(B, n)), device, tag=tag)
+
+
+def contrast_fused(P, T, CLN, nodes, node_off, inv_temp, coef, loss, contrib, dT, ws):
+    """K8 fused InfoNCE (include/gmr.h gmr_contrast_fused_f32): loss rows, dP rows into contrib and
+    the dense table gradient dT, without the B x n logits."""
+    B, n = P.shape[0], T.shape[0]
+    with _Probe("infonce", (B, n)):
+        _lib.call("gmr_contrast_fused_f32", B, n, ptr(P), _ld(P), ptr(T), _ld(T), ptr(CLN), ptr(nodes), node_off,
+                  float(inv_temp), float(coef), ptr(loss), ptr(contrib), _ld(contrib), ptr(dT), _ld(dT), ptr(ws),
+                  ws.numel(), stream())
+
+
 def colsum(x, out, group=None, n_groups=1, accumulate=False):
     rows, cols = x.shape
     if group is None and cols <= 2048 and rows >= 1024:  # few column blocks: split the rows too

@@ -148,6 +148,19 @@ int gmr_fill2d_f32(int64_t rows, int64_t cols, float* p, int64_t ld, float value
 int gmr_row_softmax_f32(int64_t rows, int64_t cols, float* L, int64_t ld, float coef, float* lse, void* stream);
 int gmr_contrast_rows(int32_t B, const float* CLN, const int32_t* nodes, int64_t node_off, const float* lse,
                       float inv_temp, float coef, float* loss, float* contrib, int64_t ld_contrib, void* stream);
+/* K8 fused InfoNCE: forward + backward of DiffMM.contrastLoss (models/diffmm.py:251-258) for one
+ * gathered batch, replacing the logits GEMM + row softmax + two gradient GEMMs.  P = view-1 rows of
+ * the batch (B x 64, ldp; P_i = CLN[node_off + nodes[i], 0:64]), T = the view-2 table (n x 64, ldt),
+ * CLN = the N x 128 [view 1 | view 2] table.  Writes loss[i] = log sum_j exp(<P_i,T_j>/temp) -
+ * <P_i,T_node(i)>/temp; contrib[i, 0:64] = dL/dP_i and contrib[i, 64:128] = -coef/temp P_i (the
+ * T_node(i) term, for the caller's scatter); dT (n x 64, ld_dt, overwritten) = the dense table
+ * gradient; gradients scaled by coef.  No B x n matrix in HBM; f32 MFMA; deterministic.
+ * workspace: gmr_contrast_workspace_floats(B, n) floats. */
+int64_t gmr_contrast_workspace_floats(int32_t B, int64_t n);
+int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int64_t ldp, const float* T, int64_t ldt,
+                           const float* CLN, const int32_t* nodes, int64_t node_off, float inv_temp, float coef,
+                           float* loss, float* contrib, int64_t ld_contrib, float* dT, int64_t ld_dt, float* workspace,
+                           int64_t workspace_floats, void* stream);
 /* K2 gather / deterministic scatter-add through a sorted (key << 32 | slot) plan */
 int gmr_gather_rows_f32(int32_t B, int32_t cols, const float* src, int64_t lds, const int32_t* idx, int64_t off,
                         float* out, int64_t ldo, void* stream);

@@ -284,3 +284,42 @@ def test_normalize_rows_and_bwd(K):
     dx = torch.empty(333, 64, device=DEV)
     K.normalize_rows_bwd(yd, nrm, dy.to(DEV), dx, slope=0.2)
     np.testing.assert_allclose(dx.cpu().numpy(), xr.grad[:, :64].numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,n", [(2048, 19445), (974, 7050), (37, 100), (300, 33)])
+def test_contrast_fused_vs_fp64(K, B, n):
+    """K8 fused InfoNCE (gmr_contrast_fused_f32: contrastLoss fwd + bwd without the B x n logits)
+    vs a float64 restatement of models/diffmm.py:251-258 on unit rows (|logit| <= 1/temp, no max
+    subtraction, as the reference).  Loss rows rtol 1e-5; gradients rtol 2e-4 of their scale."""
+    rng = _rng(11)
+    off = 5
+    N = off + n + 3
+    C = rng.standard_normal((N, 128))
+    C[:, :64] /= np.linalg.norm(C[:, :64], axis=1, keepdims=True)
+    C[:, 64:] /= np.linalg.norm(C[:, 64:], axis=1, keepdims=True)
+    C = C.astype(np.float32)
+    nodes = rng.integers(0, n, B).astype(np.int32)
+    temp, coef = 0.1, 0.01 / B
+    Cd, nd = _dev(C), _dev(nodes)
+    P = torch.empty((B, 64), device=DEV)
+    K.gather_rows(Cd[:, :64], nd, P, off=off)
+    loss = torch.empty(B, device=DEV)
+    contrib = torch.empty((B, 128), device=DEV)
+    dbuf = torch.full((N, 128), float("nan"), device=DEV)
+    ws = K.contrast_workspace(B, n, DEV, "test_cl")
+    K.contrast_fused(P, Cd[off:off + n, 64:], Cd, nd, off, 1.0 / temp, coef, loss, contrib, dbuf[off:off + n, 64:], ws)
+    p = C[off + nodes, :64].astype(np.float64)
+    T = C[off:off + n, 64:].astype(np.float64)
+    E = np.exp(p @ T.T / temp)
+    z = E.sum(1)
+    p2 = T[nodes]
+    k = coef / temp
+    want_loss = np.log(z) - (p * p2).sum(1) / temp
+    want_dp = k * (E @ T / z[:, None] - p2)
+    want_dt = k * (E / z[:, None]).T @ p
+    np.testing.assert_allclose(loss.cpu().numpy(), want_loss, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(contrib[:, :64].cpu().numpy(), want_dp, rtol=2e-4, atol=2e-4 * np.abs(want_dp).max())
+    np.testing.assert_allclose(contrib[:, 64:].cpu().numpy(), -k * p, rtol=1e-6, atol=1e-12)
+    got_dt = dbuf[off:off + n, 64:].cpu().numpy()
+    np.testing.assert_allclose(got_dt, want_dt, rtol=2e-4, atol=2e-4 * np.abs(want_dt).max())
+    assert np.isnan(dbuf[:off].cpu().numpy()).all() and np.isnan(dbuf[off:off + n, :64].cpu().numpy()).all()
