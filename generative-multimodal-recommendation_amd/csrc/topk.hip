@@ -24,9 +24,17 @@ __global__ void mask_kernel(int64_t n, const int* __restrict__ rows, const int* 
 
 constexpr int TK_THREADS = 256;
 
+// STAGED: the row's order-preserving keys are staged in LDS once (n_cols <= TK_STAGE_COLS), so the
+// four radix passes and the collection read LDS instead of re-reading the row from HBM / L2.  The
+// histogram adds are run-length aggregated per thread: scores are close together, so the early
+// passes put nearly every key in one bin and per-element LDS atomics would serialise on it.
+constexpr int TK_STAGE_COLS = 36864;  // 144 KB of the 160 KB LDS
+
+template <bool STAGED>
 __global__ void __launch_bounds__(TK_THREADS) topk_rows_kernel(int64_t n_rows, int64_t n_cols, const float* __restrict__ S,
                                                                int64_t ld, int K, int* __restrict__ out_idx,
                                                                int64_t ld_idx, float* __restrict__ out_val) {
+  extern __shared__ uint32_t s_key[];
   __shared__ int hist[256];
   __shared__ uint32_t s_prefix;
   __shared__ int s_need;
@@ -37,6 +45,10 @@ __global__ void __launch_bounds__(TK_THREADS) topk_rows_kernel(int64_t n_rows, i
   if (row >= n_rows) return;
   const float* p = S + row * ld;
   const int t = threadIdx.x;
+  auto key = [&](int64_t j) -> uint32_t { return STAGED ? s_key[j] : fkey(p[j]); };
+  if (STAGED) {
+    for (int64_t j = t; j < n_cols; j += TK_THREADS) s_key[j] = fkey(p[j]);
+  }
 
   uint32_t prefix = 0, pmask = 0;
   int need = K;
@@ -44,10 +56,20 @@ __global__ void __launch_bounds__(TK_THREADS) topk_rows_kernel(int64_t n_rows, i
     const int shift = 24 - 8 * pass;
     hist[t] = 0;
     __syncthreads();
+    int run_bin = 0, run_cnt = 0;
     for (int64_t j = t; j < n_cols; j += TK_THREADS) {
-      const uint32_t k = fkey(p[j]);
-      if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
+      const uint32_t k = key(j);
+      if ((k & pmask) == prefix) {
+        const int b = (k >> shift) & 255;
+        if (b != run_bin && run_cnt) {
+          atomicAdd(&hist[run_bin], run_cnt);
+          run_cnt = 0;
+        }
+        run_bin = b;
+        ++run_cnt;
+      }
     }
+    if (run_cnt) atomicAdd(&hist[run_bin], run_cnt);
     __syncthreads();
     if (t == 0) {
       int acc = 0, b = 255;
@@ -70,7 +92,7 @@ __global__ void __launch_bounds__(TK_THREADS) topk_rows_kernel(int64_t n_rows, i
   const int64_t c0 = t * chunk, c1 = min(n_cols, c0 + chunk);
   int n_gt = 0, n_eq = 0;
   for (int64_t j = c0; j < c1; ++j) {
-    const uint32_t k = fkey(p[j]);
+    const uint32_t k = key(j);
     n_gt += k > T;
     n_eq += k == T;
   }
@@ -92,7 +114,7 @@ __global__ void __launch_bounds__(TK_THREADS) topk_rows_kernel(int64_t n_rows, i
   if (t < 64) cand[t] = ~0ull;
   __syncthreads();
   for (int64_t j = c0; j < c1; ++j) {
-    const uint32_t k = fkey(p[j]);
+    const uint32_t k = key(j);
     int slot = -1;
     if (k > T) slot = gt_slot++;
     else if (k == T) {
@@ -244,9 +266,16 @@ extern "C" int gmr_topk_rows_f32(int64_t n_rows, int64_t n_cols, const float* sc
   if (k == 1)
     hipLaunchKernelGGL(argmax_rows_kernel, dim3((unsigned)n_rows), dim3(256), 0, (hipStream_t)stream, n_rows, n_cols,
                        scores, ld, out_idx, ld_idx, out_val);
-  else
-    hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)n_rows), dim3(TK_THREADS), 0, (hipStream_t)stream, n_rows,
-                       n_cols, scores, ld, k, out_idx, ld_idx, out_val);
+  else if (n_cols <= TK_STAGE_COLS) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(topk_rows_kernel<true>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)sizeof(uint32_t) * TK_STAGE_COLS);
+    if (attr != hipSuccess) return gmr::hip_status(__func__, attr);
+    hipLaunchKernelGGL(topk_rows_kernel<true>, dim3((unsigned)n_rows), dim3(TK_THREADS), sizeof(uint32_t) * n_cols,
+                       (hipStream_t)stream, n_rows, n_cols, scores, ld, k, out_idx, ld_idx, out_val);
+  } else
+    hipLaunchKernelGGL(topk_rows_kernel<false>, dim3((unsigned)n_rows), dim3(TK_THREADS), 0, (hipStream_t)stream,
+                       n_rows, n_cols, scores, ld, k, out_idx, ld_idx, out_val);
   GMR_LAUNCHED();
   return GMR_OK;
 }
