@@ -65,12 +65,15 @@ def setup(args):
     return cfg, ds, tr, tl, vl, model, trainer
 
 
-def pmc_traffic(model="diffmm"):
+def pmc_traffic(model="diffmm", shape=None):
     """HBM bytes per launch per kernel class from the newest committed PMC summary of this workload
-    (profiles/*_pmc_traffic.json for DiffMM, *_pmc_traffic_<model>.json otherwise; made by
-    scripts/pmc_traffic.sh on the same command)."""
+    (profiles/*_pmc_traffic.json for DiffMM at its default shape, *_pmc_traffic_<model>[_<shape>].json
+    otherwise; made by scripts/pmc_traffic.sh on the same command).  Another workload's counters are
+    never reused: traffic stays null without a summary of this one."""
     import glob
-    pat = "*_pmc_traffic.json" if model == "diffmm" else f"*_pmc_traffic_{model}.json"
+    default = shape in (None, DEFAULT_SHAPE.get(model))
+    tag = model if default else f"{model}_{shape}"
+    pat = "*_pmc_traffic.json" if tag == "diffmm" else f"*_pmc_traffic_{tag}.json"
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)))
     if not files:
         return {}, None
@@ -85,10 +88,10 @@ def spmm_kernel_name():
     return "spmm_seg_kernel (CSR, wave/segment)"
 
 
-def summarize_probe(p, model="diffmm"):
+def summarize_probe(p, model="diffmm", shape=None):
     """Aggregate HIP-event timings per kernel class into roofline objects."""
     out = {}
-    pmc, pmc_src = pmc_traffic(model)
+    pmc, pmc_src = pmc_traffic(model, shape)
     for tag, recs in p.items():
         if not recs:
             continue
@@ -307,7 +310,7 @@ def main():
         trainer._use_graphs = graphs
         if probed:
             raw = K.probe_end()
-            probe_all = summarize_probe(raw, args.model)
+            probe_all = summarize_probe(raw, args.model, args.shape)
             if os.environ.get("GMR_PROBE_REPORT"):
                 report_shapes(raw)
         log(f"warmup epoch {i}: {time.time() - t0:.3f}s")
@@ -323,7 +326,7 @@ def main():
         trainer._train_epoch(tl, args.warmup + i)
     barrier()
     dt = max_over_ranks(time.time() - t0)
-    live = summarize_probe(K.probe_end(), args.model) if not args.no_probe else {}
+    live = summarize_probe(K.probe_end(), args.model, args.shape) if not args.no_probe else {}
     train_ups = U * args.steps / dt
 
     # full-rank evaluation passes (valid split)
