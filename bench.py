@@ -84,7 +84,8 @@ def pmc_traffic(model="diffmm", shape=None):
 def spmm_kernel_name():
     from gmr import kernels as K
     if K.SPMM_SEG_NNZ & K.SPMM_LANE_PLAN:
-        return f"spmm_lane_kernel (CSR, XCD column slices, lane group per row, L={K.SPMM_SEG_NNZ & 0xFFFF})"
+        return (f"spmm_lane_kernel (CSR, XCD column slices, lane group per row, L={K.SPMM_SEG_NNZ & 0xFFFF}; "
+                "norm_adj on the packed lane plan)")
     return "spmm_seg_kernel (CSR, wave/segment)"
 
 

@@ -453,6 +453,7 @@ __global__ void __launch_bounds__(kBlkThreads) spmm_blk_kernel(const int* __rest
 // Plan: hdr {n_hub, n_short, 0, L}, then n_rows x int4 {row, beg, end, 0}: hub rows (longest
 // first by power of two), then the others by descending degree (rows of one class in any order).
 constexpr int kLaneThreads = 256;
+constexpr int kPackTab = 34;  // packed lane plan: bucket-table entries per column (see below)
 constexpr int kLaneMaxBuckets = 160;
 
 __device__ __forceinline__ int lane_bucket(int deg, int L, int HB) {
@@ -460,7 +461,7 @@ __device__ __forceinline__ int lane_bucket(int deg, int L, int HB) {
 }
 
 __global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__ rowptr, int n_rows, int L, int HB,
-                                                         int* __restrict__ plan) {
+                                                         int packed, int* __restrict__ plan) {
   __shared__ int s_cnt[kLaneMaxBuckets], s_off[kLaneMaxBuckets];
   const int t = threadIdx.x, nbk = HB + L + 1;
   for (int i = t; i < nbk; i += 1024) s_cnt[i] = 0;
@@ -476,8 +477,19 @@ __global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__
     }
     plan[0] = n_hub;
     plan[1] = n_rows - n_hub;
-    plan[2] = 0;
+    plan[2] = packed;
     plan[3] = L;
+    if (packed) {  // bucket j = degree L - j: first plan index and first packed entry
+      int* tb = plan + kPlanHdr + 4 * n_rows;
+      int e = 0;
+      for (int j = 0; j <= L; ++j) {
+        tb[j] = s_off[HB + j];
+        tb[kPackTab + j] = e;
+        e += s_cnt[HB + j] * (L - j);
+      }
+      tb[L + 1] = n_rows;
+      tb[kPackTab + L + 1] = e;
+    }
   }
   __syncthreads();
   int4* desc = reinterpret_cast<int4*>(plan + kPlanHdr);
@@ -487,15 +499,40 @@ __global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__
   }
 }
 
-template <int LPR>
+// Packed lane plan (GMR_SPMM_LANE_PLAN | GMR_SPMM_PACKED | 32).  The short rows' col/val are
+// copied into plan order, so the rows of one degree bucket sit back to back with a fixed stride:
+// a lane group finds its row's entries from a 34-entry bucket table in LDS (no descriptor load on
+// the critical path), and the next pass's col/val are in flight while the current gathers land.
+// Plan words after the descriptors: table {first plan index}[34] {first entry}[34], then
+// pcol[nnz], pval[nnz].  Entries keep their CSR order, so sums are bit-identical to the lane plan.
+__host__ __device__ inline int64_t pack_off(int64_t n_rows) { return kPlanHdr + 4 * n_rows + 2 * kPackTab; }
+
+__global__ void __launch_bounds__(256) lane_pack_kernel(const int* __restrict__ col, const float* __restrict__ val,
+                                                        int n_rows, int64_t nnz, int* __restrict__ plan) {
+  const int n_hub = plan[0], L = plan[3];
+  const int* tb = plan + kPlanHdr + 4 * n_rows;
+  const int4* desc = reinterpret_cast<const int4*>(plan + kPlanHdr);
+  int* pcol = plan + pack_off(n_rows);
+  float* pval = reinterpret_cast<float*>(pcol + nnz);
+  for (int k = n_hub + blockIdx.x * blockDim.x + threadIdx.x; k < n_rows; k += gridDim.x * blockDim.x) {
+    const int4 d = desc[k];
+    const int deg = d.z - d.y, j = L - deg;
+    const int e0 = tb[kPackTab + j] + (k - tb[j]) * deg;
+    for (int q = 0; q < deg; ++q) {
+      pcol[e0 + q] = col[d.y + q];
+      pval[e0 + q] = val[d.y + q];
+    }
+  }
+}
+
+template <int LPR, bool PACKED, int EB>
 __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __restrict__ col,
                                                                   const float* __restrict__ val,
                                                                   const int* __restrict__ plan, int S, int wpx, Src src,
                                                                   float alpha, float beta, float* __restrict__ y,
-                                                                  int64_t ldy) {
+                                                                  int64_t ldy, int n_rows, int64_t nnz) {
   constexpr int NW = kLaneThreads / 64;  // waves per workgroup
   constexpr int NG = 64 / LPR;           // lane groups per wave
-  constexpr int EB = 8;                  // entries per batch
   constexpr int EPL = EB / LPR;          // col/val words per lane per batch
   __shared__ float4 s_red[NW][LPR];
   const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
@@ -553,6 +590,11 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
   };
 
   const int wg = part * wpx + k, n_wg = P * wpx;
+  __shared__ int s_tb[2 * kPackTab];
+  if (PACKED) {
+    if (threadIdx.x < 2 * kPackTab) s_tb[threadIdx.x] = plan[kPlanHdr + 4 * n_rows + threadIdx.x];
+    __syncthreads();
+  }
   // hub rows: one workgroup each; group partials meet in a fixed butterfly + LDS order
   for (int hb = wg; hb < n_hub; hb += n_wg) {
     const int4 d = desc[hb];
@@ -573,6 +615,87 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
   // flight while the current row is walked
   const int stride = n_wg * NW * NG;
   int base = (wg * NW + wid) * NG;
+  if constexpr (PACKED) {
+    constexpr int EM = 32 / LPR;  // col/val words per lane of a degree-32 row
+    const int* __restrict__ pcol = plan + pack_off(n_rows);
+    const float* __restrict__ pval = reinterpret_cast<const float*>(pcol + nnz);
+    const int* __restrict__ drow = plan + kPlanHdr;  // desc[k].x = plan + kPlanHdr + 4k
+    // row, degree and entries of short row `base + grp` (bucket j: largest j with s_tb[j] <= k)
+    auto fetch = [&](int b, int& row, int& deg, int* cc, float* vv) {
+      const int k = n_hub + b + grp;
+      deg = 0;
+      row = -1;
+      if (b + grp < n_short) {
+        int j = 0;
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1)
+          if (j + st <= 32 && s_tb[j + st] <= k) j += st;
+        deg = 32 - j;
+        const int e0 = s_tb[kPackTab + j] + (k - s_tb[j]) * deg;
+        row = drow[4 * k];
+#pragma unroll
+        for (int q = 0; q < EM; ++q) {
+          const int i = q * LPR + sub;
+          cc[q] = i < deg ? pcol[e0 + i] : 0;
+          vv[q] = i < deg ? pval[e0 + i] : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < EM; ++q) {
+          cc[q] = 0;
+          vv[q] = 0.f;
+        }
+      }
+    };
+    int row, deg, cc[EM];
+    float vv[EM];
+    fetch(base, row, deg, cc, vv);
+    for (; base < n_short; base += stride) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 xs[EB];
+      float vs[EB];
+      // batch 0 gathers first, then the next pass's indices, then the rest of this row
+#pragma unroll
+      for (int u = 0; u < EB; ++u) {
+        const int c = __shfl(cc[u / LPR], gbase + u % LPR);
+        vs[u] = __shfl(vv[u / LPR], gbase + u % LPR);
+        xs[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (u < deg)
+          xs[u] = *reinterpret_cast<const float4*>(c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh);
+      }
+      int rown, degn, cn[EM];
+      float vn[EM];
+      fetch(base + stride, rown, degn, cn, vn);
+#pragma unroll
+      for (int u = 0; u < EB; ++u) acc = gmr::f4_fma(vs[u], xs[u], acc);
+#pragma unroll
+      for (int bt = 1; bt < 32 / EB; ++bt) {
+        if (bt * EB < deg) {
+#pragma unroll
+          for (int u = 0; u < EB; ++u) {
+            const int e = bt * EB + u;
+            const int c = __shfl(cc[e / LPR], gbase + e % LPR);
+            vs[u] = __shfl(vv[e / LPR], gbase + e % LPR);
+            xs[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < deg)
+              xs[u] =
+                  *reinterpret_cast<const float4*>(c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh);
+          }
+#pragma unroll
+          for (int u = 0; u < EB; ++u) acc = gmr::f4_fma(vs[u], xs[u], acc);
+        }
+      }
+      if (row >= 0) store(row, acc);
+      row = rown;
+      deg = degn;
+#pragma unroll
+      for (int q = 0; q < EM; ++q) {
+        cc[q] = cn[q];
+        vv[q] = vn[q];
+      }
+    }
+    return;
+  }
   int4 d = base + grp < n_short ? desc[n_hub + base + grp] : make_int4(-1, 0, 0, 0);
   for (; base < n_short; base += stride) {
     const int nb = base + stride + grp;
@@ -587,8 +710,10 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
 
 static inline int lane_l(int32_t seg_nnz) {  // longest short row of a lane plan, 0 if seg_nnz is invalid
   const int L = seg_nnz & 0xFFFF;
+  if ((seg_nnz & ~0xFFFF) == (GMR_SPMM_LANE_PLAN | GMR_SPMM_PACKED)) return L == 32 ? L : 0;
   return (seg_nnz & ~0xFFFF) == GMR_SPMM_LANE_PLAN && (L == 32 || L == 64 || L == 128) ? L : 0;
 }
+static inline bool lane_packed(int32_t seg_nnz) { return (seg_nnz & GMR_SPMM_PACKED) != 0; }
 static inline int lane_hb(int L) { return L == 32 ? 26 : L == 64 ? 25 : 24; }  // hub buckets = 31 - log2(L)
 
 static int lane_wpx_cap() {  // workgroups per XCD of a lane-plan launch (GMR_SPMM_WPX overrides, for tuning)
@@ -600,8 +725,28 @@ static int lane_wpx_cap() {  // workgroups per XCD of a lane-plan launch (GMR_SP
   return cap;
 }
 
+static int lane_eb() {  // GMR_SPMM_EB = 16: 16 gathers in flight per lane group and batch (tuning)
+  static const int eb = [] {
+    const char* s = getenv("GMR_SPMM_EB");
+    return s && atoi(s) == 16 ? 16 : 8;
+  }();
+  return eb;
+}
+
+static int lane_wpx_cap_packed() {  // the packed kernel pipelines passes, so it wants fewer, longer waves
+  static const int cap = [] {
+    const char* s = getenv("GMR_SPMM_WPX_PACKED");
+    const int v = s ? atoi(s) : 0;
+    return v > 0 && v <= 1024 ? v : 512;
+  }();
+  return cap;
+}
+
 extern "C" int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_nnz) {
-  if (seg_nnz & GMR_SPMM_LANE_PLAN) return lane_l(seg_nnz) ? kPlanHdr + 4 * n_rows : -1;
+  if (seg_nnz & GMR_SPMM_LANE_PLAN) {
+    if (!lane_l(seg_nnz)) return -1;
+    return lane_packed(seg_nnz) ? pack_off(n_rows) + 2 * nnz : kPlanHdr + 4 * n_rows;
+  }
   if (seg_nnz <= 0) return -1;
   if (seg_nnz >= 512) return kPlanHdr + 2 * (blk_max_blocks(n_rows, nnz, seg_nnz) + 1);
   return kPlanHdr + 4 * plan_max_seg(n_rows, nnz, seg_nnz) + 3 * plan_max_fix(n_rows, nnz, seg_nnz);
@@ -620,10 +765,10 @@ extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_
   GMR_ARG(n_rows > 0 && n_rows < (1ll << 31) && nnz >= 0 && nnz < (1ll << 31), "bad size");
   if (seg_nnz & GMR_SPMM_LANE_PLAN) {
     const int L = lane_l(seg_nnz);
-    GMR_ARG(L, "lane plans take seg_nnz = GMR_SPMM_LANE_PLAN | 32, 64 or 128");
+    GMR_ARG(L, "lane plans take seg_nnz = GMR_SPMM_LANE_PLAN | 32, 64 or 128 (packed: 32)");
     GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
     hipLaunchKernelGGL(lane_plan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, (int)n_rows, L,
-                       lane_hb(L), plan);
+                       lane_hb(L), (int)lane_packed(seg_nnz), plan);
     GMR_LAUNCHED();
     return GMR_OK;
   }
@@ -640,6 +785,17 @@ extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_
   PlanView pv = plan_view(plan, n_rows, nnz, seg_nnz);
   hipLaunchKernelGGL(plan_build_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, (int)n_rows, seg_nnz,
                      pv);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_spmm_plan_pack(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, int32_t seg_nnz,
+                                  int32_t* plan, void* stream) {
+  GMR_ARG(plan && (nnz == 0 || (col && val)), "null pointer");
+  GMR_ARG(n_rows > 0 && n_rows < (1ll << 29) && nnz >= 0 && nnz < (1ll << 31), "bad size");
+  GMR_ARG(lane_l(seg_nnz) && lane_packed(seg_nnz), "not a packed lane plan");
+  const int grid = (int)std::min<int64_t>((n_rows + 255) / 256, 2048);
+  hipLaunchKernelGGL(lane_pack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, col, val, (int)n_rows, nnz, plan);
   GMR_LAUNCHED();
   return GMR_OK;
 }
@@ -681,14 +837,22 @@ extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const
     const int lpr = n_blocks == 4 ? 8 : 4;  // lanes per row: a slice is 4 * lpr columns
     const int S = 16 * n_blocks / lpr;      // column slices: 4 (d = 64), 8 (d = 128, 256)
     const int64_t waves = (n_rows + 64 / lpr - 1) / (64 / lpr) / (8 / S) + 1;  // one pass over the rows
-    const int wpx = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, lane_wpx_cap()));
+    const bool packed = lane_packed(seg_nnz);
+    const int cap = packed ? lane_wpx_cap_packed() : lane_wpx_cap();
+    const int wpx = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, cap));
     const dim3 grid((unsigned)(8 * wpx));
-    if (lpr == 8)
-      hipLaunchKernelGGL(spmm_lane_kernel<8>, grid, dim3(kLaneThreads), 0, st0, col, val, plan, S, wpx, s, alpha,
-                         beta, y, ldy);
-    else
-      hipLaunchKernelGGL(spmm_lane_kernel<4>, grid, dim3(kLaneThreads), 0, st0, col, val, plan, S, wpx, s, alpha,
-                         beta, y, ldy);
+#define GMR_LANE_LAUNCH(LPRV, PK, EBV)                                                                      \
+  hipLaunchKernelGGL((spmm_lane_kernel<LPRV, PK, EBV>), grid, dim3(kLaneThreads), 0, st0, col, val, plan, S, wpx, \
+                     s, alpha, beta, y, ldy, (int)n_rows, nnz)
+    const bool wide = lane_eb() == 16;  // entries gathered per lane group and batch
+    if (lpr == 8) {
+      if (packed) { if (wide) GMR_LANE_LAUNCH(8, true, 16); else GMR_LANE_LAUNCH(8, true, 8); }
+      else { if (wide) GMR_LANE_LAUNCH(8, false, 16); else GMR_LANE_LAUNCH(8, false, 8); }
+    } else {
+      if (packed) { if (wide) GMR_LANE_LAUNCH(4, true, 16); else GMR_LANE_LAUNCH(4, true, 8); }
+      else { if (wide) GMR_LANE_LAUNCH(4, false, 16); else GMR_LANE_LAUNCH(4, false, 8); }
+    }
+#undef GMR_LANE_LAUNCH
     GMR_LAUNCHED();
     return GMR_OK;
   }

@@ -136,7 +136,8 @@ class DiffMM(GeneralRecommender):
         tl = dataloader
         self.user_ptr = torch.as_tensor(tl.uptr_np).to(dev)
         self.user_items = torch.as_tensor(tl.uitems_np).to(dev)
-        self.norm_adj = K.bipartite_symnorm(U, I, self.user_ptr, self.user_items, self_loops=False, deg_eps=1e-7)
+        self.norm_adj = K.bipartite_symnorm(U, I, self.user_ptr, self.user_items, self_loops=False, deg_eps=1e-7,
+                                          seg_nnz=K.SPMM_NORM_ADJ)
         self.image_UI_matrix = None
         self.text_UI_matrix = None
         self._w = None

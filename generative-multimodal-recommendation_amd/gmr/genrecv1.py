@@ -155,7 +155,8 @@ class GenRecV1(GeneralRecommender):
         tl = dataloader
         self.user_ptr = torch.as_tensor(tl.uptr_np).to(dev)
         self.user_items = torch.as_tensor(tl.uitems_np).to(dev)
-        self.norm_adj = K.bipartite_symnorm(U, I, self.user_ptr, self.user_items, self_loops=False, deg_eps=1e-7)
+        self.norm_adj = K.bipartite_symnorm(U, I, self.user_ptr, self.user_items, self_loops=False, deg_eps=1e-7,
+                                          seg_nnz=K.SPMM_NORM_ADJ)
         self.R = K.user_item_csr(U, I, self.user_ptr, self.user_items)
         self.RT = K.csr_transpose(self.R)
         self.image_UI_matrix = None

@@ -148,7 +148,12 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
 # (scripts/spmm_bench.py, profiles/r01_spmm_lane_bench.txt).
 SPMM_NO_SPLIT_ROWS = 1
 SPMM_LANE_PLAN = 1 << 16  # | L (32, 64, 128): lane plan (include/gmr.h)
+SPMM_PACKED = 1 << 17  # | SPMM_LANE_PLAN | 32: packed lane plan (col/val of short rows in plan order)
 SPMM_SEG_NNZ = SPMM_LANE_PLAN | 32
+# the fixed norm_adj (built once, 8 of the 12 products of a DiffMM step) runs the packed lane plan:
+# bit-identical sums, 4-7 % faster there at d = 128/256 and slower on the small rebuilt UI graphs
+# (scripts/spmm_bench.py, profiles/r01g_spmm_packed_bench.txt)
+SPMM_NORM_ADJ = SPMM_PACKED | SPMM_LANE_PLAN | 32
 
 
 class CSR:
@@ -168,6 +173,9 @@ class CSR:
         prow = _lib.load().gmr_spmm_partial_rows(self.n_rows, self.nnz, seg_nnz)
         self.partial = torch.zeros((prow, 256), dtype=torch.float32, device=dev)
         _lib.call("gmr_spmm_plan_build", ptr(rowptr), self.n_rows, self.nnz, seg_nnz, ptr(self.plan), stream())
+        if seg_nnz & SPMM_PACKED:  # col/val are final here (every CSR is built before it is wrapped)
+            _lib.call("gmr_spmm_plan_pack", ptr(col), ptr(val), self.n_rows, self.nnz, seg_nnz, ptr(self.plan),
+                      stream())
         hdr = (ctypes.c_int32 * 4)()
         _lib.call("gmr_spmm_plan_info", ptr(self.plan), hdr, stream())  # one sync per graph build
         self.plan_header = tuple(hdr)

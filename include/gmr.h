@@ -62,17 +62,25 @@ int gmr_zero(void* ptr, int64_t bytes, void* stream);
  *            slices pinned one per XCD (L2-resident), one lane group per row of degree <= L
  *            (rows ordered by degree), one workgroup per hub row (degree > L); one launch,
  *            `partial` unused.
+ *   GMR_SPMM_LANE_PLAN | GMR_SPMM_PACKED | 32: packed lane plan — as the lane plan, with the
+ *            short rows' col/val copied into plan order by gmr_spmm_plan_pack (call it after
+ *            gmr_spmm_plan_build, and again whenever col/val change): a row's entries are found
+ *            from a degree-bucket table, so no descriptor load sits on the gather chain and the
+ *            next rows' entries load while the current gathers land.  Same sums, bit for bit.
  * All are deterministic.  flags: GMR_SPMM_NO_SPLIT_ROWS when the segment plan has no row
  * longer than seg_nnz (gmr_spmm_plan_info header word 1 == 0): the combine pass is skipped. */
 #define GMR_SPMM_NO_SPLIT_ROWS 1
 #define GMR_SPMM_LANE_PLAN (1 << 16)
+#define GMR_SPMM_PACKED (1 << 17)
 int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_nnz);
 int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t seg_nnz);
 int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t seg_nnz, int32_t* plan,
                         void* stream);
 /* Copies the 4-word plan header to the host (synchronises the stream): segment plan
  * {n_segments, n_split_rows, n_partials, 0}; blocked plan {n_blocks, 0, 0, seg_nnz};
- * lane plan {n_hub_rows, n_short_rows, 0, L}. */
+ * lane plan {n_hub_rows, n_short_rows, packed (0/1), L}. */
+int gmr_spmm_plan_pack(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, int32_t seg_nnz,
+                       int32_t* plan, void* stream);
 int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream);
 int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                      const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,

@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--segs", default="128,1024")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--cap", type=int, default=0, help="also time norm_adj with item degrees capped at this (hub test)")
     args = ap.parse_args()
     segs = [int(x) for x in args.segs.split(",")]
     cfg = Config("DiffMM", "baby", {"synthetic": "baby"})
@@ -43,6 +44,29 @@ def main():
         graphs[("norm_adj", seg)] = K.bipartite_symnorm(U, I, uptr, uit, self_loops=False, deg_eps=1e-7, seg_nnz=seg)
         graphs[("ui_top1", seg)] = K.bipartite_symnorm(U, I, torch.arange(U + 1, dtype=torch.int32, device=dev), top1,
                                                        self_loops=True, deg_eps=0.0, seg_nnz=seg)
+    names = ["norm_adj", "ui_top1"]
+    if args.cap:
+        # hub test: the same users and items, each item keeping only its first `cap` users
+        up, ui = tl.uptr_np, tl.uitems_np
+        seen = np.zeros(I, np.int64)
+        keep_rows = []
+        for u in range(U):
+            its = ui[up[u]:up[u + 1]]
+            k = []
+            for i in its:
+                if seen[i] < args.cap:
+                    seen[i] += 1
+                    k.append(i)
+            keep_rows.append(np.array(k, np.int32))
+        cptr = np.zeros(U + 1, np.int32)
+        cptr[1:] = np.cumsum([len(k) for k in keep_rows])
+        cit = np.concatenate(keep_rows).astype(np.int32)
+        for seg in segs:
+            graphs[("adj_cap", seg)] = K.bipartite_symnorm(U, I, torch.as_tensor(cptr).to(dev), torch.as_tensor(cit).to(dev),
+                                                          self_loops=False, deg_eps=1e-7, seg_nnz=seg)
+        names.append("adj_cap")
+        deg = np.bincount(tl.uitems_np, minlength=I)
+        print(f"item degree max {deg.max()} p99 {np.percentile(deg, 99):.0f}; capped nnz {2 * len(cit)} of {2 * len(ui)}")
     X = torch.randn(N, 256, device=dev)
     t = torch.empty_like(X)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -54,7 +78,7 @@ def main():
     us = 1e3 * s.elapsed_time(e) / args.reps
     print(f"copy N x 256 fp32: {us:.1f} us, {2 * X.numel() * 4 / us / 1e3:.0f} GB/s")
     print(f"{'graph':10s} {'nnz':>7s} {'nb':>2s} {'seg':>4s} {'us':>8s} {'GB/s':>7s} {'frac':>6s} max|diff|")
-    for name in ("norm_adj", "ui_top1"):
+    for name in names:
         for nb in (1, 2, 4):
             ref = None
             for seg in segs:

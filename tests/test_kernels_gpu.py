@@ -89,7 +89,8 @@ def test_bipartite_build_many_items(K):
     assert np.array_equal(csr.val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
 
 
-SPMM_SEGS = [64, 128, 512, 2048, (1 << 16) | 32, (1 << 16) | 64, (1 << 16) | 128]  # segment, blocked, lane plans
+LANE32, PACKED32 = (1 << 16) | 32, (1 << 17) | (1 << 16) | 32
+SPMM_SEGS = [64, 128, 512, 2048, LANE32, (1 << 16) | 64, (1 << 16) | 128, PACKED32]  # segment, blocked, lane, packed
 
 
 @pytest.mark.parametrize("seg", SPMM_SEGS)
@@ -135,7 +136,35 @@ def test_spmm_split_sources(K, seg):
     np.testing.assert_allclose(out.cpu().numpy(), np.concatenate([want0, want1], 1), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("seg", [128, (1 << 16) | 32, (1 << 16) | 128])
+@pytest.mark.parametrize("nb", [1, 2, 4])
+def test_spmm_packed_bit_exact_vs_lane(K, nb):
+    """The packed lane plan sums every row in the lane plan's order: bit-identical outputs, on a
+    graph with hub rows, empty rows and rows of degree 31/32/33 around the packed bucket limit."""
+    rng = _rng(7)
+    U, I = 3000, 1200
+    deg = rng.integers(0, 40, size=U)
+    deg[:30] = 32
+    deg[30:60] = 33
+    deg[60:90] = 31
+    rows = np.repeat(np.arange(U), deg)
+    p = 1.0 / np.arange(1, I + 1) ** 1.1
+    cols = rng.choice(I, size=rows.size, p=p / p.sum())
+    rp, col, val = graph_ref.norm_adj_csr(U, I, rows, cols)
+    N = U + I
+    lane = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=LANE32)
+    packed = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=PACKED32)
+    assert packed.plan_header[2] == 1 and packed.plan_header[0] > 0  # packed, with hub rows
+    X = _dev(rng.standard_normal((N, 64 * nb)).astype(np.float32))
+    Y0 = rng.standard_normal((N, 64 * nb)).astype(np.float32)
+    outs = []
+    for g in (lane, packed):
+        Yd = _dev(Y0)
+        g.spmm(Yd, [(X[:, 64 * b:64 * (b + 1)],) for b in range(nb)], alpha=0.9, beta=0.25)
+        outs.append(Yd.cpu().numpy())
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
+@pytest.mark.parametrize("seg", [128, LANE32, (1 << 16) | 128, PACKED32])
 def test_spmm_empty_runs_and_repeat(K, seg):
     """Long runs of empty rows, a tiny and an empty matrix,
     and repeated products: bit-identical
