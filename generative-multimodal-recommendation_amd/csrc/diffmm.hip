@@ -11,6 +11,8 @@
 // Reference: models/diffmm.py:129-258.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "gmr_common.h"
 
 namespace {
@@ -862,14 +864,21 @@ __global__ void cl_table_reduce_kernel(int n, int nc, const float* __restrict__ 
 struct ClPlan {
   int nca, chunk_a, ncb, chunk_b;
 };
-// chunk the j (rows pass) and i (table pass) ranges for ~1024 workgroups each, in 32-row blocks
+// workgroups per pass (GMR_CL_WG_ROWS / GMR_CL_WG_TABLE override, for tuning)
+int cl_wg_target(const char* env, int dflt) {
+  const char* s = getenv(env);
+  const int v = s ? atoi(s) : 0;
+  return v >= 64 && v <= 16384 ? v : dflt;
+}
+// chunk the j (rows pass) and i (table pass) ranges for ~cl_wg_target workgroups each, in 32-row blocks
 ClPlan cl_plan(int64_t B, int64_t n) {
+  static const int wa = cl_wg_target("GMR_CL_WG_ROWS", 512), wb = cl_wg_target("GMR_CL_WG_TABLE", 1024);
   ClPlan p;
   const int64_t rb = (B + 127) / 128, tb = (n + 127) / 128;
-  int64_t want = std::max<int64_t>(1, std::min<int64_t>((1024 + rb - 1) / rb, (n + 31) / 32));
+  int64_t want = std::max<int64_t>(1, std::min<int64_t>((wa + rb - 1) / rb, (n + 31) / 32));
   p.chunk_a = (int)(((n + want - 1) / want + 31) / 32 * 32);
   p.nca = (int)((n + p.chunk_a - 1) / p.chunk_a);
-  want = std::max<int64_t>(1, std::min<int64_t>((1024 + tb - 1) / tb, (B + 31) / 32));
+  want = std::max<int64_t>(1, std::min<int64_t>((wb + tb - 1) / tb, (B + 31) / 32));
   p.chunk_b = (int)(((B + want - 1) / want + 31) / 32 * 32);
   p.ncb = (int)((B + p.chunk_b - 1) / p.chunk_b);
   return p;

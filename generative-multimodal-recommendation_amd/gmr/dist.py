@@ -73,6 +73,21 @@ def all_reduce_(t):
     return t
 
 
+def all_reduce_start(t):
+    """SUM all-reduce issued without blocking the compute stream (RCCL runs it on its own stream);
+    returns a handle for wait(), or None outside a process group.  `t` must not be touched until
+    then: the diffusion phase overlaps one denoiser's gradient exchange with the other's step."""
+    if is_dist():
+        return tdist.all_reduce(t, op=tdist.ReduceOp.SUM, async_op=True)
+    return None
+
+
+def wait(handle):
+    """Make the current stream wait for an all_reduce_start (no host block under RCCL)."""
+    if handle is not None:
+        handle.wait()
+
+
 def all_gather_rows_(full, size):
     """full: (world * size, ...) buffer whose rank slice [rank*size, (rank+1)*size) is filled
     locally; gathers every rank's slice in place."""

@@ -278,6 +278,7 @@ class DiffMMTrainer(Trainer):
         _lib.call("gmr_permutation", U, m.seed, 1000 + self._epoch_ctr, ptr(self._perm), stream())
         K.zero_(self._dloss)
         dens = ((m.denoise_model_image, feats_i), (m.denoise_model_text, feats_t))
+        opts = (self.denoise_opt_image, self.denoise_opt_text)
         steps = 0
         for g, lo in enumerate(range(0, U, B * W)):
             hi = min(U, lo + B * W)
@@ -285,6 +286,7 @@ class DiffMMTrainer(Trainer):
             users = self._perm[lo + a:lo + b]
             nb = users.numel()
             base = ((self._epoch_ctr * 100000 + g) * W + r) * 2
+            pending = []
             for j, (den, feats) in enumerate(dens):
                 if nb > 0:
                     diff, gc = m.diffusion_step(den, users, feats, iE, base + j, norm_rows=hi - lo)
@@ -293,10 +295,11 @@ class DiffMMTrainer(Trainer):
                               stream())
                 else:
                     den.slab.zero_grad()
-                if W > 1:
-                    dist.all_reduce_(den.slab.grad)
-            self.denoise_opt_image.step()
-            self.denoise_opt_text.step()
+                # the image gradient exchange runs while the text denoiser steps (one bucket each)
+                pending.append(dist.all_reduce_start(den.slab.grad) if W > 1 else None)
+            for h, opt in zip(pending, opts):
+                dist.wait(h)
+                opt.step()
             steps += 1
         dist.all_reduce_(self._dloss)
         self._epoch_ctr += 1

@@ -66,7 +66,11 @@ def _rank_main(rank, world, port, out_q):
     loss = part * ((hi - lo) / norm) + share * reg
     loss.backward()
     grads = torch.cat([p[k].grad.reshape(-1) for k in names])
-    dist.all_reduce_(grads)
+    # two buckets in flight at once, as the diffusion phase exchanges its two denoiser slabs
+    half = grads.numel() // 2
+    handles = [dist.all_reduce_start(grads[:half]), dist.all_reduce_start(grads[half:])]
+    for h in handles:
+        dist.wait(h)
     lv = torch.tensor([loss.item()], dtype=torch.float64)
     dist.all_reduce_(lv)
     # all-gather of a padded user shard (the graph-rebuild exchange)
