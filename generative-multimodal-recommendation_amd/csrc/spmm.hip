@@ -123,6 +123,7 @@ struct Src {
   int64_t ld_lo[4];
   int64_t ld_hi[4];
   int64_t split;
+  int64_t panel_rows;  // lane plans: > 0 = X in column-panel layout (gmr_spmm_panel_f32), lo[0] = base
 };
 
 // NB = number of 64-column blocks (d = 64 * NB).  LPR = lanes per neighbour row.
@@ -543,9 +544,12 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
   const int4* __restrict__ desc = reinterpret_cast<const int4*>(plan + kPlanHdr);
   const int c0 = slice * 4 * LPR;  // first column of the slice
   const int blk = c0 >> 6, cin = (c0 & 63) + sub * 4;
-  const float* lo = src.lo[blk] + cin;
-  const float* hi = src.hi[blk] + cin;
-  const int64_t ldl = src.ld_lo[blk], ldh = src.ld_hi[blk], split = src.split;
+  // column-panel X: slice s is a contiguous panel_rows x W block, so an XCD's slice fills whole lines
+  const bool panel = src.panel_rows > 0;
+  const float* lo = panel ? src.lo[0] + (int64_t)slice * src.panel_rows * (4 * LPR) + sub * 4 : src.lo[blk] + cin;
+  const float* hi = panel ? lo : src.hi[blk] + cin;
+  const int64_t ldl = panel ? 4 * LPR : src.ld_lo[blk], ldh = panel ? 4 * LPR : src.ld_hi[blk];
+  const int64_t split = panel ? src.panel_rows : src.split;
   float* yc = y + c0 + sub * 4;
 
   // sum over the batches at e0, e0 + step, ... below end (e0, end and step are uniform in the group)
@@ -800,12 +804,60 @@ extern "C" int gmr_spmm_plan_pack(const int32_t* col, const float* val, int64_t 
   return GMR_OK;
 }
 
+static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
+                       int32_t seg_nnz, int32_t n_blocks, const Src& s, float alpha, float beta, float* y, int64_t ldy,
+                       hipStream_t st0);
+
+extern "C" int gmr_spmm_panel_f32(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
+                                  const int32_t* plan, int32_t seg_nnz, int32_t n_blocks, const float* x_panel,
+                                  int64_t panel_rows, float alpha, float beta, float* y, int64_t ldy, void* stream) {
+  GMR_ARG(plan && y && x_panel && (nnz == 0 || (col && val)), "null pointer");
+  GMR_ARG(lane_l(seg_nnz), "column-panel sources need a lane plan");
+  GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "n_blocks must be 1, 2 or 4");
+  GMR_ARG(n_rows > 0 && panel_rows > 0 && ldy >= 64 * n_blocks && ldy % 4 == 0, "bad shape");
+  GMR_ARG((((uintptr_t)y | (uintptr_t)x_panel | (uintptr_t)plan) & 15) == 0, "pointers must be 16-byte aligned");
+  Src s;
+  for (int b = 0; b < 4; ++b) {
+    s.lo[b] = s.hi[b] = x_panel;
+    s.ld_lo[b] = s.ld_hi[b] = 0;
+  }
+  s.split = panel_rows;
+  s.panel_rows = panel_rows;
+  return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, y, ldy, (hipStream_t)stream);
+}
+
 extern "C" int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream) {
   GMR_ARG(plan && host_hdr, "null pointer");
   hipStream_t st = (hipStream_t)stream;
   hipError_t e = hipMemcpyAsync(host_hdr, plan, sizeof(int32_t) * kPlanHdr, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return gmr::hip_status(__func__, e);
+  return GMR_OK;
+}
+
+static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
+                       int32_t seg_nnz, int32_t n_blocks, const Src& s, float alpha, float beta, float* y, int64_t ldy,
+                       hipStream_t st0) {
+  const int lpr = n_blocks == 4 ? 8 : 4;  // lanes per row: a slice is 4 * lpr columns
+  const int S = 16 * n_blocks / lpr;      // column slices: 4 (d = 64), 8 (d = 128, 256)
+  const int64_t waves = (n_rows + 64 / lpr - 1) / (64 / lpr) / (8 / S) + 1;  // one pass over the rows
+  const bool packed = lane_packed(seg_nnz);
+  const int cap = packed ? lane_wpx_cap_packed() : lane_wpx_cap();
+  const int wpx = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, cap));
+  const dim3 grid((unsigned)(8 * wpx));
+#define GMR_LANE_LAUNCH(LPRV, PK, EBV)                                                                      \
+  hipLaunchKernelGGL((spmm_lane_kernel<LPRV, PK, EBV>), grid, dim3(kLaneThreads), 0, st0, col, val, plan, S, wpx, \
+                   s, alpha, beta, y, ldy, (int)n_rows, nnz)
+  const bool wide = lane_eb() == 16;  // entries gathered per lane group and batch
+  if (lpr == 8) {
+    if (packed) { if (wide) GMR_LANE_LAUNCH(8, true, 16); else GMR_LANE_LAUNCH(8, true, 8); }
+    else { if (wide) GMR_LANE_LAUNCH(8, false, 16); else GMR_LANE_LAUNCH(8, false, 8); }
+  } else {
+    if (packed) { if (wide) GMR_LANE_LAUNCH(4, true, 16); else GMR_LANE_LAUNCH(4, true, 8); }
+    else { if (wide) GMR_LANE_LAUNCH(4, false, 16); else GMR_LANE_LAUNCH(4, false, 8); }
+  }
+#undef GMR_LANE_LAUNCH
+  GMR_LAUNCHED();
   return GMR_OK;
 }
 
@@ -820,6 +872,7 @@ extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const
   GMR_ARG(((uintptr_t)y & 15) == 0, "y must be 16-byte aligned");
   Src s;
   s.split = split;
+  s.panel_rows = 0;
   for (int b = 0; b < 4; ++b) {
     int bb = b < n_blocks ? b : 0;
     s.lo[b] = x_lo[bb];
@@ -834,27 +887,7 @@ extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const
   if (seg_nnz & GMR_SPMM_LANE_PLAN) {
     GMR_ARG(lane_l(seg_nnz), "bad lane plan seg_nnz");
     GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
-    const int lpr = n_blocks == 4 ? 8 : 4;  // lanes per row: a slice is 4 * lpr columns
-    const int S = 16 * n_blocks / lpr;      // column slices: 4 (d = 64), 8 (d = 128, 256)
-    const int64_t waves = (n_rows + 64 / lpr - 1) / (64 / lpr) / (8 / S) + 1;  // one pass over the rows
-    const bool packed = lane_packed(seg_nnz);
-    const int cap = packed ? lane_wpx_cap_packed() : lane_wpx_cap();
-    const int wpx = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, cap));
-    const dim3 grid((unsigned)(8 * wpx));
-#define GMR_LANE_LAUNCH(LPRV, PK, EBV)                                                                      \
-  hipLaunchKernelGGL((spmm_lane_kernel<LPRV, PK, EBV>), grid, dim3(kLaneThreads), 0, st0, col, val, plan, S, wpx, \
-                     s, alpha, beta, y, ldy, (int)n_rows, nnz)
-    const bool wide = lane_eb() == 16;  // entries gathered per lane group and batch
-    if (lpr == 8) {
-      if (packed) { if (wide) GMR_LANE_LAUNCH(8, true, 16); else GMR_LANE_LAUNCH(8, true, 8); }
-      else { if (wide) GMR_LANE_LAUNCH(8, false, 16); else GMR_LANE_LAUNCH(8, false, 8); }
-    } else {
-      if (packed) { if (wide) GMR_LANE_LAUNCH(4, true, 16); else GMR_LANE_LAUNCH(4, true, 8); }
-      else { if (wide) GMR_LANE_LAUNCH(4, false, 16); else GMR_LANE_LAUNCH(4, false, 8); }
-    }
-#undef GMR_LANE_LAUNCH
-    GMR_LAUNCHED();
-    return GMR_OK;
+    return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, y, ldy, st0);
   }
   if (seg_nnz >= 512) {
     const int64_t mb = blk_max_blocks(n_rows, nnz, seg_nnz);

@@ -214,6 +214,20 @@ class CSR:
         return out
 
 
+def spmm_panel(a, out, x_panel, nb, alpha=1.0, beta=0.0):
+    """out = alpha * A @ X + beta * out with X given in column-panel layout (S, n, W), see
+    include/gmr.h gmr_spmm_panel_f32 (lane plans only)."""
+    W = 32 if nb == 4 else 16
+    if x_panel.shape != (64 * nb // W, a.n_cols, W) or not x_panel.is_contiguous():
+        raise ValueError(f"x_panel must be a contiguous ({64 * nb // W}, {a.n_cols}, {W}) panel stack")
+    if out.shape[0] != a.n_rows or out.shape[1] != 64 * nb:
+        raise ValueError("out shape")
+    with _Probe("spmm", (a.nnz, a.n_rows, a.n_cols, nb, beta != 0.0)):
+        _lib.call("gmr_spmm_panel_f32", ptr(a.col), ptr(a.val), a.n_rows, a.nnz, ptr(a.plan), a.seg_nnz, nb,
+                  ptr(x_panel), a.n_cols, float(alpha), float(beta), ptr(out), _ld(out), stream())
+    return out
+
+
 def bipartite_symnorm(n_users, n_items, user_ptr, user_items, self_loops, deg_eps, seg_nnz=None):
     """Build the normalised (U+I)^2 bipartite adjacency on the device (graph.hip)."""
     lib = _lib.load()

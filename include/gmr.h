@@ -81,6 +81,13 @@ int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int3
  * lane plan {n_hub_rows, n_short_rows, packed (0/1), L}. */
 int gmr_spmm_plan_pack(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, int32_t seg_nnz,
                        int32_t* plan, void* stream);
+/* Lane-plan SpMM with X in column-panel layout: S contiguous panels of panel_rows x W floats
+ * (W = 16 for n_blocks 1 and 2, 32 for 4; S = 64 * n_blocks / W), panel s holding columns
+ * [s*W, (s+1)*W) of X, so each XCD's slice occupies whole cache lines.  Same sums as
+ * gmr_spmm_csr_f32 on the row-major X. */
+int gmr_spmm_panel_f32(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
+                       int32_t seg_nnz, int32_t n_blocks, const float* x_panel, int64_t panel_rows, float alpha,
+                       float beta, float* y, int64_t ldy, void* stream);
 int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream);
 int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                      const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,

@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--segs", default="128,1024")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--panel", action="store_true", help="also time column-panel sources (lane plans)")
     ap.add_argument("--cap", type=int, default=0, help="also time norm_adj with item degrees capped at this (hub test)")
     args = ap.parse_args()
     segs = [int(x) for x in args.segs.split(",")]
@@ -108,6 +109,27 @@ def main():
                     ref = Y.clone()
                 diff = (Y - ref).abs().max().item()
                 print(f"{name:10s} {g.nnz:7d} {nb:2d} {seg:4d} {us:8.2f} {gbs:7.0f} {gbs / 8000:6.3f} {diff:.2e}")
+                if args.panel and (seg & K.SPMM_LANE_PLAN):
+                    # the same product from a column-panel copy of X (gmr_spmm_panel_f32)
+                    W = 32 if nb == 4 else 16
+                    S = 64 * nb // W
+                    Xp = X[:, :64 * nb].reshape(N, S, W).permute(1, 0, 2).contiguous()
+                    Y2 = torch.empty_like(Y)
+                    cg2 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(cg2):
+                        for _ in range(args.reps):
+                            K.spmm_panel(g, Y2, Xp, nb)
+                    cg2.replay()
+                    torch.cuda.synchronize()
+                    s.record()
+                    cg2.replay()
+                    e.record()
+                    torch.cuda.synchronize()
+                    us = 1e3 * s.elapsed_time(e) / args.reps
+                    gbs = byts / us / 1e3
+                    same = bool(torch.equal(Y2.view(torch.int32), Y.view(torch.int32)))
+                    print(f"{name + '/panel':10s} {g.nnz:7d} {nb:2d} {seg:4d} {us:8.2f} {gbs:7.0f} {gbs / 8000:6.3f} "
+                          f"bit-identical={same}")
 
 
 if __name__ == "__main__":

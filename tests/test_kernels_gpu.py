@@ -164,6 +164,31 @@ def test_spmm_packed_bit_exact_vs_lane(K, nb):
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
 
 
+@pytest.mark.parametrize("seg", [LANE32, PACKED32])
+@pytest.mark.parametrize("nb", [1, 2, 4])
+def test_spmm_panel_sources_bit_exact(K, nb, seg):
+    """gmr_spmm_panel_f32: X as column panels gives the row-major product bit for bit."""
+    rng = _rng(8)
+    U, I = 2000, 700
+    deg = rng.integers(0, 30, size=U)
+    rows = np.repeat(np.arange(U), deg)
+    p = 1.0 / np.arange(1, I + 1) ** 1.1
+    cols = rng.choice(I, size=rows.size, p=p / p.sum())
+    rp, col, val = graph_ref.norm_adj_csr(U, I, rows, cols)
+    N = U + I
+    g = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=seg)
+    X = _dev(rng.standard_normal((N, 64 * nb)).astype(np.float32))
+    Y0 = rng.standard_normal((N, 64 * nb)).astype(np.float32)
+    Ya, Yb = _dev(Y0), _dev(Y0)
+    g.spmm(Ya, [(X[:, 64 * b:64 * (b + 1)],) for b in range(nb)], alpha=1.25, beta=0.5)
+    W = 32 if nb == 4 else 16
+    Xp = X.reshape(N, 64 * nb // W, W).permute(1, 0, 2).contiguous()
+    K.spmm_panel(g, Yb, Xp, nb, alpha=1.25, beta=0.5)
+    assert torch.equal(Ya.view(torch.int32), Yb.view(torch.int32))
+    with pytest.raises(ValueError):
+        K.spmm_panel(g, Yb, Xp[:, :-1], nb)
+
+
 @pytest.mark.parametrize("seg", [128, LANE32, (1 << 16) | 128, PACKED32])
 def test_spmm_empty_runs_and_repeat(K, seg):
     """Long runs of empty rows, a tiny and an empty matrix,
