@@ -126,6 +126,12 @@ struct Src {
   int64_t panel_rows;  // lane plans: > 0 = X in column-panel layout (gmr_spmm_panel_f32), lo[0] = base
 };
 
+// lane plans: output block b (64 columns) goes to y[b] with row stride ld[b] (gmr_spmm_multi_f32)
+struct Dst {
+  float* y[4];
+  int64_t ld[4];
+};
+
 // NB = number of 64-column blocks (d = 64 * NB).  LPR = lanes per neighbour row.
 template <int NB>
 __global__ void __launch_bounds__(256) spmm_seg_kernel(const int* __restrict__ col, const float* __restrict__ val,
@@ -530,8 +536,8 @@ template <int LPR, bool PACKED, int EB>
 __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __restrict__ col,
                                                                   const float* __restrict__ val,
                                                                   const int* __restrict__ plan, int S, int wpx, Src src,
-                                                                  float alpha, float beta, float* __restrict__ y,
-                                                                  int64_t ldy, int n_rows, int64_t nnz) {
+                                                                  float alpha, float beta, Dst dst, int n_rows,
+                                                                  int64_t nnz) {
   constexpr int NW = kLaneThreads / 64;  // waves per workgroup
   constexpr int NG = 64 / LPR;           // lane groups per wave
   constexpr int EPL = EB / LPR;          // col/val words per lane per batch
@@ -550,7 +556,8 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
   const float* hi = panel ? lo : src.hi[blk] + cin;
   const int64_t ldl = panel ? 4 * LPR : src.ld_lo[blk], ldh = panel ? 4 * LPR : src.ld_hi[blk];
   const int64_t split = panel ? src.panel_rows : src.split;
-  float* yc = y + c0 + sub * 4;
+  float* yc = dst.y[blk] + (c0 & 63) + sub * 4;
+  const int64_t ldy = dst.ld[blk];
 
   // sum over the batches at e0, e0 + step, ... below end (e0, end and step are uniform in the group)
   auto walk = [&](int e0, int end, int step) -> float4 {
@@ -729,6 +736,18 @@ static int lane_wpx_cap() {  // workgroups per XCD of a lane-plan launch (GMR_SP
   return cap;
 }
 
+static int lane_lpr(int n_blocks) {  // GMR_SPMM_LPR = 4 / 8 overrides (tuning); row-major X only
+  static const int ov = [] {
+    const char* s = getenv("GMR_SPMM_LPR");
+    const int v = s ? atoi(s) : 0;
+    return v == 4 || v == 8 ? v : 0;
+  }();
+  // 16-column slices below d = 256: 32-column ones (full 128-byte lines, 2 XCDs per slice) win
+  // 5-10 % at d = 128 in isolation (profiles/r01h_spmm_lpr_bench.txt) but lose 20-45 % inside the
+  // DiffMM step, next to the side-stream products (rocprof r01j); d = 256 takes 32 columns (S <= 8)
+  return n_blocks == 4 ? 8 : ov ? ov : 4;
+}
+
 static int lane_eb() {  // GMR_SPMM_EB = 16: 16 gathers in flight per lane group and batch (tuning)
   static const int eb = [] {
     const char* s = getenv("GMR_SPMM_EB");
@@ -805,8 +824,16 @@ extern "C" int gmr_spmm_plan_pack(const int32_t* col, const float* val, int64_t 
 }
 
 static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
-                       int32_t seg_nnz, int32_t n_blocks, const Src& s, float alpha, float beta, float* y, int64_t ldy,
+                       int32_t seg_nnz, int32_t n_blocks, const Src& s, float alpha, float beta, const Dst& d,
                        hipStream_t st0);
+static Dst dst_rowmajor(float* y, int64_t ldy, int n_blocks) {
+  Dst d;
+  for (int b = 0; b < 4; ++b) {
+    d.y[b] = y + 64 * (b < n_blocks ? b : 0);
+    d.ld[b] = ldy;
+  }
+  return d;
+}
 
 extern "C" int gmr_spmm_panel_f32(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                                   const int32_t* plan, int32_t seg_nnz, int32_t n_blocks, const float* x_panel,
@@ -823,7 +850,8 @@ extern "C" int gmr_spmm_panel_f32(const int32_t* col, const float* val, int64_t 
   }
   s.split = panel_rows;
   s.panel_rows = panel_rows;
-  return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, y, ldy, (hipStream_t)stream);
+  return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, dst_rowmajor(y, ldy, n_blocks),
+                     (hipStream_t)stream);
 }
 
 extern "C" int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream) {
@@ -836,9 +864,10 @@ extern "C" int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* 
 }
 
 static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
-                       int32_t seg_nnz, int32_t n_blocks, const Src& s, float alpha, float beta, float* y, int64_t ldy,
+                       int32_t seg_nnz, int32_t n_blocks, const Src& s, float alpha, float beta, const Dst& d,
                        hipStream_t st0) {
-  const int lpr = n_blocks == 4 ? 8 : 4;  // lanes per row: a slice is 4 * lpr columns
+  // lanes per row: a slice is 4 * lpr columns (column panels are 16 wide below d = 256)
+  const int lpr = s.panel_rows > 0 ? (n_blocks == 4 ? 8 : 4) : lane_lpr(n_blocks);
   const int S = 16 * n_blocks / lpr;      // column slices: 4 (d = 64), 8 (d = 128, 256)
   const int64_t waves = (n_rows + 64 / lpr - 1) / (64 / lpr) / (8 / S) + 1;  // one pass over the rows
   const bool packed = lane_packed(seg_nnz);
@@ -847,7 +876,7 @@ static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int
   const dim3 grid((unsigned)(8 * wpx));
 #define GMR_LANE_LAUNCH(LPRV, PK, EBV)                                                                      \
   hipLaunchKernelGGL((spmm_lane_kernel<LPRV, PK, EBV>), grid, dim3(kLaneThreads), 0, st0, col, val, plan, S, wpx, \
-                   s, alpha, beta, y, ldy, (int)n_rows, nnz)
+                   s, alpha, beta, d, (int)n_rows, nnz)
   const bool wide = lane_eb() == 16;  // entries gathered per lane group and batch
   if (lpr == 8) {
     if (packed) { if (wide) GMR_LANE_LAUNCH(8, true, 16); else GMR_LANE_LAUNCH(8, true, 8); }
@@ -859,6 +888,33 @@ static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int
 #undef GMR_LANE_LAUNCH
   GMR_LAUNCHED();
   return GMR_OK;
+}
+
+extern "C" int gmr_spmm_multi_f32(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
+                                  const int32_t* plan, int32_t seg_nnz, int32_t n_blocks, const float* const* x_lo,
+                                  const int64_t* ld_lo, const float* const* x_hi, const int64_t* ld_hi, int64_t split,
+                                  float alpha, float beta, float* const* y_blocks, const int64_t* ld_y, void* stream) {
+  GMR_ARG(plan && x_lo && ld_lo && y_blocks && ld_y && (nnz == 0 || (col && val)), "null pointer");
+  GMR_ARG(lane_l(seg_nnz), "per-block outputs need a lane plan");
+  GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "n_blocks must be 1, 2 or 4");
+  GMR_ARG(n_rows > 0 && nnz >= 0 && ((uintptr_t)plan & 15) == 0, "bad shape");
+  Src s;
+  Dst d;
+  s.split = split;
+  s.panel_rows = 0;
+  for (int b = 0; b < 4; ++b) {
+    const int bb = b < n_blocks ? b : 0;
+    s.lo[b] = x_lo[bb];
+    s.ld_lo[b] = ld_lo[bb];
+    s.hi[b] = (split < n_rows && x_hi) ? x_hi[bb] : x_lo[bb];
+    s.ld_hi[b] = (split < n_rows && ld_hi) ? ld_hi[bb] : ld_lo[bb];
+    d.y[b] = y_blocks[bb];
+    d.ld[b] = ld_y[bb];
+    GMR_ARG(s.lo[b] && s.hi[b] && d.y[b], "null block");
+    GMR_ARG((((uintptr_t)s.lo[b] | (uintptr_t)s.hi[b] | (uintptr_t)d.y[b]) & 15) == 0, "blocks must be 16-byte aligned");
+    GMR_ARG(s.ld_lo[b] % 4 == 0 && s.ld_hi[b] % 4 == 0 && d.ld[b] % 4 == 0 && d.ld[b] >= 64, "bad block stride");
+  }
+  return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, d, (hipStream_t)stream);
 }
 
 extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
@@ -887,7 +943,8 @@ extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const
   if (seg_nnz & GMR_SPMM_LANE_PLAN) {
     GMR_ARG(lane_l(seg_nnz), "bad lane plan seg_nnz");
     GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
-    return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, y, ldy, st0);
+    return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, dst_rowmajor(y, ldy, n_blocks),
+                       st0);
   }
   if (seg_nnz >= 512) {
     const int64_t mb = blk_max_blocks(n_rows, nnz, seg_nnz);

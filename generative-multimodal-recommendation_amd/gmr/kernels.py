@@ -214,6 +214,31 @@ class CSR:
         return out
 
 
+def spmm_multi(a, outs, blocks, split=None, alpha=1.0, beta=0.0):
+    """One lane-plan launch for independent products of `a`: block b (64 columns, a (lo, hi) split
+    source as in CSR.spmm) lands in outs[b] (an n_rows x 64 view).  gmr_spmm_multi_f32."""
+    nb = len(blocks)
+    if nb not in (1, 2, 4) or len(outs) != nb:
+        raise ValueError("1, 2 or 4 blocks, one output each")
+    for o in outs:
+        if o.shape != (a.n_rows, 64):
+            raise ValueError(f"output block shape {tuple(o.shape)} != ({a.n_rows}, 64)")
+    PArr, LArr = ctypes.c_void_p * 4, ctypes.c_int64 * 4
+    lo = PArr(*[b[0].data_ptr() for b in blocks] + [0] * (4 - nb))
+    ldl = LArr(*[_ld(b[0]) for b in blocks] + [0] * (4 - nb))
+    if split is None:
+        split, hi, ldh = a.n_cols, lo, ldl
+    else:
+        hi = PArr(*[b[1].data_ptr() for b in blocks] + [0] * (4 - nb))
+        ldh = LArr(*[_ld(b[1]) for b in blocks] + [0] * (4 - nb))
+    ys = PArr(*[o.data_ptr() for o in outs] + [0] * (4 - nb))
+    ldy = LArr(*[_ld(o) for o in outs] + [0] * (4 - nb))
+    with _Probe("spmm", (a.nnz, a.n_rows, a.n_cols, nb, beta != 0.0)):
+        _lib.call("gmr_spmm_multi_f32", ptr(a.col), ptr(a.val), a.n_rows, a.nnz, ptr(a.plan), a.seg_nnz, nb, lo, ldl,
+                  hi, ldh, split, float(alpha), float(beta), ys, ldy, stream())
+    return outs
+
+
 def spmm_panel(a, out, x_panel, nb, alpha=1.0, beta=0.0):
     """out = alpha * A @ X + beta * out with X given in column-panel layout (S, n, W), see
     include/gmr.h gmr_spmm_panel_f32 (lane plans only)."""

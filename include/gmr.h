@@ -88,6 +88,13 @@ int gmr_spmm_plan_pack(const int32_t* col, const float* val, int64_t n_rows, int
 int gmr_spmm_panel_f32(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
                        int32_t seg_nnz, int32_t n_blocks, const float* x_panel, int64_t panel_rows, float alpha,
                        float beta, float* y, int64_t ldy, void* stream);
+/* Lane-plan SpMM with one output per 64-column block: block b goes to y_blocks[b] (row stride
+ * ld_y[b]; host arrays of device pointers / strides).  Fuses independent products of one matrix
+ * (DiffMM's H and K2) into one launch; same sums as the separate gmr_spmm_csr_f32 calls. */
+int gmr_spmm_multi_f32(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
+                       int32_t seg_nnz, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
+                       const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
+                       float* const* y_blocks, const int64_t* ld_y, void* stream);
 int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream);
 int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                      const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,

@@ -189,6 +189,36 @@ def test_spmm_panel_sources_bit_exact(K, nb, seg):
         K.spmm_panel(g, Yb, Xp[:, :-1], nb)
 
 
+@pytest.mark.parametrize("seg", [LANE32, PACKED32])
+def test_spmm_multi_outputs_bit_exact(K, seg):
+    """gmr_spmm_multi_f32: two independent 128-column products of one matrix in one launch, with
+    split sources and per-block outputs, equal the two separate products (bit for bit on the
+    rows of degree <= 32; the hub rows' partial sums split by 8- instead of 4-lane groups)."""
+    rng = _rng(9)
+    U, I = 2200, 800
+    deg = rng.integers(0, 30, size=U)
+    rows = np.repeat(np.arange(U), deg)
+    p = 1.0 / np.arange(1, I + 1) ** 1.1
+    cols = rng.choice(I, size=rows.size, p=p / p.sum())
+    rp, col, val = graph_ref.norm_adj_csr(U, I, rows, cols)
+    N = U + I
+    g = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=seg)
+    G = _dev(rng.standard_normal((N, 128)).astype(np.float32))
+    E = _dev(rng.standard_normal((I, 64)).astype(np.float32))
+    Q = _dev(rng.standard_normal((N, 128)).astype(np.float32))
+    H1, K1 = torch.empty((N, 128), device=DEV), torch.empty((N, 128), device=DEV)
+    g.spmm(H1, [(G[:, :64], E), (G[:, 64:], E)], split=U)
+    g.spmm(K1, [(Q[:, :64],), (Q[:, 64:],)])
+    H2, K2 = torch.empty((N, 128), device=DEV), torch.empty((N, 128), device=DEV)
+    K.spmm_multi(g, [H2[:, :64], H2[:, 64:], K2[:, :64], K2[:, 64:]],
+                 [(G[:, :64], E), (G[:, 64:], E), (Q[:, :64], Q[U:, :64]), (Q[:, 64:], Q[U:, 64:])], split=U)
+    short = torch.as_tensor(np.diff(rp) <= 32, device=DEV)
+    assert torch.equal(H1[short].view(torch.int32), H2[short].view(torch.int32))
+    assert torch.equal(K1[short].view(torch.int32), K2[short].view(torch.int32))
+    np.testing.assert_allclose(H2.cpu().numpy(), H1.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(K2.cpu().numpy(), K1.cpu().numpy(), rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("seg", [128, LANE32, (1 << 16) | 128, PACKED32])
 def test_spmm_empty_runs_and_repeat(K, seg):
     """Long runs of empty rows, a tiny and an empty matrix,
