@@ -60,10 +60,13 @@ class Trainer:
         self.evaluator = TopKEvaluator(config)
         self.mg = mg
         self._loss_acc = torch.zeros(2, dtype=torch.float32, device=self.device)
-        # HIP-graph replay of the fixed-size BPR steps: opt-in (GMR_GRAPHS=1).  Measured on the baby
-        # shape it does not pay: the host keeps ahead of the GPU, and the graph is re-captured every
-        # epoch because the rebuilt UI adjacencies are new allocations (157.9 vs 155.5 ms/epoch).
-        self._use_graphs = os.environ.get("GMR_GRAPHS", "0") == "1" and hasattr(model, "graph_key")
+        # HIP-graph replay of the fixed-size BPR steps (GMR_GRAPHS=1) was measured not to pay on the
+        # baby shape (157.9 vs 155.5 ms/epoch: the graph is re-captured every epoch because the
+        # rebuilt UI adjacencies are new allocations).  Since the rec step forks side streams and
+        # allocates lazily sized workspaces, its capture crashes the process: refused here.
+        if os.environ.get("GMR_GRAPHS", "0") == "1":
+            raise NotImplementedError("GMR_GRAPHS=1: HIP-graph capture of the side-stream rec step is not supported")
+        self._use_graphs = False
         self._graph = None
 
     def _build_optimizer(self):
