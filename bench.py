@@ -48,8 +48,12 @@ def setup(args):
     from gmr.utils import get_model, get_trainer, init_seed
 
     name = MODELS[args.model]
-    cfg = Config(name, "tiktok" if args.shape == "tiktok" else "baby",
-                 {"synthetic": args.shape, "save_recommended_topk": False, "epochs": 1})
+    over = {"synthetic": args.shape, "save_recommended_topk": False, "epochs": 1}
+    if args.scoring_dtype:
+        if args.model != "genrecv1":
+            raise SystemExit("--scoring-dtype applies to GenRecV1 (config 5)")
+        over["scoring_dtype"] = args.scoring_dtype
+    cfg = Config(name, "tiktok" if args.shape == "tiktok" else "baby", over)
     init_seed(999)
     t0 = time.time()
     ds = make_dataset(cfg, args.shape, seed=0)
@@ -265,6 +269,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eval-passes", type=int, default=3)
     ap.add_argument("--no-probe", action="store_true", help="no HIP-event probes (A/B timing only)")
+    ap.add_argument("--scoring-dtype", default=None, choices=["fp32", "fp16"],
+                    help="GenRecV1 full-catalog scoring precision (config 5's fp16 MFMA scoring GEMM)")
     args = ap.parse_args()
     args.shape = args.shape or DEFAULT_SHAPE[args.model]
 
@@ -356,6 +362,7 @@ def main():
                        "global_batch": cfg["train_batch_size"], "eval_batch": cfg["eval_batch_size"],
                        "parallelism": f"dp{world}"},
             "eval_users_per_s": round(eval_ups, 1), "eval_recall@20": res.get("recall@20"),
+            "eval_scoring_dtype": getattr(model, "scoring_dtype", "fp32"),
             "roofline": roof, "roofline_by_kernel": probe_all, "dominant_kernel": dominant,
         }
         if world == 1 and not args.no_cpu_baseline:

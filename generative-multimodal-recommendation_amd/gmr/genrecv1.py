@@ -110,6 +110,9 @@ class GenRecV1(GeneralRecommender):
         self.keep_rate = float(c["keep_rate"])
         self.sparse_temp = float(c["sparse_temp"])
         self.temp = float(c["temperature"])
+        self.scoring_dtype = str(c["scoring_dtype"] if "scoring_dtype" in c else "fp32")
+        if self.scoring_dtype not in ("fp32", "fp16"):
+            raise ValueError(f"scoring_dtype {self.scoring_dtype!r}: fp32 or fp16")
         self.ssl_reg1, self.ssl_reg2 = float(c["ssl_reg1"]), float(c["ssl_reg2"])
         self.gen_topk, self.rebuild_k = int(c["gen_topk"]), int(c["rebuild_k"])
         self.d_emb_size, self.nhead, self.num_layers = int(c["d_emb_size"]), int(c["nhead"]), int(c["num_layers"])
@@ -499,8 +502,16 @@ class GenRecV1(GeneralRecommender):
         ub = torch.empty((user.numel(), 64), device=self.device)
         K.gather_rows(usr, user, ub)
         scores = torch.empty((user.numel(), self.n_items), device=self.device)
-        K.gemm(ub, itm, scores, trans_b=True)
+        self._score(ub, itm, scores)
         return scores
+
+    def _score(self, ub, itm, out):
+        """usr[users] @ itm^T (genrecv1.py:419-427): fp32 MFMA GEMM, or the opt-in fp16 MFMA one."""
+        if self.scoring_dtype == "fp16":
+            K.score_f16(ub, itm, out)
+        else:
+            K.gemm(ub, itm, out, trans_b=True)
+        return out
 
     @torch.no_grad()
     def topk_from_embeddings(self, usr, itm, users_i32, mask_rows, mask_cols, k, out_idx, scores_buf):
@@ -508,7 +519,7 @@ class GenRecV1(GeneralRecommender):
         ub = scores_buf.new_empty((E, 64))
         K.gather_rows(usr, users_i32, ub)
         sc = scores_buf[:E, :self.n_items]
-        K.gemm(ub, itm, sc, trans_b=True)
+        self._score(ub, itm, sc)
         K.mask_scores(sc, mask_rows, mask_cols)
         K.topk_rows(sc, k, out_idx)
         return out_idx

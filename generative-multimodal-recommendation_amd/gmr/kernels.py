@@ -214,6 +214,16 @@ class CSR:
         return out
 
 
+def score_f16(a, b, out):
+    """out = fp16(a) @ fp16(b)^T with fp32 accumulation (gmr_score_f16; a: E x 64, b: I x 64)."""
+    E, d = a.shape
+    n = b.shape[0]
+    if d != 64 or b.shape[1] != 64 or out.shape != (E, n):
+        raise ValueError("score_f16: a (E, 64), b (I, 64), out (E, I)")
+    _lib.call("gmr_score_f16", E, n, d, ptr(a), _ld(a), ptr(b), _ld(b), ptr(out), _ld(out), stream())
+    return out
+
+
 def spmm_multi(a, outs, blocks, split=None, alpha=1.0, beta=0.0):
     """One lane-plan launch for independent products of `a`: block b (64 columns, a (lo, hi) split
     source as in CSR.spmm) lands in outs[b] (an n_rows x 64 view).  gmr_spmm_multi_f32."""

@@ -101,6 +101,14 @@ int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val
                      const float* const* x_lo, const int64_t* ld_lo, const float* const* x_hi, const int64_t* ld_hi,
                      int64_t split, float alpha, float beta, float* y, int64_t ldy, int32_t flags, void* stream);
 
+/* ---------------------------------------------------------------- K9b fp16 scoring (opt-in)
+ * C (E x I, fp32) = fp16(A) (E x 64) . fp16(B)^T, fp32 accumulation on v_mfma_f32_32x32x16_f16;
+ * the fp16 MFMA scoring GEMM of BASELINE config 5, replacing the fp32 product of
+ * GenRecV1.full_sort_predict (models/genrecv1.py:419-427) when scoring_dtype = fp16.  A and B
+ * are fp32 and rounded on load.  d must be 64. */
+int gmr_score_f16(int64_t E, int64_t I, int64_t d, const float* A, int64_t lda, const float* B, int64_t ldb,
+                  float* C, int64_t ldc, void* stream);
+
 /* ---------------------------------------------------------------- K11 graph construction
  * Symmetric-normalised bipartite adjacency (N = U + I) in CSR from a user->items CSR
  * (items ascending and distinct per user).  Replaces DiffMM.get_norm_adj_mat

@@ -180,6 +180,19 @@ def test_rec_step_loss_grads_and_eval(G, M):
     model.eval()
     sc = model.full_sort_predict([_dev(m["eval_users"])])
     np.testing.assert_allclose(sc.cpu().numpy(), m["eval_scores"], rtol=1e-5, atol=1e-6)
+    # opt-in fp16 MFMA scoring (config 5): inputs rounded to fp16, fp32 accumulation.  Tolerance
+    # from the rounding: |err| <= 2^-10 * sum_k |u_k i_k| per score (parity unpinned: the
+    # reference has no fp16 path)
+    model.scoring_dtype = "fp16"
+    try:
+        s16 = model.full_sort_predict([_dev(m["eval_users"])]).cpu().numpy()
+    finally:
+        model.scoring_dtype = "fp32"
+    want = m["eval_scores"]
+    np.testing.assert_allclose(s16, want, rtol=0, atol=2e-3 * float(np.abs(want).max()) + 1e-6)
+    top16, top32 = np.argsort(-s16, 1)[:, :10], np.argsort(-want, 1)[:, :10]
+    overlap = np.mean([len(set(a) & set(b)) / 10 for a, b in zip(top16, top32)])
+    assert overlap >= 0.8, overlap
     C, S = model.forward(train=False)
     np.testing.assert_allclose(S.cpu().numpy(), m["eval_side"], rtol=1e-4, atol=1e-6)
     model.train()

@@ -189,6 +189,23 @@ def test_spmm_panel_sources_bit_exact(K, nb, seg):
         K.spmm_panel(g, Yb, Xp[:, :-1], nb)
 
 
+@pytest.mark.parametrize("E,I", [(300, 1000), (64, 64), (4096, 6710), (1, 7)])
+def test_score_f16_vs_torch(K, E, I):
+    """gmr_score_f16 (fp16 MFMA scoring, config 5) against torch on the same fp16-rounded inputs:
+    fp16 x fp16 products are exact in fp32, so only the summation order differs."""
+    rng = _rng(10)
+    A = torch.zeros((E, 68), device=DEV)[:, :64]  # padded rows: lda = 68
+    A.copy_(_dev(0.1 * rng.standard_normal((E, 64)).astype(np.float32)))
+    B = _dev(0.1 * rng.standard_normal((I, 64)).astype(np.float32))
+    C = torch.full((E, I + 5), 7.0, device=DEV)
+    K.score_f16(A, B, C[:, :I])
+    want = A.half().float() @ B.half().float().T
+    np.testing.assert_allclose(C[:, :I].cpu().numpy(), want.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    assert torch.all(C[:, I:] == 7.0)  # nothing written past the I columns
+    with pytest.raises(ValueError):
+        K.score_f16(A[:, :32], B[:, :32], C[:, :I])
+
+
 @pytest.mark.parametrize("seg", [LANE32, PACKED32])
 def test_spmm_multi_outputs_bit_exact(K, seg):
     """gmr_spmm_multi_f32: two independent 128-column products of one matrix in one launch, with
