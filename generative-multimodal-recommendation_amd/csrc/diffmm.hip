@@ -740,6 +740,15 @@ __device__ __forceinline__ void cl_frag(float4 (&fr)[2][4], const float* __restr
       fr[u][q] = row < n_rows ? ld4(src + (int64_t)row * ld + 32 * u + 16 * h + 4 * q) : f4(0.f, 0.f, 0.f, 0.f);
 }
 
+// exp(t x) on the transcendental unit: v_exp_f32 of x * (t log2 e) (relative error ~ |t x| 2^-24
+// from rounding the product, 6e-7 at |t x| <= 10) instead of the range-reduced expf (~14 VALU ops)
+template <bool FAST>
+__device__ __forceinline__ float cl_exp(float inv_t, float x) {
+  if (FAST) return __builtin_amdgcn_exp2f(x * (inv_t * 1.4426950408889634f));
+  return expf(inv_t * x);
+}
+
+template <bool FAST>
 __global__ void __launch_bounds__(256) cl_rows_kernel(int B, int n, const float* __restrict__ P, int64_t ldp,
                                                       const float* __restrict__ T, int64_t ldt, float inv_t, int chunk,
                                                       float* __restrict__ part_u, float* __restrict__ part_z) {
@@ -766,7 +775,7 @@ __global__ void __launch_bounds__(256) cl_rows_kernel(int B, int n, const float*
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int r = (e & 3) + 8 * (e >> 2) + 4 * h;
-      s[e] = j + r < j1 ? expf(inv_t * s[e]) : 0.f;
+      s[e] = j + r < j1 ? cl_exp<FAST>(inv_t, s[e]) : 0.f;
       z += s[e];
     }
     cl_acc(blk, s, y0, y1, l32, h);
@@ -808,6 +817,7 @@ __global__ void __launch_bounds__(256) cl_finalize_kernel(int B, int nc, const f
   }
 }
 
+template <bool FAST>
 __global__ void __launch_bounds__(256) cl_table_kernel(int B, int n, const float* __restrict__ P, int64_t ldp,
                                                        const float* __restrict__ r, const float* __restrict__ T,
                                                        int64_t ldt, float inv_t, int chunk, float* __restrict__ part_t) {
@@ -838,7 +848,7 @@ __global__ void __launch_bounds__(256) cl_table_kernel(int B, int n, const float
     const float* blk = s_blk[cur];
     clx16 s = cl_dot(blk, fr, l32, h);  // S' (rows i of the block x the wave's 32 table rows)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) s[e] = s_r[cur][(e & 3) + 8 * (e >> 2) + 4 * h] * expf(inv_t * s[e]);
+    for (int e = 0; e < 16; ++e) s[e] = s_r[cur][(e & 3) + 8 * (e >> 2) + 4 * h] * cl_exp<FAST>(inv_t, s[e]);
     cl_acc(blk, s, y0, y1, l32, h);  // dT^T += P_blk^T (r E)
     if (more) {
       cl_store(st, s_blk[cur ^ 1]);
@@ -909,14 +919,26 @@ extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int6
   float* r = part_z + (int64_t)p.nca * B;
   float* part_t = r + B;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(cl_rows_kernel, dim3((unsigned)((B + 127) / 128), (unsigned)p.nca), dim3(256), 0, st, B, (int)n,
-                     P, ldp, T, ldt, inv_temp, p.chunk_a, part_u, part_z);
+  static const bool fast = [] {  // v_exp_f32 (default; 8 % faster, scripts/contrast_bench.py); =0: expf
+    const char* e = getenv("GMR_CL_FASTEXP");
+    return !(e && atoi(e) == 0);
+  }();
+  if (fast)
+    hipLaunchKernelGGL(cl_rows_kernel<true>, dim3((unsigned)((B + 127) / 128), (unsigned)p.nca), dim3(256), 0, st, B,
+                       (int)n, P, ldp, T, ldt, inv_temp, p.chunk_a, part_u, part_z);
+  else
+    hipLaunchKernelGGL(cl_rows_kernel<false>, dim3((unsigned)((B + 127) / 128), (unsigned)p.nca), dim3(256), 0, st, B,
+                       (int)n, P, ldp, T, ldt, inv_temp, p.chunk_a, part_u, part_z);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(cl_finalize_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, p.nca, part_u, part_z, CLN,
                      nodes, node_off, inv_temp, coef, loss, contrib, ld_contrib, r);
   GMR_LAUNCHED();
-  hipLaunchKernelGGL(cl_table_kernel, dim3((unsigned)((n + 127) / 128), (unsigned)p.ncb), dim3(256), 0, st, B, (int)n,
-                     P, ldp, r, T, ldt, inv_temp, p.chunk_b, part_t);
+  if (fast)
+    hipLaunchKernelGGL(cl_table_kernel<true>, dim3((unsigned)((n + 127) / 128), (unsigned)p.ncb), dim3(256), 0, st, B,
+                       (int)n, P, ldp, r, T, ldt, inv_temp, p.chunk_b, part_t);
+  else
+    hipLaunchKernelGGL(cl_table_kernel<false>, dim3((unsigned)((n + 127) / 128), (unsigned)p.ncb), dim3(256), 0, st, B,
+                       (int)n, P, ldp, r, T, ldt, inv_temp, p.chunk_b, part_t);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(cl_table_reduce_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n, p.ncb, part_t,
                      dT, ld_dt);
