@@ -163,10 +163,18 @@ def check(rc, name="gmr"):
     return rc
 
 
+_fns = {}
+
+
 def call(name, *args):
     """Call an int-returning entry point and raise on a non-zero status (argument count checked:
     ctypes would silently pass surplus arguments to a C function)."""
-    fn = getattr(load(), name)
-    if len(args) != len(fn.argtypes):
-        raise TypeError(f"{name} takes {len(fn.argtypes)} arguments, got {len(args)}")
-    return check(fn(*args), name)
+    ent = _fns.get(name)
+    if ent is None:
+        fn = getattr(load(), name)
+        ent = _fns[name] = (fn, len(fn.argtypes))
+    fn, n = ent
+    if len(args) != n:
+        raise TypeError(f"{name} takes {n} arguments, got {len(args)}")
+    rc = fn(*args)
+    return rc if rc == 0 else check(rc, name)
