@@ -800,7 +800,21 @@ __global__ void __launch_bounds__(256) cl_finalize_kernel(int B, int nc, const f
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6), d = threadIdx.x & 63;
   if (i >= B) return;
   float u = 0.f, z = 0.f;
-  for (int c = 0; c < nc; ++c) {
+  int c = 0;
+  for (; c + 8 <= nc; c += 8) {  // eight chunk partials in flight, summed in chunk order
+    float uu[8], zz[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      uu[q] = part_u[((int64_t)(c + q) * B + i) * 64 + d];
+      zz[q] = part_z[(int64_t)(c + q) * B + i];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      u += uu[q];
+      z += zz[q];
+    }
+  }
+  for (; c < nc; ++c) {
     u += part_u[((int64_t)c * B + i) * 64 + d];
     z += part_z[(int64_t)c * B + i];
   }
@@ -867,7 +881,15 @@ __global__ void cl_table_reduce_kernel(int n, int nc, const float* __restrict__ 
   const int64_t j = g >> 4;
   const int c4 = (int)(g & 15) * 4;
   float4 s = ld4(part_t + j * 64 + c4);
-  for (int c = 1; c < nc; ++c) s = gmr::f4_add(s, ld4(part_t + ((int64_t)c * n + j) * 64 + c4));
+  int c = 1;
+  for (; c + 4 <= nc; c += 4) {  // four chunk partials in flight, summed in chunk order
+    float4 t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = ld4(part_t + ((int64_t)(c + q) * n + j) * 64 + c4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s = gmr::f4_add(s, t[q]);
+  }
+  for (; c < nc; ++c) s = gmr::f4_add(s, ld4(part_t + ((int64_t)c * n + j) * 64 + c4));
   st4(dT + j * ld + c4, s);
 }
 
