@@ -904,7 +904,7 @@ int cl_wg_target(const char* env, int dflt) {
 }
 // chunk the j (rows pass) and i (table pass) ranges for ~cl_wg_target workgroups each, in 32-row blocks
 ClPlan cl_plan(int64_t B, int64_t n) {
-  static const int wa = cl_wg_target("GMR_CL_WG_ROWS", 512), wb = cl_wg_target("GMR_CL_WG_TABLE", 1024);
+  static const int wa = cl_wg_target("GMR_CL_WG_ROWS", 512), wb = cl_wg_target("GMR_CL_WG_TABLE", 768);
   ClPlan p;
   const int64_t rb = (B + 127) / 128, tb = (n + 127) / 128;
   int64_t want = std::max<int64_t>(1, std::min<int64_t>((wa + rb - 1) / rb, (n + 31) / 32));
