@@ -171,10 +171,13 @@ class DiffMM(GeneralRecommender):
     def _project(self, w):
         """F = leaky_relu([v_feat @ image_trans | t_feat @ text_trans], 0.2); NF = row-normalised F."""
         s = self.rec_slab
+        st = self._streams
+        with st.on(1):  # the text projection runs beside the image one
+            K.gemm(self.t_feat, s.view("text_trans"), w["F"][:, 64:], epi=K.EPI_LEAKY, slope=0.2)
+            K.normalize_rows(w["F"][:, 64:], w["NF"][:, 64:], w["nrmF"][1])
         K.gemm(self.v_feat, s.view("image_trans"), w["F"][:, :64], epi=K.EPI_LEAKY, slope=0.2)
-        K.gemm(self.t_feat, s.view("text_trans"), w["F"][:, 64:], epi=K.EPI_LEAKY, slope=0.2)
         K.normalize_rows(w["F"][:, :64], w["NF"][:, :64], w["nrmF"][0])
-        K.normalize_rows(w["F"][:, 64:], w["NF"][:, 64:], w["nrmF"][1])
+        st.join(1)
 
     def _forward_mm(self, w, with_cl):
         U = self.n_users
@@ -264,25 +267,28 @@ class DiffMM(GeneralRecommender):
         _lib.call("gmr_sum_f32", B, ptr(w["loss_ci"]), self.ssl_reg / nr, ptr(loss), 1, stream())
         # --- backward
         dEmb, dCLN = w["dEmb"], w["dCLN"]
+        adj, iadj, tadj = self.norm_adj, self.image_UI_matrix, self.text_UI_matrix
+        dK = w["dCLN"]
+        # contrastive views (side stream 0, beside the BPR branch below): sparse terms into dCLN,
+        # dK = normalize backward (the +1e-8 shift has unit Jacobian), Tcl = adj^T dK
+        with st.on(0):
+            _lib.call("gmr_scatter_sorted_f32", plan_cl.numel(), 128, ptr(plan_cl), ptr(w["contrib_cl"]), 128,
+                      ptr(dCLN), 128, stream())
+            K.normalize_rows_bwd(w["CLN"][:, :64], w["nrmCL"][0], dCLN[:, :64], dK[:, :64])
+            K.normalize_rows_bwd(w["CLN"][:, 64:], w["nrmCL"][1], dCLN[:, 64:], dK[:, 64:])
+            adj.spmm(w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], partial=w["part_cl"])
         K.zero_(dEmb)
         _lib.call("gmr_scatter_sorted_f32", plan_bpr.numel(), 64, ptr(plan_bpr), ptr(w["contrib_bpr"]), 64,
                   ptr(dEmb), 64, stream())
-        _lib.call("gmr_scatter_sorted_f32", plan_cl.numel(), 128, ptr(plan_cl), ptr(w["contrib_cl"]), 128,
-                  ptr(dCLN), 128, stream())
-        adj, iadj, tadj = self.norm_adj, self.image_UI_matrix, self.text_UI_matrix
         s.zero_grad()
         adj.spmm(w["T1"], [(dEmb,)])                                            # adj^T dEmb (adj symmetric)
         _lib.call("gmr_dmm_final_bwd", N, ptr(dEmb), ptr(w["T1"]), ptr(w["M"]), ptr(w["nrmM"]), self.ris_lambda,
                   ptr(w["G"]), ptr(s.view("modal_weight")), ptr(w["dE"]), ptr(w["partials"]), stream())
         _lib.call("gmr_dmm_mw_grad", w["partials"].numel() // 2, ptr(w["partials"]), ptr(s.view("modal_weight")),
                   ptr(s.gview("modal_weight")), 0, stream())
-        # contrastive views: dK = normalize backward (the +1e-8 shift has unit Jacobian)
-        dK = w["dCLN"]
-        K.normalize_rows_bwd(w["CLN"][:, :64], w["nrmCL"][0], dCLN[:, :64], dK[:, :64])
-        K.normalize_rows_bwd(w["CLN"][:, 64:], w["nrmCL"][1], dCLN[:, 64:], dK[:, 64:])
-        # the contrastive branch (side stream 0) and the two-hop GCN branch (main) only meet in assemble
+        # the contrastive branch (side stream 0, now also after dE) and the two-hop GCN branch (main)
+        # only meet in assemble
         with st.on(0):
-            adj.spmm(w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], partial=w["part_cl"])
             _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
                       ptr(w["Rt"]), stream())
             with st.on(1):
@@ -295,12 +301,14 @@ class DiffMM(GeneralRecommender):
         st.join(0)
         _lib.call("gmr_dmm_assemble", N, U, ptr(w["T2"]), ptr(w["T3"]), ptr(w["OutI"]), ptr(w["OutT"]), ptr(E0),
                   2.0 * self.reg_weight * reg_share, ptr(s.gview("E0")), ptr(w["dNF"]), stream())
-        # modality projections: normalize + leaky-relu backward, then W grads
+        # modality projections: normalize + leaky-relu backward, then W grads (text beside image)
         dNF = w["dNF"]
+        with st.on(1):
+            K.normalize_rows_bwd(w["NF"][:, 64:], w["nrmF"][1], dNF[:, 64:], dNF[:, 64:], slope=0.2)
+            K.gemm(self.t_feat, dNF[:, 64:], s.gview("text_trans"), trans_a=True)
         K.normalize_rows_bwd(w["NF"][:, :64], w["nrmF"][0], dNF[:, :64], dNF[:, :64], slope=0.2)
-        K.normalize_rows_bwd(w["NF"][:, 64:], w["nrmF"][1], dNF[:, 64:], dNF[:, 64:], slope=0.2)
         K.gemm(self.v_feat, dNF[:, :64], s.gview("image_trans"), trans_a=True)
-        K.gemm(self.t_feat, dNF[:, 64:], s.gview("text_trans"), trans_a=True)
+        st.join(1)
         self._step += 1
         return loss[0]
 
