@@ -411,28 +411,33 @@ class DiffMM(GeneralRecommender):
         return out_idx
 
     # ================================================================= diffusion
-    def _dwork(self, B):
-        if self._dw is not None and self._dw["B"] >= B:
-            return self._dw
+    def _dwork(self, B, slot=0):
+        """Diffusion-step buffers; one set per slot, so the two denoisers can step concurrently."""
+        if self._dw is None:
+            self._dw = {}
+        cur = self._dw.get(slot)
+        if cur is not None and cur["B"] >= B:
+            return cur
         I, dev = self.n_items, self.device
         H = self.denoise_model_image.H
         Ip = (I + 3) // 4 * 4
         f = lambda *s, dt=torch.float32: torch.empty(s, dtype=dt, device=dev)  # noqa: E731
-        self._dw = {"B": B, "x": f(B, Ip), "h": f(B, H), "out": f(B, Ip), "dpre": f(B, H), "Z": f(B, 64),
-                    "Gc": f(B, 64), "S": f(self.steps, H), "t": f(B, dt=torch.int32),
-                    "mse": f(B, dt=torch.float64), "diff": f(B, dt=torch.float64), "gc": f(B, dt=torch.float64),
-                    "users": torch.arange(self.n_users, dtype=torch.int32, device=dev)}
-        return self._dw
+        self._dw[slot] = {"B": B, "x": f(B, Ip), "h": f(B, H), "out": f(B, Ip), "dpre": f(B, H), "Z": f(B, 64),
+                          "Gc": f(B, 64), "S": f(self.steps, H), "t": f(B, dt=torch.int32),
+                          "mse": f(B, dt=torch.float64), "diff": f(B, dt=torch.float64),
+                          "gc": f(B, dt=torch.float64),
+                          "users": torch.arange(self.n_users, dtype=torch.int32, device=dev)}
+        return self._dw[slot]
 
     def diffusion_step(self, den, batch_users, feats, item_embeds, step, noise=None, keep=None, t=None,
-                       norm_rows=None):
+                       norm_rows=None, slot=0):
         """One GaussianDiffusion.training_losses + backward for one denoiser (diffmm.py:453-477).
 
         Writes the denoiser's gradients into its slab; returns (diff_loss, gc_loss) per-row
         fp64 views.  noise/keep/t may be supplied (parity tests); else drawn by Philox."""
         B = batch_users.numel()
         nr = float(norm_rows or B)
-        w = self._dwork(B)
+        w = self._dwork(B, slot)
         I, T = self.n_items, self.steps
         x, h, out, Z = w["x"][:B], w["h"][:B], w["out"][:B], w["Z"][:B]
         tt = w["t"][:B]

@@ -282,6 +282,7 @@ class DiffMMTrainer(Trainer):
         K.zero_(self._dloss)
         dens = ((m.denoise_model_image, feats_i), (m.denoise_model_text, feats_t))
         opts = (self.denoise_opt_image, self.denoise_opt_text)
+        st = m._streams
         steps = 0
         for g, lo in enumerate(range(0, U, B * W)):
             hi = min(U, lo + B * W)
@@ -289,17 +290,25 @@ class DiffMMTrainer(Trainer):
             users = self._perm[lo + a:lo + b]
             nb = users.numel()
             base = ((self._epoch_ctr * 100000 + g) * W + r) * 2
-            pending = []
-            for j, (den, feats) in enumerate(dens):
+            # the two denoisers are independent until their Adam steps: the text one runs on a side
+            # stream (own work buffers, slot 1) beside the image one; under DP the image gradient
+            # exchange starts as soon as its step is issued (one bucket per slab)
+            def one(j):
+                den, feats = dens[j]
                 if nb > 0:
-                    diff, gc = m.diffusion_step(den, users, feats, iE, base + j, norm_rows=hi - lo)
+                    diff, gc = m.diffusion_step(den, users, feats, iE, base + j, norm_rows=hi - lo, slot=j)
                     _lib.call("gmr_sum_f64", nb, ptr(diff), 1.0 / (hi - lo), ptr(self._dloss[j:j + 1]), 1, stream())
                     _lib.call("gmr_sum_f64", nb, ptr(gc), m.e_loss / (hi - lo), ptr(self._dloss[j:j + 1]), 1,
                               stream())
                 else:
                     den.slab.zero_grad()
-                # the image gradient exchange runs while the text denoiser steps (one bucket each)
-                pending.append(dist.all_reduce_start(den.slab.grad) if W > 1 else None)
+
+            with st.on(1):
+                one(1)
+            one(0)
+            pending = [dist.all_reduce_start(dens[0][0].slab.grad) if W > 1 else None]
+            st.join(1)
+            pending.append(dist.all_reduce_start(dens[1][0].slab.grad) if W > 1 else None)
             for h, opt in zip(pending, opts):
                 dist.wait(h)
                 opt.step()
