@@ -466,10 +466,10 @@ class DiffMM(GeneralRecommender):
         return w["diff"][:B], w["gc"][:B]
 
     @torch.no_grad()
-    def p_sample_topk(self, den, users_lo, users_hi, out_topk, k, x_out=None, w1t_fresh=False):
+    def p_sample_topk(self, den, users_lo, users_hi, out_topk, k, x_out=None, w1t_fresh=False, slot=0):
         """p_sample(x0, steps=0, no noise) for users [lo, hi) + per-row top-k (trainer.py:545-546)."""
         B = users_hi - users_lo
-        w = self._dwork(min(B, 8192))
+        w = self._dwork(min(B, 8192), slot)
         I, T = self.n_items, self.steps
         assert B <= w["B"]
         x, h = w["x"][:B], w["h"][:B]
@@ -500,14 +500,25 @@ class DiffMM(GeneralRecommender):
         dev = self.device
         lo_r, hi_r, size = dist.padded_shard(U)
         W = dist.world()
-        topk = torch.zeros((W * size, k), dtype=torch.int32, device=dev)
+        topks = [torch.zeros((W * size, k), dtype=torch.int32, device=dev) for _ in range(2)]
         uptr = torch.empty(U + 1, dtype=torch.int32, device=dev)
         uitems = torch.empty(U * k, dtype=torch.int32, device=dev)
         graphs = []
-        for den in (self.denoise_model_image, self.denoise_model_text):
-            den.refresh_w1t()
+        dens = (self.denoise_model_image, self.denoise_model_text)
+
+        def sample(j):
+            dens[j].refresh_w1t()
             for lo in range(lo_r, hi_r, chunk):
-                self.p_sample_topk(den, lo, min(hi_r, lo + chunk), topk, k, w1t_fresh=True)
+                self.p_sample_topk(dens[j], lo, min(hi_r, lo + chunk), topks[j], k, w1t_fresh=True, slot=j)
+
+        # the two p_sample sweeps are independent: text on a side stream beside image (own buffers);
+        # the graph builds (one host sync each, for the SpMM plan header) follow on the main stream
+        st = self._streams
+        with st.on(1):
+            sample(1)
+        sample(0)
+        st.join(1)
+        for topk in topks:
             dist.all_gather_rows_(topk, size)
             K.topk_to_user_csr(topk[:U], uptr, uitems)
             g = K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0)
