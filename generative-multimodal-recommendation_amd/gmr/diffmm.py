@@ -179,7 +179,7 @@ class DiffMM(GeneralRecommender):
         K.normalize_rows(w["F"][:, :64], w["NF"][:, :64], w["nrmF"][0])
         st.join(1)
 
-    def _forward_mm(self, w, with_cl):
+    def _forward_mm(self, w, with_cl, on_cl=None):
         U = self.n_users
         E0 = self.rec_slab.view("E0")
         iE = E0[U:]
@@ -203,6 +203,12 @@ class DiffMM(GeneralRecommender):
             K.spmm_multi(adj, [H[:, :64], H[:, 64:], K2[:, :64], K2[:, 64:]],
                          [(G[:, :64], iE), (G[:, 64:], iE), (Qi[:, 64:], Qi[U:, 64:]), (Qt[:, 64:], Qt[U:, 64:])],
                          split=U)
+            # CLN = normalize([C + K2] + 1e-8)   (diffmm.py:171-195, 252-253): ready now, so the
+            # contrastive terms (on_cl, side streams) overlap the rest of forward_MM below
+            _lib.call("gmr_dmm_cl_fwd", self.N, ptr(Qi), ptr(Qt), ptr(w["K2"]), ptr(w["CLN"]), ptr(w["nrmCL"]),
+                      stream())
+            if on_cl is not None:
+                on_cl()
         else:
             adj.spmm(H, [(G[:, :64], iE), (G[:, 64:], iE)], split=U)
         # E = G + H + ris_adj * [IA | TA] (over G);  M = w0 E_img + w1 E_txt  (:155-158)
@@ -211,10 +217,6 @@ class DiffMM(GeneralRecommender):
         adj.spmm(w["L"], [(w["M"],)])                                  # one GCN layer (:160-165)
         _lib.call("gmr_dmm_final_fwd", self.N, ptr(w["M"]), ptr(w["L"]), self.ris_lambda, ptr(w["Emb"]),
                   ptr(w["nrmM"]), stream())                             # + ris * normalize(M) (:167)
-        if with_cl:
-            # CLN = normalize([C + K2] + 1e-8)   (diffmm.py:171-195, 252-253; K2 computed with H above)
-            _lib.call("gmr_dmm_cl_fwd", self.N, ptr(Qi), ptr(Qt), ptr(w["K2"]), ptr(w["CLN"]), ptr(w["nrmCL"]),
-                      stream())
         return w["Emb"]
 
     # ================================================================= fused rec step
@@ -249,13 +251,17 @@ class DiffMM(GeneralRecommender):
         if plan_bpr is None:
             plan_bpr, plan_cl = self._plans(users, pos, neg)
         st = self._streams
-        self._forward_mm(w, with_cl=True)
-        K.zero_(w["dCLN"])  # [:, 64:] is then overwritten by the d-table GEMMs, [:, :64] by scatters
-        # --- losses and their sparse gradient contributions (the two InfoNCE terms run side by side)
-        with st.on(0):
-            self._contrast(w, users, 0, U, 0, w["loss_cu"], B, nr, slot="u")
-        with st.on(1):
-            self._contrast(w, pos, U, I, B, w["loss_ci"], B, nr, slot="i")
+
+        def contrast():
+            K.zero_(w["dCLN"])  # [:, 64:] is then overwritten by the d-table GEMMs, [:, :64] by scatters
+            # the two InfoNCE terms run side by side, beside the GCN layer of forward_MM
+            with st.on(0):
+                self._contrast(w, users, 0, U, 0, w["loss_cu"], B, nr, slot="u")
+            with st.on(1):
+                self._contrast(w, pos, U, I, B, w["loss_ci"], B, nr, slot="i")
+
+        self._forward_mm(w, with_cl=True, on_cl=contrast)
+        # --- losses and their sparse gradient contributions
         _lib.call("gmr_bpr_fwd_bwd", B, U, ptr(w["Emb"]), ptr(users), ptr(pos), ptr(neg), ptr(w["loss_bpr"]),
                   ptr(w["contrib_bpr"]), 1.0 / nr, stream())
         loss = w["loss"][:1]
