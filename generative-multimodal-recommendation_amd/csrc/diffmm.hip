@@ -627,6 +627,61 @@ extern "C" int gmr_sqnorm_f32(int64_t n, const float* x, float scale, float* out
   return GMR_OK;
 }
 
+// parts-only squared norm (the ordered final sum is done by gmr_dmm_loss_total)
+extern "C" int64_t gmr_sqnorm_nparts(int64_t n) { return gmr::grid_for(n, 256 * 8, GMR_SQNORM_PARTS); }
+
+extern "C" int gmr_sqnorm_part_f32(int64_t n, const float* x, double* workspace, void* stream) {
+  GMR_ARG(x && workspace && n >= 0, "bad args");
+  const int g = gmr::grid_for(n, 256 * 8, GMR_SQNORM_PARTS);
+  hipLaunchKernelGGL(sqnorm_part_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, n, x, workspace);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+namespace {
+// the block-wide fp64 sum of sum_kernel / sqnorm_fin_kernel, as a device function (same order)
+template <typename T>
+__device__ double block_sum_d(int64_t n, const T* __restrict__ x, double* red) {
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) s += (double)x[i];
+  s = gmr::wave_sum_d(s);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// loss = sum(bpr)/nr + reg * |E0|^2 + ssl/nr * (sum(cu) + sum(ci)), in the order of the four
+// separate reductions it replaces (sum, sqnorm fin, sum, sum): the same float value
+__global__ void __launch_bounds__(256) loss_total_kernel(int64_t B, const float* __restrict__ bpr, float inv_nr,
+                                                         const double* __restrict__ parts, int nparts, float reg,
+                                                         const float* __restrict__ cu, const float* __restrict__ ci,
+                                                         float ssl, float* __restrict__ out) {
+  __shared__ double red[4];
+  const double a = block_sum_d(B, bpr, red);
+  const double b = block_sum_d((int64_t)nparts, parts, red);
+  const double c = block_sum_d(B, cu, red);
+  const double d = block_sum_d(B, ci, red);
+  if (threadIdx.x == 0) {
+    float v = (float)(a * (double)inv_nr);
+    v = v + (float)(b * (double)reg);
+    v = v + (float)(c * (double)ssl);
+    v = v + (float)(d * (double)ssl);
+    out[0] = v;
+  }
+}
+}  // namespace
+
+extern "C" int gmr_dmm_loss_total(int64_t B, const float* loss_bpr, float inv_nr, const double* parts, int64_t nparts,
+                                  float reg_scale, const float* loss_cu, const float* loss_ci, float ssl_scale,
+                                  float* out, void* stream) {
+  GMR_ARG(loss_bpr && parts && loss_cu && loss_ci && out && B > 0 && nparts > 0 && nparts < (1 << 30), "bad args");
+  hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, loss_bpr, inv_nr, parts,
+                     (int)nparts, reg_scale, loss_cu, loss_ci, ssl_scale, out);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
 extern "C" int gmr_sort_batch_keys(int64_t n_batches, const int32_t* keys, const int64_t* offsets,
                                    const int32_t* key_add, int32_t n_keysets, int64_t key_stride, uint64_t* out,
                                    int64_t out_stride, int32_t pow2, void* stream) {

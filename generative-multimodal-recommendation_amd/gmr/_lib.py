@@ -24,6 +24,7 @@ SIGNATURES = {
     "gmr_device_name": (I32, [P, I32]),
     "gmr_zero": (I32, [P, I64, P]),
     "gmr_spmm_plan_words": (I64, [I64, I64, I32]),
+    "gmr_sqnorm_nparts": (I64, [I64]),
     "gmr_spmm_partial_rows": (I64, [I64, I64, I32]),
     "gmr_spmm_plan_build": (I32, [P, I64, I64, I32, P, P]),
     "gmr_spmm_plan_pack": (I32, [P, P, I64, I64, I32, P, P]),
@@ -60,6 +61,8 @@ SIGNATURES = {
     "gmr_sort_batch_keys": (I32, [I64, P, P, P, I32, I64, P, I64, I32, P]),
     "gmr_sum_f32": (I32, [I64, P, F32, P, I32, P]),
     "gmr_sqnorm_f32": (I32, [I64, P, F32, P, I32, P, P]),
+    "gmr_sqnorm_part_f32": (I32, [I64, P, P, P]),
+    "gmr_dmm_loss_total": (I32, [I64, P, F32, P, I64, F32, P, P, F32, P, P]),
     "gmr_sum_f64": (I32, [I64, P, F64, P, I32, P]),
     "gmr_colsum_f32": (I32, [I64, I64, P, I64, P, I32, P, I32, P]),
     "gmr_sample_epoch": (I32, [I64, P, P, P, P, P, I64, U64, U64, P, P, P, P]),

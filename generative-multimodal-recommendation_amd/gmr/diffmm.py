@@ -144,6 +144,7 @@ class DiffMM(GeneralRecommender):
         self._dw = None
         self._step = 0
         self._streams = K.Streams(2)
+        self._sq_parts = int(_lib.load().gmr_sqnorm_nparts(self.N * 64))
 
     # ================================================================= buffers
     def _work(self, B):
@@ -265,12 +266,12 @@ class DiffMM(GeneralRecommender):
         _lib.call("gmr_bpr_fwd_bwd", B, U, ptr(w["Emb"]), ptr(users), ptr(pos), ptr(neg), ptr(w["loss_bpr"]),
                   ptr(w["contrib_bpr"]), 1.0 / nr, stream())
         loss = w["loss"][:1]
-        _lib.call("gmr_sum_f32", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(loss), 0, stream())
-        _lib.call("gmr_sqnorm_f32", N * 64, ptr(E0), self.reg_weight * reg_share, ptr(loss), 1, ptr(w["sqws"]),
-                  stream())
+        _lib.call("gmr_sqnorm_part_f32", N * 64, ptr(E0), ptr(w["sqws"]), stream())
         st.join(0, 1)
-        _lib.call("gmr_sum_f32", B, ptr(w["loss_cu"]), self.ssl_reg / nr, ptr(loss), 1, stream())
-        _lib.call("gmr_sum_f32", B, ptr(w["loss_ci"]), self.ssl_reg / nr, ptr(loss), 1, stream())
+        # BPR mean + regulariser + both InfoNCE means in one ordered reduction (calculate_loss, :243-249)
+        _lib.call("gmr_dmm_loss_total", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(w["sqws"]), self._sq_parts,
+                  self.reg_weight * reg_share, ptr(w["loss_cu"]), ptr(w["loss_ci"]), self.ssl_reg / nr, ptr(loss),
+                  stream())
         # --- backward
         dEmb, dCLN = w["dEmb"], w["dCLN"]
         adj, iadj, tadj = self.norm_adj, self.image_UI_matrix, self.text_UI_matrix

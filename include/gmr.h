@@ -204,6 +204,15 @@ int gmr_sum_f32(int64_t n, const float* x, float scale, float* out, int32_t accu
 #define GMR_SQNORM_PARTS 1024 /* workspace doubles of gmr_sqnorm_f32 */
 int gmr_sqnorm_f32(int64_t n, const float* x, float scale, float* out, int32_t accumulate, double* workspace,
                    void* stream);
+/* The same as two steps: per-block fp64 partials (gmr_sqnorm_nparts(n) of them) into workspace,
+ * then gmr_dmm_loss_total sums them in order with the other loss terms of DiffMM.calculate_loss
+ * (models/diffmm.py:203-249): out = sum(bpr)*inv_nr + reg*|x|^2 + ssl*(sum(cu) + sum(ci)), one
+ * launch and the same float value as the four separate reductions. */
+int64_t gmr_sqnorm_nparts(int64_t n);
+int gmr_sqnorm_part_f32(int64_t n, const float* x, double* workspace, void* stream);
+int gmr_dmm_loss_total(int64_t B, const float* loss_bpr, float inv_nr, const double* parts, int64_t nparts,
+                       float reg_scale, const float* loss_cu, const float* loss_ci, float ssl_scale, float* out,
+                       void* stream);
 int gmr_sum_f64(int64_t n, const double* x, double scale, double* out, int32_t accumulate, void* stream);
 int gmr_colsum_f32(int64_t rows, int64_t cols, const float* x, int64_t ld, const int32_t* group, int32_t n_groups,
                    float* out, int32_t accumulate, void* stream);
