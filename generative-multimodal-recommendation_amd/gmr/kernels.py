@@ -113,7 +113,8 @@ def _ld(t):
 def workspace(nfloats, device, tag="gemm"):
     """Cached scratch per (tag, device, stream): kernels running concurrently on different
     streams never share one."""
-    key = (tag, device, torch.cuda.current_stream().cuda_stream)
+    key = (tag, device, _raw_stream(_cur_device()) if _raw_stream is not None and _cur_device is not None
+           else torch.cuda.current_stream().cuda_stream)
     w = _ws.get(key)
     if w is None or w.numel() < nfloats:
         w = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
