@@ -29,3 +29,29 @@ extern "C" int gmr_device_name(char* buf, int32_t len) {
   snprintf(buf, (size_t)len, "%s", p.gcnArchName);
   return GMR_OK;
 }
+
+// Stream fork/join for the host layer: record `ev` on `from`, make `to` wait for it.  The
+// DiffMM rec step forks and joins side streams ~17 times per step; doing it here costs one
+// ctypes call instead of torch Stream/Event objects, and the step is host-issue-bound.
+extern "C" int gmr_event_create(void** ev) {
+  if (!ev) {
+    gmr::set_error(__func__, "null pointer");
+    return GMR_ERR_ARG;
+  }
+  hipEvent_t e = nullptr;
+  const hipError_t rc = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  if (rc != hipSuccess) return gmr::hip_status(__func__, rc);
+  *ev = (void*)e;
+  return GMR_OK;
+}
+
+extern "C" int gmr_stream_fork(void* from, void* to, void* ev) {
+  if (!ev) {
+    gmr::set_error(__func__, "null event");
+    return GMR_ERR_ARG;
+  }
+  hipError_t rc = hipEventRecord((hipEvent_t)ev, (hipStream_t)from);
+  if (rc == hipSuccess) rc = hipStreamWaitEvent((hipStream_t)to, (hipEvent_t)ev, 0);
+  if (rc != hipSuccess) return gmr::hip_status(__func__, rc);
+  return GMR_OK;
+}

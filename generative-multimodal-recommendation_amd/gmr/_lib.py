@@ -29,6 +29,8 @@ SIGNATURES = {
     "gmr_spmm_plan_build": (I32, [P, I64, I64, I32, P, P]),
     "gmr_spmm_plan_pack": (I32, [P, P, I64, I64, I32, P, P]),
     "gmr_spmm_plan_info": (I32, [P, P, P]),
+    "gmr_event_create": (I32, [P]),
+    "gmr_stream_fork": (I32, [P, P, P]),
     "gmr_score_f16": (I32, [I64, I64, I64, P, I64, P, I64, P, I64, P]),
     "gmr_spmm_multi_f32": (I32, [P, P, I64, I64, P, I32, I32, P, P, P, P, I64, F32, F32, P, P, P]),
     "gmr_spmm_panel_f32": (I32, [P, P, I64, I64, P, I32, I32, P, I64, F32, F32, P, I64, P]),

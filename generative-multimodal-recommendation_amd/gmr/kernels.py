@@ -72,26 +72,51 @@ def stream():
 
 
 class Streams:
-    """Fork/join helper over a few side streams (events preallocated): work issued inside
-    `with st.on(i):` runs on side stream i after everything already issued on the main stream;
-    st.join(i) makes the main stream wait for it."""
+    """Fork/join helper over a few side streams: work issued inside `with st.on(i):` runs on side
+    stream i after everything already issued on the current stream; st.join(i) makes the current
+    stream wait for it.  The fork/join is one C-ABI call on raw stream handles (gmr_stream_fork)
+    and the current stream is switched with torch's raw setter: the DiffMM rec step forks ~17
+    times per step and is host-issue-bound, so torch Stream/Event objects are kept off this path."""
 
     def __init__(self, n):
         self.side = [torch.cuda.Stream() for _ in range(n)]
-        self.fork_ev = [torch.cuda.Event() for _ in range(n)]
-        self.join_ev = [torch.cuda.Event() for _ in range(n)]
+        self._raw = [ctypes.c_void_p(s.cuda_stream) for s in self.side]
+        self._ids = [(s.stream_id, s.device_index, s.device_type) for s in self.side]
+        self._dev = torch.cuda.current_device()
+        lib = _lib.load()
+        self._ev = []
+        for _ in range(2 * n):
+            e = ctypes.c_void_p()
+            _lib.check(lib.gmr_event_create(ctypes.cast(ctypes.pointer(e), ctypes.c_void_p)), "gmr_event_create")
+            self._ev.append(e)
 
     def on(self, i):
-        main = torch.cuda.current_stream()
-        self.fork_ev[i].record(main)
-        self.side[i].wait_event(self.fork_ev[i])
-        return torch.cuda.stream(self.side[i])
+        return _OnSide(self, i)
 
     def join(self, *idx):
-        main = torch.cuda.current_stream()
+        cur = stream()
         for i in idx:
-            self.join_ev[i].record(self.side[i])
-            main.wait_event(self.join_ev[i])
+            _lib.call("gmr_stream_fork", self._raw[i], cur, self._ev[2 * i + 1])
+
+
+class _OnSide:
+    __slots__ = ("st", "i", "prev")
+
+    def __init__(self, st, i):
+        self.st, self.i = st, i
+
+    def __enter__(self):
+        st, i = self.st, self.i
+        self.prev = torch._C._cuda_getCurrentStream(st._dev)
+        _lib.call("gmr_stream_fork", stream(), st._raw[i], st._ev[2 * i])
+        sid, dev, dt = st._ids[i]
+        torch._C._cuda_setStream(stream_id=sid, device_index=dev, device_type=dt)
+        return st.side[i]
+
+    def __exit__(self, *a):
+        sid, dev, dt = self.prev
+        torch._C._cuda_setStream(stream_id=sid, device_index=dev, device_type=dt)
+        return False
 
 
 def ptr(t):

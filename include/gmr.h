@@ -44,6 +44,9 @@ const char* gmr_last_error_string(void);
 int gmr_version(void);
 int gmr_device_name(char* buf /* host */, int32_t len);
 int gmr_zero(void* ptr, int64_t bytes, void* stream);
+/* host-layer stream plumbing: an event (timing disabled) and "record ev on from, make to wait" */
+int gmr_event_create(void** ev /* host */);
+int gmr_stream_fork(void* from, void* to, void* ev);
 
 /* ---------------------------------------------------------------- K1 graph convolution
  * Y = alpha * A * X + beta * Y for CSR A (int32 rowptr/col, fp32 val).
