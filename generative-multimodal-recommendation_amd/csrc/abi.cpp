@@ -45,6 +45,13 @@ extern "C" int gmr_event_create(void** ev) {
   return GMR_OK;
 }
 
+extern "C" int gmr_event_destroy(void* ev) {
+  if (!ev) return GMR_OK;
+  const hipError_t rc = hipEventDestroy((hipEvent_t)ev);
+  if (rc != hipSuccess) return gmr::hip_status(__func__, rc);
+  return GMR_OK;
+}
+
 extern "C" int gmr_stream_fork(void* from, void* to, void* ev) {
   if (!ev) {
     gmr::set_error(__func__, "null event");

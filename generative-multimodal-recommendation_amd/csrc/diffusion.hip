@@ -47,10 +47,10 @@ __device__ __forceinline__ Draw4 draw4(uint64_t seed, uint64_t step, int64_t b, 
   return d;
 }
 
-__global__ void sample_t_kernel(int B, int T, uint64_t seed, uint64_t step, int* __restrict__ t) {
+__global__ void sample_t_kernel(int B, int T, uint64_t seed, uint64_t step, int64_t row0, int* __restrict__ t) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  uint4 r = gmr::Philox::gen(seed ^ 0xA5A5A5A5ull, step, (uint64_t)b);
+  uint4 r = gmr::Philox::gen(seed ^ 0xA5A5A5A5ull, step, (uint64_t)(row0 + b));
   t[b] = (int)(((uint64_t)r.x * (uint64_t)T) >> 32);
 }
 
@@ -58,7 +58,7 @@ __global__ void sample_t_kernel(int B, int T, uint64_t seed, uint64_t step, int*
 __global__ void qsample_dense_kernel(int B, int I, const int* __restrict__ t, const float* __restrict__ sa,
                                      const float* __restrict__ s1, const float* __restrict__ noise, int64_t ld_noise,
                                      const float* __restrict__ keep, int64_t ld_keep, float keep_prob, int dropout,
-                                     uint64_t seed, uint64_t step, float* __restrict__ x, int64_t ldx) {
+                                     uint64_t seed, uint64_t step, int64_t row0, float* __restrict__ x, int64_t ldx) {
   const int64_t c4n = (I + 3) / 4;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)B * c4n) return;
@@ -66,7 +66,7 @@ __global__ void qsample_dense_kernel(int B, int I, const int* __restrict__ t, co
   const int tb = t[b];
   const float s1v = s1[tb];
   Draw4 d;
-  if (!noise || (dropout && !keep)) d = draw4(seed, step, b, c4, keep_prob);
+  if (!noise || (dropout && !keep)) d = draw4(seed, step, row0 + b, c4, keep_prob);
   const float kscale = 1.f / keep_prob;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -84,7 +84,7 @@ __global__ void qsample_sparse_kernel(int B, const int* __restrict__ users, cons
                                       const float* __restrict__ sa, const float* __restrict__ s1,
                                       const float* __restrict__ noise, int64_t ld_noise, const float* __restrict__ keep,
                                       int64_t ld_keep, float keep_prob, int dropout, uint64_t seed, uint64_t step,
-                                      float* __restrict__ x, int64_t ldx) {
+                                      int64_t row0, float* __restrict__ x, int64_t ldx) {
   const int b = blockIdx.x;
   if (b >= B) return;
   const int u = users[b];
@@ -95,7 +95,7 @@ __global__ void qsample_sparse_kernel(int B, const int* __restrict__ users, cons
     const int64_t c = uitems[e];
     const int64_t c4 = c >> 2;
     Draw4 d;
-    if (!noise || (dropout && !keep)) d = draw4(seed, step, b, c4, keep_prob);
+    if (!noise || (dropout && !keep)) d = draw4(seed, step, row0 + b, c4, keep_prob);
     const float eps = noise ? noise[b * ld_noise + c] : d.eps[c & 3];
     float v = sav * 1.0f + s1v * eps;
     if (dropout) v = v * ((keep ? keep[b * ld_keep + c] : d.keep[c & 3]) * kscale);
@@ -345,15 +345,15 @@ __global__ void __launch_bounds__(1024) time_bwd_e_kernel(int T, int E, int H, c
 // One 1024-thread block; T <= 1024.
 __global__ void __launch_bounds__(1024) sample_t_importance_kernel(int B, int T, int Hn, const double* __restrict__ hist,
                                                                   const int* __restrict__ count, double uniform_prob,
-                                                                  uint64_t seed, uint64_t step, int* __restrict__ t,
-                                                                  float* __restrict__ pt) {
+                                                                  uint64_t seed, uint64_t step, int64_t row0,
+                                                                  int* __restrict__ t, float* __restrict__ pt) {
   __shared__ double cdf[1024];
   __shared__ double pall[1024];
   const int i = threadIdx.x;
   const int full = __syncthreads_and(i >= T || count[i] == Hn);
   if (!full) {
     for (int b = i; b < B; b += 1024) {
-      uint4 r = gmr::Philox::gen(seed ^ 0xA5A5A5A5ull, step, (uint64_t)b);
+      uint4 r = gmr::Philox::gen(seed ^ 0xA5A5A5A5ull, step, (uint64_t)(row0 + b));
       t[b] = (int)(((uint64_t)r.x * (uint64_t)T) >> 32);
       pt[b] = 1.f;
     }
@@ -377,7 +377,7 @@ __global__ void __launch_bounds__(1024) sample_t_importance_kernel(int B, int T,
   }
   __syncthreads();
   for (int b = i; b < B; b += 1024) {
-    uint4 r = gmr::Philox::gen(seed ^ 0x5EED5EEDull, step, (uint64_t)b);
+    uint4 r = gmr::Philox::gen(seed ^ 0x5EED5EEDull, step, (uint64_t)(row0 + b));
     const double u = (((uint64_t)r.x << 21) ^ (uint64_t)(r.y >> 11)) * (1.0 / 9007199254740992.0) * cdf[T - 1];
     int lo = 0, hi = T - 1;  // first j with cdf[j] > u
     while (lo < hi) {
@@ -469,20 +469,22 @@ __global__ void __launch_bounds__(256) sparse_hidden_kernel(int B, int H, const 
 
 }  // namespace
 
-extern "C" int gmr_diff_sample_t(int32_t B, int32_t T, uint64_t seed, uint64_t step, int32_t* t, void* stream) {
-  GMR_ARG(t && B > 0 && T > 0, "bad args");
-  hipLaunchKernelGGL(sample_t_kernel, dim3(gmr::grid_for(B, 256)), dim3(256), 0, (hipStream_t)stream, B, T, seed, step, t);
+extern "C" int gmr_diff_sample_t(int32_t B, int32_t T, uint64_t seed, uint64_t step, int64_t row0, int32_t* t,
+                                 void* stream) {
+  GMR_ARG(t && B > 0 && T > 0 && row0 >= 0, "bad args");
+  hipLaunchKernelGGL(sample_t_kernel, dim3(gmr::grid_for(B, 256)), dim3(256), 0, (hipStream_t)stream, B, T, seed, step,
+                     row0, t);
   GMR_LAUNCHED();
   return GMR_OK;
 }
 
 extern "C" int gmr_diff_sample_t_importance(int32_t B, int32_t T, int32_t hist_len, const double* hist,
                                             const int32_t* count, double uniform_prob, uint64_t seed, uint64_t step,
-                                            int32_t* t, float* pt, void* stream) {
-  GMR_ARG(hist && count && t && pt && B > 0 && T > 0 && T <= 1024, "bad args (T <= 1024)");
+                                            int64_t row0, int32_t* t, float* pt, void* stream) {
+  GMR_ARG(hist && count && t && pt && B > 0 && T > 0 && T <= 1024 && row0 >= 0, "bad args (T <= 1024)");
   GMR_ARG(hist_len >= 1 && hist_len <= 16, "history length must be 1..16");
   hipLaunchKernelGGL(sample_t_importance_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, T, hist_len, hist,
-                     count, uniform_prob, seed, step, t, pt);
+                     count, uniform_prob, seed, step, row0, t, pt);
   GMR_LAUNCHED();
   return GMR_OK;
 }
@@ -501,16 +503,17 @@ extern "C" int gmr_diff_qsample(int32_t B, int32_t I, const int32_t* users, cons
                                 const int32_t* user_items, const int32_t* t, const float* sqrt_ac,
                                 const float* sqrt_1mac, const float* noise, int64_t ld_noise, const float* keep,
                                 int64_t ld_keep, float keep_prob, int32_t dropout, uint64_t seed, uint64_t step,
-                                float* x, int64_t ldx, void* stream) {
-  GMR_ARG(users && user_ptr && user_items && t && sqrt_ac && sqrt_1mac && x && B > 0 && I > 0, "bad args");
+                                int64_t row0, float* x, int64_t ldx, void* stream) {
+  GMR_ARG(users && user_ptr && user_items && t && sqrt_ac && sqrt_1mac && x && B > 0 && I > 0 && row0 >= 0,
+          "bad args");
   GMR_ARG(keep_prob > 0.f && keep_prob <= 1.f, "keep_prob must be in (0, 1]");
   hipStream_t st = (hipStream_t)stream;
   const int64_t c4n = (I + 3) / 4;
   hipLaunchKernelGGL(qsample_dense_kernel, dim3(gmr::grid_for((int64_t)B * c4n, 256)), dim3(256), 0, st, B, I, t,
-                     sqrt_ac, sqrt_1mac, noise, ld_noise, keep, ld_keep, keep_prob, dropout, seed, step, x, ldx);
+                     sqrt_ac, sqrt_1mac, noise, ld_noise, keep, ld_keep, keep_prob, dropout, seed, step, row0, x, ldx);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(qsample_sparse_kernel, dim3(B), dim3(64), 0, st, B, users, user_ptr, user_items, t, sqrt_ac,
-                     sqrt_1mac, noise, ld_noise, keep, ld_keep, keep_prob, dropout, seed, step, x, ldx);
+                     sqrt_1mac, noise, ld_noise, keep, ld_keep, keep_prob, dropout, seed, step, row0, x, ldx);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -352,12 +352,52 @@ void launch_tile(int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M,
     launch_t<BM, BN, WGM, WGN, false, true>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
 }
 
+// Tile and split-K choice of gmr_gemm_f32 (tile / split_k = 0: automatic).
+struct Plan {
+  int tile, bm, bn, splits;
+  int64_t tm, tn, kps;
+};
+
+Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int split_k) {
+  if (tile == 0) {
+    // measured on MI355X (scripts/gemm_bench.py): 256^2 tiles win the long-K products of the
+    // denoiser (M >= 2048, N >= 1000, K >= 4096; one 16-wave block per CU), 128^2 the wide
+    // K ~ 1000 ones, 64^2 (with split-K) the skinny N = 64 / K = 64 products and the TN updates.
+    // The 2048 x 512 x 512 transformer products (GenRecV1) run best on 64^2 tiles without split-K,
+    // their K = 6710 input projection on 128^2, the K = 256 output projection on 256^2.
+    const bool tnm = ta && !tb;
+    if (!tnm && M >= 2048 && N >= 1000 && K >= 4096) tile = 256;
+    else if (!tnm && M >= 2048 && N >= 4096 && K >= 256 && K <= 512) tile = 256;
+    else if (!tnm && M * N >= (int64_t)8 << 20 && K >= 512) tile = 128;
+    else if (!tnm && M * N >= (int64_t)1 << 20 && K >= 4096) tile = 128;
+    else tile = 64;
+  }
+  Plan p;
+  p.tile = tile;
+  p.bm = tile == 256128 ? 256 : tile == 128256 ? 128 : tile;
+  p.bn = tile == 256128 ? 128 : tile == 128256 ? 256 : tile;
+  p.tm = (M + p.bm - 1) / p.bm;
+  p.tn = (N + p.bn - 1) / p.bn;
+  int splits = split_k;
+  if (splits <= 0) {  // auto: aim for >= 512 workgroups on 256 CUs
+    splits = 1;
+    while (p.tm * p.tn * splits < 512 && K / (splits * 2) >= 512 && splits < 16) splits *= 2;
+  }
+  int64_t kps = (K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  p.splits = (int)((K + kps - 1) / kps);
+  p.kps = kps;
+  return p;
+}
+
 }  // namespace
 
-extern "C" int64_t gmr_gemm_workspace_floats(int64_t M, int64_t N, int64_t K) {
-  // upper bound used by gmr_gemm_f32's split-K path
-  (void)K;
-  return 16 * M * N;
+extern "C" int64_t gmr_gemm_workspace_floats(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
+                                             int32_t tile, int32_t split_k) {
+  // exact scratch of gmr_gemm_f32 with the same arguments: splits * M * N partial sums, 0 without split-K
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const Plan p = make_plan(trans_a, trans_b, M, N, K, tile, split_k);
+  return p.splits > 1 ? (int64_t)p.splits * M * N : 0;
 }
 
 extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, float alpha,
@@ -388,34 +428,15 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   e.rv1 = rowvec1;
   e.rv2 = rowvec2;
   const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
-  if (tile == 0) {
-    // measured on MI355X (scripts/gemm_bench.py): 256^2 tiles win the long-K products of the
-    // denoiser (M >= 2048, N >= 1000, K >= 4096; one 16-wave block per CU), 128^2 the wide
-    // K ~ 1000 ones, 64^2 (with split-K) the skinny N = 64 / K = 64 products and the TN updates.
-    // The 2048 x 512 x 512 transformer products (GenRecV1) run best on 64^2 tiles without split-K,
-    // their K = 6710 input projection on 128^2, the K = 256 output projection on 256^2.
-    const bool tn = trans_a && !trans_b;
-    if (!tn && M >= 2048 && N >= 1000 && K >= 4096) tile = 256;
-    else if (!tn && M >= 2048 && N >= 4096 && K >= 256 && K <= 512) tile = 256;
-    else if (!tn && M * N >= (int64_t)8 << 20 && K >= 512) tile = 128;
-    else if (!tn && M * N >= (int64_t)1 << 20 && K >= 4096) tile = 128;
-    else tile = 64;
-  }
-  const int bm = tile == 256128 ? 256 : tile == 128256 ? 128 : tile;
-  const int bn = tile == 256128 ? 128 : tile == 128256 ? 256 : tile;
-  const int64_t tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
+  const Plan pl = make_plan(trans_a, trans_b, M, N, K, tile, split_k);
+  tile = pl.tile;
+  const int64_t tm = pl.tm, tn = pl.tn, kps = pl.kps;
+  const int splits = pl.splits;
   GMR_ARG(tm * tn < (1ll << 31), "too many tiles");
-  int splits = split_k;
-  if (splits <= 0) {  // auto: aim for >= 512 workgroups on 256 CUs
-    splits = 1;
-    while (tm * tn * splits < 512 && K / (splits * 2) >= 512 && splits < 16) splits *= 2;
-  }
-  int64_t kps = (K + splits - 1) / splits;
-  kps = (kps + BK - 1) / BK * BK;
-  splits = (int)((K + kps - 1) / kps);
   float* ws = nullptr;
   if (splits > 1) {
-    GMR_ARG(workspace && workspace_floats >= (int64_t)splits * M * N, "split-K needs workspace of splits*M*N floats");
+    GMR_ARG(workspace && workspace_floats >= (int64_t)splits * M * N,
+            "split-K needs workspace of splits*M*N floats (gmr_gemm_workspace_floats)");
     ws = workspace;
   }
   hipStream_t st = (hipStream_t)stream;

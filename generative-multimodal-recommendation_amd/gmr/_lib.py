@@ -30,6 +30,7 @@ SIGNATURES = {
     "gmr_spmm_plan_pack": (I32, [P, P, I64, I64, I32, P, P]),
     "gmr_spmm_plan_info": (I32, [P, P, P]),
     "gmr_event_create": (I32, [P]),
+    "gmr_event_destroy": (I32, [P]),
     "gmr_stream_fork": (I32, [P, P, P]),
     "gmr_score_f16": (I32, [I64, I64, I64, P, I64, P, I64, P, I64, P]),
     "gmr_spmm_multi_f32": (I32, [P, P, I64, I64, P, I32, I32, P, P, P, P, I64, F32, F32, P, P, P]),
@@ -39,7 +40,7 @@ SIGNATURES = {
     "gmr_bipartite_workspace_ints": (I64, [I64, I64]),
     "gmr_bipartite_symnorm_build": (I32, [I64, I64, P, P, I64, I32, F64, P, P, P, P, P]),
     "gmr_topk_to_user_csr": (I32, [I64, I32, P, I64, P, P, P]),
-    "gmr_gemm_workspace_floats": (I64, [I64, I64, I64]),
+    "gmr_gemm_workspace_floats": (I64, [I32, I32, I64, I64, I64, I32, I32]),
     "gmr_gemm_f32": (I32, [I32, I32, I64, I64, I64, F32, P, I64, P, I64, F32, P, I64, I32, P, P, I64, P, I64, P, P,
                            F32, I32, I32, P, I64, P]),
     "gmr_dmm_combine_fwd": (I32, [I64, P, P, P, P, P, F32, P, P]),
@@ -69,8 +70,8 @@ SIGNATURES = {
     "gmr_colsum_f32": (I32, [I64, I64, P, I64, P, I32, P, I32, P]),
     "gmr_sample_epoch": (I32, [I64, P, P, P, P, P, I64, U64, U64, P, P, P, P]),
     "gmr_permutation": (I32, [I64, U64, U64, P, P]),
-    "gmr_diff_sample_t": (I32, [I32, I32, U64, U64, P, P]),
-    "gmr_diff_qsample": (I32, [I32, I32, P, P, P, P, P, P, P, I64, P, I64, F32, I32, U64, U64, P, I64, P]),
+    "gmr_diff_sample_t": (I32, [I32, I32, U64, U64, I64, P, P]),
+    "gmr_diff_qsample": (I32, [I32, I32, P, P, P, P, P, P, P, I64, P, I64, F32, I32, U64, U64, I64, P, I64, P]),
     "gmr_diff_densify": (I32, [I32, I32, P, P, P, P, I64, P]),
     "gmr_diff_time_bias": (I32, [I32, I32, P, P, P, I64, I64, P, I32, P, P, P, P]),
     "gmr_diff_loss_rows": (I32, [I32, I32, P, P, P, P, P, P, P, I64, F32, P, P, P, I32, P]),
@@ -78,7 +79,7 @@ SIGNATURES = {
     "gmr_fill2d_f32": (I32, [I64, I64, P, I64, F32, P]),
     "gmr_transpose_f32": (I32, [I64, I64, P, I64, P, I64, P]),
     "gmr_diff_sparse_hidden": (I32, [I32, I32, P, P, P, P, I64, P, P, I64, P]),
-    "gmr_diff_sample_t_importance": (I32, [I32, I32, I32, P, P, F64, U64, U64, P, P, P]),
+    "gmr_diff_sample_t_importance": (I32, [I32, I32, I32, P, P, F64, U64, U64, I64, P, P, P]),
     "gmr_diff_history_update": (I32, [I32, I32, I32, P, P, P, P, P]),
     "gmr_diff_gc_rows": (I32, [I32, P, P, P, P, I64, P, I64, F32, P, I64, P, P]),
     "gmr_diff_time_bwd": (I32, [I32, I32, I32, P, P, P, P, I64, I64, P, P, P, P, I32, P]),

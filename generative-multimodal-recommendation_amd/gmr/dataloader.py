@@ -55,20 +55,39 @@ class TrainDataLoader:
         self.pr = 0
 
     # --- device state -------------------------------------------------------------
+    def sub_batch_offsets(self, world):
+        """Interaction offsets of the (batch, rank) sub-batches: batch b = rows [b*B, min((b+1)*B, n))
+        of the epoch draw, split in contiguous shards over `world` data-parallel ranks (the first
+        rows % world ranks hold one more row).  Returns nb * world + 1 monotone offsets."""
+        nb = (self.n_inter + self.batch_size - 1) // self.batch_size
+        offs = [0]
+        for b in range(nb):
+            lo, hi = b * self.batch_size, min((b + 1) * self.batch_size, self.n_inter)
+            q, rem = divmod(hi - lo, world)
+            for r in range(world):
+                offs.append(offs[-1] + q + (1 if r < rem else 0))
+        return np.asarray(offs, np.int64)
+
     def to_device(self):
+        from . import dist
+        W = dist.world()
+        if self._dev is not None and self._dev["world"] != W:
+            self._dev = None
         if self._dev is None:
             d = self.device
             t = lambda a: torch.as_tensor(a).to(d)  # noqa: E731
             nb = (self.n_inter + self.batch_size - 1) // self.batch_size
-            offs = np.minimum(np.arange(nb + 1, dtype=np.int64) * self.batch_size, self.n_inter)
+            offs = self.sub_batch_offsets(W)
+            sb = -(-self.batch_size // W)  # rows of the largest sub-batch
             self._dev = {
+                "world": W,
                 "inter_user": t(self.u_np), "inter_item": t(self.i_np),
                 "user_ptr": t(self.uptr_np), "user_items": t(self.uitems_np),
                 "all_items": t(self.all_items_np),
-                "batch_offsets": t(offs), "n_batches": nb,
+                "batch_offsets": t(offs), "offsets_np": offs, "n_batches": nb,
                 "sample": torch.empty((3, self.n_inter), dtype=torch.int32, device=d),
-                "plan_bpr": torch.empty((nb, _pow2(3 * self.batch_size)), dtype=torch.int64, device=d),
-                "plan_cl": torch.empty((nb, _pow2(2 * self.batch_size)), dtype=torch.int64, device=d),
+                "plan_bpr": torch.empty((nb * W, _pow2(3 * sb)), dtype=torch.int64, device=d),
+                "plan_cl": torch.empty((nb * W, _pow2(2 * sb)), dtype=torch.int64, device=d),
                 "key_add_bpr": t(np.array([0, self.n_users, self.n_users], np.int32)),
                 "key_add_cl": t(np.array([0, self.n_users], np.int32)),
             }
@@ -91,19 +110,27 @@ class TrainDataLoader:
                   ptr(s[0]), ptr(s[1]), ptr(s[2]), stream())
         self._epoch += 1
         if with_plans:
-            nb = d["n_batches"]
+            nb = d["n_batches"] * d["world"]  # one plan per (batch, rank) sub-batch
             _lib.call("gmr_sort_batch_keys", nb, ptr(s), ptr(d["batch_offsets"]), ptr(d["key_add_bpr"]), 3,
                       self.n_inter, ptr(d["plan_bpr"]), d["plan_bpr"].shape[1], d["plan_bpr"].shape[1], stream())
             _lib.call("gmr_sort_batch_keys", nb, ptr(s), ptr(d["batch_offsets"]), ptr(d["key_add_cl"]), 2,
                       self.n_inter, ptr(d["plan_cl"]), d["plan_cl"].shape[1], d["plan_cl"].shape[1], stream())
         return d
 
-    def batches(self, d):
+    def batches(self, d, rank=None):
+        """Per batch b of the epoch draw: (b, global rows, users, pos, neg, plan_bpr, plan_cl) of this
+        rank's sub-batch (the whole batch at world size 1).  `global rows` is the size of batch b,
+        which the data-parallel step normalises by; a rank's sub-batch may be empty."""
+        from . import dist
+        W = d["world"]
+        r = dist.rank() if rank is None else rank
         nb, B = d["n_batches"], self.batch_size
-        s = d["sample"]
+        s, offs = d["sample"], d["offsets_np"]
         for b in range(nb):
-            lo, hi = b * B, min((b + 1) * B, self.n_inter)
-            yield b, s[0, lo:hi], s[1, lo:hi], s[2, lo:hi], d["plan_bpr"][b], d["plan_cl"][b]
+            lo, hi = int(offs[b * W + r]), int(offs[b * W + r + 1])
+            rows = min((b + 1) * B, self.n_inter) - b * B
+            yield (b, rows, s[0, lo:hi], s[1, lo:hi], s[2, lo:hi], d["plan_bpr"][b * W + r],
+                   d["plan_cl"][b * W + r])
 
     # --- reference-style iteration -------------------------------------------------------
     def __len__(self):
@@ -111,8 +138,9 @@ class TrainDataLoader:
 
     def __iter__(self):
         d = self.epoch(with_plans=False)
-        for b, u, p, n, _, _ in self.batches(d):
-            yield torch.stack([u, p, n]).long()
+        s, B = d["sample"], self.batch_size
+        for lo in range(0, self.n_inter, B):
+            yield s[:, lo:lo + B].long()
 
 
 class EvalDataLoader:

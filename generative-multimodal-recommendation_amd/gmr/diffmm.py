@@ -437,11 +437,13 @@ class DiffMM(GeneralRecommender):
         return self._dw[slot]
 
     def diffusion_step(self, den, batch_users, feats, item_embeds, step, noise=None, keep=None, t=None,
-                       norm_rows=None, slot=0):
+                       norm_rows=None, slot=0, row0=0):
         """One GaussianDiffusion.training_losses + backward for one denoiser (diffmm.py:453-477).
 
         Writes the denoiser's gradients into its slab; returns (diff_loss, gc_loss) per-row
-        fp64 views.  noise/keep/t may be supplied (parity tests); else drawn by Philox."""
+        fp64 views.  noise/keep/t may be supplied (parity tests); else drawn by Philox, keyed by
+        (step, row0 + row): a data-parallel rank holding rows [row0, row0 + B) of a global batch
+        draws exactly what one process drawing the whole batch would."""
         B = batch_users.numel()
         nr = float(norm_rows or B)
         w = self._dwork(B, slot)
@@ -449,14 +451,14 @@ class DiffMM(GeneralRecommender):
         x, h, out, Z = w["x"][:B], w["h"][:B], w["out"][:B], w["Z"][:B]
         tt = w["t"][:B]
         if t is None:
-            _lib.call("gmr_diff_sample_t", B, T, self.seed, step, ptr(tt), stream())
+            _lib.call("gmr_diff_sample_t", B, T, self.seed, step, row0, ptr(tt), stream())
         else:
             tt.copy_(t)
         EB, _, _ = den.time_bias(T)
         _lib.call("gmr_diff_qsample", B, I, ptr(batch_users), ptr(self.user_ptr), ptr(self.user_items), ptr(tt),
                   ptr(self._tab_dev["sqrt_ac"]), ptr(self._tab_dev["sqrt_1mac"]), ptr(noise),
                   noise.stride(0) if noise is not None else 0, ptr(keep), keep.stride(0) if keep is not None else 0,
-                  den.keep_prob, 1, self.seed, step, ptr(x), x.stride(0), stream())
+                  den.keep_prob, 1, self.seed, step, row0, ptr(x), x.stride(0), stream())
         xi = x[:, :I]
         den.hidden(xi, h, EB, t_rows=tt)
         o = out[:, :I]

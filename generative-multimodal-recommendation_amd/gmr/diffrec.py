@@ -13,9 +13,10 @@ one fused step per batch:
 Prediction (full_sort_predict, :372-388) is p_sample over all `steps` with the posterior mean
 fused into the output GEMM's epilogue.
 
-Data parallel (gmr/dist.py): each rank trains on its loader batch; the Lt-history updates of
-all ranks are all-gathered and applied in global batch order (dp_step_end), so every rank keeps
-the identical importance-sampling state the single-process schedule would have.
+Data parallel (gmr/dist.py): each loader batch is split over the ranks (rank r holds rows
+[row0, row0 + n) of it); t, pt, noise and the dropout mask are drawn per global row, and the
+Lt-history updates of all ranks are all-gathered and applied in global batch order
+(dp_step_end), so every rank keeps the importance-sampling state of the single-process run.
 """
 import numpy as np
 import torch
@@ -68,6 +69,8 @@ class _DiffRecLoss(torch.autograd.Function):
 
 
 class DiffRec(GeneralRecommender):
+    rec_step_takes_row0 = True  # the Trainer passes the sub-batch's first row (global-row RNG keys)
+
     def __init__(self, config, dataloader):
         super().__init__(config, dataloader)
         c = config
@@ -125,7 +128,7 @@ class DiffRec(GeneralRecommender):
 
     # ------------------------------------------------------------------ training
     def rec_step(self, users, pos=None, neg=None, plan_bpr=None, plan_cl=None, norm_rows=None, reg_share=1.0,
-                 noise=None, keep=None, t=None, pt=None):
+                 noise=None, keep=None, t=None, pt=None, row0=0):
         """training_losses + backward for the users of one batch (interaction[0], duplicates kept).
         Returns the batch loss (a device fp32 scalar); gradients land in the denoiser slab.
         noise/keep/t/pt may be injected (parity tests); otherwise drawn on the device."""
@@ -136,10 +139,10 @@ class DiffRec(GeneralRecommender):
         I, T = self.n_items, self.steps
         x, h, out = w["x"][:B], w["h"][:B], w["out"][:B]
         tt, ptb = w["t"][:B], w["pt"][:B]
-        sid = self._step * dist.world() + dist.rank()  # distinct Philox stream per (step, rank)
+        sid = self._step  # Philox stream of the global step; rows keyed by their global index
         if t is None:
             _lib.call("gmr_diff_sample_t_importance", B, T, HISTORY, ptr(self.Lt_history), ptr(self.Lt_count),
-                      UNIFORM_PROB, self.seed, sid, ptr(tt), ptr(ptb), stream())
+                      UNIFORM_PROB, self.seed, sid, row0, ptr(tt), ptr(ptb), stream())
         else:
             tt.copy_(t)
             ptb.copy_(pt)
@@ -147,7 +150,7 @@ class DiffRec(GeneralRecommender):
         _lib.call("gmr_diff_qsample", B, I, ptr(users), ptr(self.user_ptr), ptr(self.user_items), ptr(tt),
                   ptr(self._tab_dev["sqrt_ac"]), ptr(self._tab_dev["sqrt_1mac"]), ptr(noise),
                   noise.stride(0) if noise is not None else 0, ptr(keep), keep.stride(0) if keep is not None else 0,
-                  den.keep_prob, 1, self.seed, sid, ptr(x), x.stride(0), stream())
+                  den.keep_prob, 1, self.seed, sid, row0, ptr(x), x.stride(0), stream())
         xi = x[:, :I]
         den.hidden(xi, h, EB, t_rows=tt)
         o = out[:, :I]
@@ -162,7 +165,7 @@ class DiffRec(GeneralRecommender):
         if not dist.is_dist():
             self._apply_history(*self._pending)
             self._pending = None
-        self._step += 1
+            self._step += 1
         return self._loss32[0]
 
     def _apply_history(self, t, loss):
@@ -170,12 +173,13 @@ class DiffRec(GeneralRecommender):
                   ptr(self.Lt_count), stream())
 
     def dp_step_end(self):
-        """Called by the Trainer on every rank after the gradient all-reduce of a global step:
-        all-gathers the (t, w*mse) rows of all ranks and applies them in global batch order."""
+        """Called by the Trainer on every rank (idle ones included) after the gradient all-reduce of
+        a global step: all-gathers the (t, w*mse) rows of all ranks and applies them in global batch
+        order (rank shards are contiguous slices of the batch)."""
         if not dist.is_dist():
             return
         W, r = dist.world(), dist.rank()
-        size = int(self.batch_size)
+        size = -(-int(self.batch_size) // W)
         tb = torch.full((W * size,), -1, dtype=torch.int32, device=self.device)
         lb = torch.zeros(W * size, dtype=torch.float64, device=self.device)
         if self._pending is not None:
@@ -187,6 +191,7 @@ class DiffRec(GeneralRecommender):
         dist.all_gather_rows_(lb, size)
         self._apply_history(tb, lb)
         self._pending = None
+        self._step += 1
 
     def calculate_loss(self, interaction):
         users = interaction[0].to(torch.int32).contiguous()

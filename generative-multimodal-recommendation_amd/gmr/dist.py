@@ -2,20 +2,19 @@
 (backend "nccl" is RCCL on ROCm, riding xGMI).  The reference has no distributed code (SURVEY.md
 F2); this module holds the sharding rules used by the trainers:
 
-  * diffusion phase  — every global step takes world x train_batch_size users of the epoch
-    permutation; rank r trains on its contiguous slice; denoiser gradients are all-reduced
-    (SUM of per-rank sums normalised by the global row count) before the identical Adam steps;
+  * diffusion phase  — each batch of train_batch_size users of the epoch permutation is split
+    over the ranks (contiguous slices); denoiser gradients are all-reduced (SUM of per-rank sums
+    normalised by the batch's row count) before the identical Adam steps;
   * graph rebuild    — users are split in contiguous shards; each rank p_samples its shard and
     the int32 top-k lists are all-gathered; every rank builds the identical CSR;
-  * BPR phase        — global step g runs loader batches g*W .. g*W+W-1, one per rank; the
-    rec gradients are all-reduced (the regulariser is counted once);
+  * BPR phase        — each train_batch_size batch of the epoch draw is split over the ranks;
+    the rec gradients are all-reduced (the regulariser is counted once);
   * evaluation       — eval users are sharded; the top-K index rows are all-gathered.
-The per-GPU batch stays train_batch_size, so the number of optimizer steps per epoch shrinks
-with the world size (the global batch grows); world = 1 is exactly the reference schedule.
+The global batch is the reference's train_batch_size at every world size, so the number of
+optimiser steps per epoch, and the trajectory up to fp32 reassociation of the sums, are the
+single-process ones (the per-GPU batch shrinks as B / world: strong scaling).
 Everything here also runs on CPU tensors with the gloo backend (tests/test_dist_cpu.py).
 """
-import math
-
 import torch
 import torch.distributed as tdist
 
@@ -50,13 +49,10 @@ def padded_shard(n, w=None, r=None):
     return lo, min(n, lo + s), s
 
 
-def global_steps(n_batches, w=None):
-    return math.ceil(n_batches / (world() if w is None else w))
-
-
-def step_batches(g, n_batches, w=None):
+def shard_sizes(n, w=None):
+    """Rows of each rank's contiguous shard of an n-row batch."""
     w = world() if w is None else w
-    return [b for b in range(g * w, g * w + w) if b < n_batches]
+    return [shard(n, w, r)[1] - shard(n, w, r)[0] for r in range(w)]
 
 
 def dp_scales(rows):

@@ -617,7 +617,7 @@ class FlipDiffusion:
         if "t" in inj:
             t.copy_(inj["t"])
         else:
-            _lib.call("gmr_diff_sample_t", B, T, seed, step, ptr(t), stream())
+            _lib.call("gmr_diff_sample_t", B, T, seed, step, 0, ptr(t), stream())
         xt, z, dz = w["xt"][:B, :I], w["z"][:B, :I], w["dz"][:B, :I]
         flip = inj.get("flip1")
         _lib.call("gmr_flip_qsample", B, I, ptr(x0), x0.stride(0), ptr(t), 0, ptr(tab), T, self.base_temp, ptr(flip),

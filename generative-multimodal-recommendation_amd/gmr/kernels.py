@@ -5,6 +5,7 @@ pointers + the current torch HIP stream to libgmr_hip.so, and raises on error.  
 used here only for memory and streams.
 """
 import ctypes
+import os
 
 import torch
 
@@ -71,12 +72,21 @@ def stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+_get_stream = getattr(torch._C, "_cuda_getCurrentStream", None)
+_set_stream = getattr(torch._C, "_cuda_setStream", None)
+
+
 class Streams:
     """Fork/join helper over a few side streams: work issued inside `with st.on(i):` runs on side
     stream i after everything already issued on the current stream; st.join(i) makes the current
     stream wait for it.  The fork/join is one C-ABI call on raw stream handles (gmr_stream_fork)
     and the current stream is switched with torch's raw setter: the DiffMM rec step forks ~17
-    times per step and is host-issue-bound, so torch Stream/Event objects are kept off this path."""
+    times per step and is host-issue-bound, so torch Stream/Event objects are kept off this path
+    (torch.cuda.stream() is the fallback when this torch build lacks the raw setters).
+    SERIAL (GMR_SERIAL=1, profiling): side work runs on the current stream, so every kernel's
+    duration is its own and not stretched by a concurrent one."""
+
+    SERIAL = False
 
     def __init__(self, n):
         self.side = [torch.cuda.Stream() for _ in range(n)]
@@ -94,28 +104,63 @@ class Streams:
         return _OnSide(self, i)
 
     def join(self, *idx):
+        if Streams.SERIAL:
+            return
         cur = stream()
         for i in idx:
             _lib.call("gmr_stream_fork", self._raw[i], cur, self._ev[2 * i + 1])
 
+    def close(self):
+        """Release the fork/join events (after the device has drained the streams' work)."""
+        ev, self._ev = getattr(self, "_ev", []), []
+        if ev and _lib is not None:
+            torch.cuda.synchronize(self._dev)
+            lib = _lib.load()
+            for e in ev:
+                lib.gmr_event_destroy(e)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 (interpreter shutdown: the runtime may be gone)
+            pass
+
+
+Streams.SERIAL = os.environ.get("GMR_SERIAL", "0") == "1"
+
 
 class _OnSide:
-    __slots__ = ("st", "i", "prev")
+    __slots__ = ("st", "i", "prev", "ctx")
 
     def __init__(self, st, i):
         self.st, self.i = st, i
 
     def __enter__(self):
         st, i = self.st, self.i
-        self.prev = torch._C._cuda_getCurrentStream(st._dev)
+        if Streams.SERIAL:
+            self.prev = None
+            return None
+        if _cur_device is not None and _cur_device() != st._dev:
+            raise RuntimeError(f"Streams built on device {st._dev} used while device {_cur_device()} is current")
         _lib.call("gmr_stream_fork", stream(), st._raw[i], st._ev[2 * i])
+        if _get_stream is None or _set_stream is None:
+            self.prev = None
+            self.ctx = torch.cuda.stream(st.side[i])
+            self.ctx.__enter__()
+            return st.side[i]
+        self.ctx = None
+        self.prev = _get_stream(st._dev)
         sid, dev, dt = st._ids[i]
-        torch._C._cuda_setStream(stream_id=sid, device_index=dev, device_type=dt)
+        _set_stream(stream_id=sid, device_index=dev, device_type=dt)
         return st.side[i]
 
     def __exit__(self, *a):
+        if self.prev is None:
+            if not Streams.SERIAL and self.ctx is not None:
+                self.ctx.__exit__(*a)
+            return False
         sid, dev, dt = self.prev
-        torch._C._cuda_setStream(stream_id=sid, device_index=dev, device_type=dt)
+        _set_stream(stream_id=sid, device_index=dev, device_type=dt)
         return False
 
 
@@ -167,12 +212,13 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
     for t in (A, B, C):
         if t.dtype != torch.float32:
             raise TypeError("gemm is fp32")
-    ws = workspace(16 * M * N, C.device)
+    need = _lib.load().gmr_gemm_workspace_floats(int(trans_a), int(trans_b), M, N, K, tile, split_k)
+    ws = workspace(need, C.device) if need > 0 else None  # split-K partials only when this call splits
     with _Probe("gemm", (M, N, K, int(trans_a), int(trans_b), epi)):
         _lib.call("gmr_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), ptr(A), _ld(A), ptr(B), _ld(B),
                   float(beta), ptr(C), _ld(C), epi, ptr(bias), ptr(bias_row), ld_bias, ptr(aux),
                   _ld(aux) if aux is not None else 0, ptr(rv1), ptr(rv2), float(slope), tile, split_k, ptr(ws),
-                  ws.numel(), stream())
+                  ws.numel() if ws is not None else 0, stream())
     return C
 
 

@@ -145,6 +145,9 @@ class TopKEvaluator:
         return np.isin(q, keys).reshape(n, Kk)
 
     def _dump(self, topk_index, eval_data, idx):
+        from . import dist
+        if dist.rank() != 0:  # every rank holds the gathered top-k: one writer
+            return
         k = max(self.topk)
         d = os.path.abspath(self.config["recommend_topk"] or "recommend_topk/")
         os.makedirs(d, exist_ok=True)

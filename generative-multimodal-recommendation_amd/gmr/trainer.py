@@ -82,21 +82,18 @@ class Trainer:
         d = train_data.epoch()
         acc = self._loss_acc
         K.zero_(acc)
-        batches = list(train_data.batches(d))
-        W, r = dist.world(), dist.rank()
+        W = dist.world()
         slabs = self.model.optim_slabs()
         hook = getattr(self.model, "dp_step_end", None)  # per-global-step model state sync (DiffRec)
-        for g in range(dist.global_steps(len(batches), W)):
-            ids = dist.step_batches(g, len(batches), W)
-            rows = [batches[i][1].numel() for i in ids] + [0] * (W - len(ids))
-            norm, share = dist.dp_scales(rows)
-            mine = g * W + r
-            if mine < len(batches):
-                _, u, p, ng, pb, pc = batches[mine]
-                if self._use_graphs and u.numel() == train_data.batch_size:
+        # one optimiser step per train_batch_size batch, as the reference (trainer.py:144-208);
+        # under data parallelism every batch is split over the ranks
+        for b, rows, u, p, ng, pb, pc in train_data.batches(d):
+            norm, share = dist.dp_scales(dist.shard_sizes(rows, W))
+            if u.numel() > 0:
+                if self._use_graphs and rows == train_data.batch_size:
                     self._graphed_step(u, p, ng, pb, pc, norm, share, acc)
                 else:
-                    loss = self.model.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share)
+                    loss = self._rec_step(u, p, ng, pb, pc, norm, share, dist.shard(rows)[0])
                     _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
             else:
                 for s_ in slabs:
@@ -113,6 +110,11 @@ class Trainer:
             self.logger.info("Loss is nan at epoch: {}. Exiting.".format(epoch_idx))
             return torch.tensor(float("nan")), []
         return total, []
+
+    def _rec_step(self, u, p, ng, pb, pc, norm, share, row0):
+        if getattr(self.model, "rec_step_takes_row0", False):
+            return self.model.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share, row0=row0)
+        return self.model.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share)
 
     def _graphed_step(self, u, p, ng, pb, pc, norm, share, acc):
         """One full-size BPR step replayed from a HIP graph (torch.cuda.CUDAGraph over the fused
@@ -192,6 +194,11 @@ class Trainer:
         return self.best_valid_score, self.best_valid_result, self.best_test_upon_valid
 
     def _save_checkpoint(self, epoch):
+        """trainer.py:345-366 (same keys), plus the generated UI graphs.  Data parallel: every rank
+        holds the same parameters; rank 0 writes, the others wait at the barrier."""
+        if dist.rank() != 0:
+            dist.barrier()
+            return
         d = self.config["checkpoint_dir"] or "saved"
         os.makedirs(d, exist_ok=True)
         path = os.path.join(d, "{}-{}.pth".format(self.config["model"], self.config["dataset"]))
@@ -203,6 +210,7 @@ class Trainer:
             state["generated_graphs"] = extra()
         torch.save(state, path)
         self.logger.info("Saved best model to {}".format(path))
+        dist.barrier()
 
     # ------------------------------------------------------------------ evaluation
     @torch.no_grad()
@@ -267,8 +275,10 @@ class DiffMMTrainer(Trainer):
         self._epoch_ctr = 0
 
     def diffusion_phase(self, epoch_idx):
-        """trainer.py:487-527 — train both denoisers over all users in shuffled batches.
-        Data parallel: a global step covers world x batch users; each rank takes a contiguous slice."""
+        """trainer.py:487-527 — train both denoisers over all users in shuffled batches of
+        train_batch_size users, two Adam steps per batch.  Data parallel: each batch is split over
+        the ranks (contiguous slices); t / noise / dropout draws are keyed by the row's index in the
+        batch, so the gradient sum equals the single-process one up to fp32 reassociation."""
         m = self.model
         m.train()
         B = self.config["train_batch_size"]
@@ -284,19 +294,19 @@ class DiffMMTrainer(Trainer):
         opts = (self.denoise_opt_image, self.denoise_opt_text)
         st = m._streams
         steps = 0
-        for g, lo in enumerate(range(0, U, B * W)):
-            hi = min(U, lo + B * W)
+        for g, lo in enumerate(range(0, U, B)):
+            hi = min(U, lo + B)
             a, b = dist.shard(hi - lo, W, r)
             users = self._perm[lo + a:lo + b]
             nb = users.numel()
-            base = ((self._epoch_ctr * 100000 + g) * W + r) * 2
+            base = (self._epoch_ctr * 100000 + g) * 2
             # the two denoisers are independent until their Adam steps: the text one runs on a side
             # stream (own work buffers, slot 1) beside the image one; under DP the image gradient
             # exchange starts as soon as its step is issued (one bucket per slab)
             def one(j):
                 den, feats = dens[j]
                 if nb > 0:
-                    diff, gc = m.diffusion_step(den, users, feats, iE, base + j, norm_rows=hi - lo, slot=j)
+                    diff, gc = m.diffusion_step(den, users, feats, iE, base + j, norm_rows=hi - lo, slot=j, row0=a)
                     _lib.call("gmr_sum_f64", nb, ptr(diff), 1.0 / (hi - lo), ptr(self._dloss[j:j + 1]), 1, stream())
                     _lib.call("gmr_sum_f64", nb, ptr(gc), m.e_loss / (hi - lo), ptr(self._dloss[j:j + 1]), 1,
                               stream())
@@ -365,9 +375,9 @@ class GenRecV1Trainer(Trainer):
         self.logger.info("Multimodal Clustering Done.")
 
     def diffusion_phase(self, epoch_idx):
-        """trainer.py:689-728: train the image denoiser over all users in shuffled batches.
-        Data parallel: a global step covers world x batch users; each rank takes a contiguous slice,
-        the schedule / pos_weight use the whole global batch (as the reference's batch)."""
+        """trainer.py:689-728: train the image denoiser over all users in shuffled batches of
+        train_batch_size users.  Data parallel: each batch is split over the ranks (contiguous
+        slices); the schedule / pos_weight use the whole batch, as the reference's batch does."""
         m = self.model
         m.train()
         B = self.config["train_batch_size"]
@@ -381,8 +391,8 @@ class GenRecV1Trainer(Trainer):
         _lib.call("gmr_permutation", U, m.seed, 2000 + self._epoch_ctr, ptr(self._perm), stream())
         K.zero_(self._dloss)
         steps = 0
-        for g, lo in enumerate(range(0, U, B * W)):
-            hi = min(U, lo + B * W)
+        for g, lo in enumerate(range(0, U, B)):
+            hi = min(U, lo + B)
             a, b = dist.shard(hi - lo, W, r)
             users = self._perm[lo + a:lo + b]
             step = ((self._epoch_ctr * 100000 + g) * W + r) * 4

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GMR_ABI_VERSION 1
+#define GMR_ABI_VERSION 2
 #define GMR_OK 0
 #define GMR_ERR_ARG (-1000)
 
@@ -46,6 +46,7 @@ int gmr_device_name(char* buf /* host */, int32_t len);
 int gmr_zero(void* ptr, int64_t bytes, void* stream);
 /* host-layer stream plumbing: an event (timing disabled) and "record ev on from, make to wait" */
 int gmr_event_create(void** ev /* host */);
+int gmr_event_destroy(void* ev);
 int gmr_stream_fork(void* from, void* to, void* ev);
 
 /* ---------------------------------------------------------------- K1 graph convolution
@@ -131,8 +132,11 @@ int gmr_topk_to_user_csr(int64_t n_users, int32_t k, const int32_t* topk, int64_
  * C[M,N] = epilogue(alpha * op(A) op(B)); op(A) = A (M x K, lda) or A^T (A stored K x M);
  * op(B) = B (K x N, ldb) or B^T (B stored N x K).  bias[(bias_row ? bias_row[m] : 0)*ld_bias + n].
  * Replaces nn.Linear / torch.mm / matmul: diffmm.py:117,124,277,352-358,472-473; vbpr.py:70,105.
- * tile: 0 auto, 64 or 128; split_k: 0 auto, else >= 1 (needs workspace >= splits*M*N floats). */
-int64_t gmr_gemm_workspace_floats(int64_t M, int64_t N, int64_t K);
+ * tile: 0 auto, 64, 128, 256, 256128 (256 x 128) or 128256; split_k: 0 auto, else >= 1.
+ * gmr_gemm_workspace_floats returns the exact scratch the same call needs (splits*M*N floats of
+ * split-K partials, 0 when it does not split). */
+int64_t gmr_gemm_workspace_floats(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, int32_t tile,
+                                  int32_t split_k);
 int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
                  int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc, int32_t epilogue,
                  const float* bias, const int32_t* bias_row, int64_t ld_bias, const float* aux, int64_t ld_aux,
@@ -236,12 +240,15 @@ int gmr_permutation(int64_t n, uint64_t seed, uint64_t epoch, int32_t* out, void
 
 /* ---------------------------------------------------------------- K5/K6 diffusion (diffmm.py:408-484, diffrec.py:182-310)
  * x_t = sqrt_ac[t]*x0 + sqrt_1mac[t]*eps, times the Denoise input dropout keep/keep_prob when
- * dropout != 0; x0 rows come from the user's train items.  noise/keep may be NULL (Philox). */
-int gmr_diff_sample_t(int32_t B, int32_t T, uint64_t seed, uint64_t step, int32_t* t, void* stream);
+ * dropout != 0; x0 rows come from the user's train items.  noise/keep may be NULL (Philox).
+ * row0: index of row 0 inside the global batch — the Philox draws of a row depend on
+ * (seed, step, row0 + b) only, so a batch split over data-parallel ranks draws what one
+ * process drawing the whole batch would (trainer.py:491-527). */
+int gmr_diff_sample_t(int32_t B, int32_t T, uint64_t seed, uint64_t step, int64_t row0, int32_t* t, void* stream);
 int gmr_diff_qsample(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
                      const int32_t* t, const float* sqrt_ac, const float* sqrt_1mac, const float* noise,
                      int64_t ld_noise, const float* keep, int64_t ld_keep, float keep_prob, int32_t dropout,
-                     uint64_t seed, uint64_t step, float* x, int64_t ldx, void* stream);
+                     uint64_t seed, uint64_t step, int64_t row0, float* x, int64_t ldx, void* stream);
 int gmr_diff_densify(int32_t B, int32_t I, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
                      float* x, int64_t ldx, void* stream);
 int gmr_diff_time_bias(int32_t T, int32_t E, const float* emb_W, const float* emb_b, const float* W1, int64_t ld_w1,
@@ -262,8 +269,8 @@ int gmr_diff_sparse_hidden(int32_t B, int32_t H, const int32_t* users, const int
 /* DiffRec importance sampling of t (models/diffrec.py:234-250): uniform t and pt = 1 until every
  * t has hist_len recorded losses, then t ~ (1-up) sqrt(mean(hist^2))/sum + up/T, pt = p[t]*T. */
 int gmr_diff_sample_t_importance(int32_t B, int32_t T, int32_t hist_len, const double* hist, const int32_t* count,
-                                 double uniform_prob, uint64_t seed, uint64_t step, int32_t* t, float* pt,
-                                 void* stream);
+                                 double uniform_prob, uint64_t seed, uint64_t step, int64_t row0, int32_t* t,
+                                 float* pt, void* stream);
 /* Lt_history / Lt_count update (models/diffrec.py:279-286), rows applied in batch order; t < 0 skips. */
 int gmr_diff_history_update(int32_t B, int32_t T, int32_t hist_len, const int32_t* t, const double* loss,
                             double* hist, int32_t* count, void* stream);

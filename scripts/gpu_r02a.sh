@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-2 first check: GPU parity tests (incl. the 2-rank DP test), GEMM tile/split sweep of the
+# long-K denoiser shapes, the default bench, and a serial-mode rocprof kernel summary.
+set -o pipefail
+TAG=${1:-r02a}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -v -m gpu -p no:cacheprovider -x --timeout 240 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
+tail -1 gpurun_out/${TAG}_tests.log
+timeout -k 10 300 python scripts/gemm_bench.py --only "train_h,dh (NN),train_out,dW2,dW1,psample_h (NT),psample_out (NT)" --tiles 64,128,256,256128,128256 --splits 1,2,4,8 --reps 10 > gpurun_out/${TAG}_gemm.txt 2>&1 || { echo "gemm bench failed"; tail -20 gpurun_out/${TAG}_gemm.txt; exit 1; }
+timeout -k 10 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo "bench failed"; tail -30 gpurun_out/${TAG}_bench.err; exit 1; }
+cat gpurun_out/${TAG}_bench.json
+GMR_SERIAL=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o prof -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-probe > gpurun_out/${TAG}_prof.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/${TAG}_prof.log; exit 1; }
+echo all-done

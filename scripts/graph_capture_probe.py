@@ -21,7 +21,7 @@ def main():
     trainer._train_epoch(tl, 0)
     torch.cuda.synchronize()
     d = tl.epoch()
-    _, u, p, ng, pb, pc = list(tl.batches(d))[0]
+    _, _, u, p, ng, pb, pc = list(tl.batches(d))[0]
     static = [t.clone() for t in (u, p, ng, pb, pc)]
     model.rec_step(*static)  # warm every lazily sized buffer outside the capture
     torch.cuda.synchronize()

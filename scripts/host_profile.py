@@ -31,7 +31,7 @@ def main():
     batches = list(tl.batches(d))[:a.steps]
 
     def run():
-        for _, u, p, ng, pb, pc in batches:
+        for _, _, u, p, ng, pb, pc in batches:
             model.rec_step(u, p, ng, pb, pc)
 
     run()

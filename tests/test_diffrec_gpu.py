@@ -107,10 +107,10 @@ def test_importance_sampling(golden):
     # histories not yet full -> uniform t, pt = 1
     partial = torch.full((T,), 10, dtype=torch.int32, device=DEV)
     partial[2] = 9
-    _lib.call("gmr_diff_sample_t_importance", B, T, 10, ptr(hist), ptr(partial), 0.001, 7, 0, ptr(t), ptr(pt), stream())
+    _lib.call("gmr_diff_sample_t_importance", B, T, 10, ptr(hist), ptr(partial), 0.001, 7, 0, 0, ptr(t), ptr(pt), stream())
     assert (pt == 1).all() and int(t.min()) >= 0 and int(t.max()) < T
     full = torch.full((T,), 10, dtype=torch.int32, device=DEV)
-    _lib.call("gmr_diff_sample_t_importance", B, T, 10, ptr(hist), ptr(full), 0.001, 7, 1, ptr(t), ptr(pt), stream())
+    _lib.call("gmr_diff_sample_t_importance", B, T, 10, ptr(hist), ptr(full), 0.001, 7, 1, 0, ptr(t), ptr(pt), stream())
     pt_all = model_ref.importance_pt_all(g["imp_hist"])
     tn = t.cpu().numpy()
     np.testing.assert_allclose(pt.cpu().numpy(), (pt_all[tn] * T).astype(np.float32), rtol=1e-6)

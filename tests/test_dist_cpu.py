@@ -27,9 +27,29 @@ def test_shard_rules():
             pads = [dist.padded_shard(n, w, r) for r in range(w)]
             covered = sorted(i for lo, hi, _ in pads for i in range(lo, hi))
             assert covered == list(range(n))
-    assert dist.step_batches(2, 10, 4) == [8, 9]
-    assert dist.global_steps(10, 4) == 3
-    assert dist.dp_scales([2048, 2048, 974, 0]) == (5070.0, 1.0 / 3)
+    assert dist.shard_sizes(2048, 3) == [683, 683, 682]
+    assert dist.shard_sizes(2, 4) == [1, 1, 0, 0]
+    assert dist.dp_scales(dist.shard_sizes(974, 8)) == (974.0, 1.0 / 8)
+    assert dist.dp_scales([2, 1, 0, 0]) == (3.0, 1.0 / 2)
+
+
+def test_sub_batch_offsets():
+    """Every reference batch (train_batch_size rows of the epoch draw) is cut into `world`
+    contiguous sub-batches that tile it exactly (gmr/dataloader.py sub_batch_offsets)."""
+    from types import SimpleNamespace
+
+    from gmr import dist
+    from gmr.dataloader import TrainDataLoader
+    for n_inter, B in ((121_846, 2048), (100, 40), (5, 2048)):
+        nb = -(-n_inter // B)
+        for w in (1, 2, 3, 8):
+            offs = TrainDataLoader.sub_batch_offsets(SimpleNamespace(n_inter=n_inter, batch_size=B), w)
+            assert len(offs) == nb * w + 1 and offs[0] == 0 and offs[-1] == n_inter
+            assert np.all(np.diff(offs) >= 0)
+            for b in range(nb):
+                lo, hi = b * B, min((b + 1) * B, n_inter)
+                assert offs[b * w] == lo and offs[(b + 1) * w] == hi
+                assert list(np.diff(offs[b * w:(b + 1) * w + 1])) == dist.shard_sizes(hi - lo, w)
 
 
 def _free_port():

@@ -1,0 +1,138 @@
+"""Data parallelism on the HIP path: two ranks sharing the one GPU of the box
+(gloo carries the gradient all-reduces, as a multi-GPU RCCL run would), against the same
+computation in one process.  The global batch is the reference's batch at every world size
+(common/trainer.py:144-208 for the BPR phase, :491-527 for the diffusion phase): each batch is
+split over the ranks, so one global step must equal the single-process step within the fp32
+tolerances of the golden tests (the per-rank partial sums are added in a different order).
+
+Cases (tiny golden shape, tests/golden/diffmm_tiny.npz):
+  * one rec step (calculate_loss + backward) on the golden batch: loss and every rec gradient;
+  * one diffusion step (training_losses + backward) with on-device Philox draws: the rank holding
+    rows [a, b) passes row0 = a, so it draws what the single process drew for those rows;
+  * the diffusion phase and the BPR epoch of DiffMMTrainer (Adam steps included, UI graphs
+    fixed): denoiser and rec parameters after the epoch.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _golden():
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "diffmm_tiny.npz"), allow_pickle=False))
+
+
+def _case():
+    """Runs every case at the current world size; returns numpy results (identical on all ranks)."""
+    from test_diffmm_gpu import build_model, tiny_config
+
+    from gmr import dist
+    from gmr.dataloader import TrainDataLoader
+    from gmr.dataset import RecDataset
+    from gmr.trainer import DiffMMTrainer, Trainer
+
+    g = _golden()
+    dev = "cuda"
+    out = {}
+    t = lambda k: torch.as_tensor(g[k].astype(np.int32)).to(dev)  # noqa: E731
+    # --- one rec step
+    m = build_model(g)
+    u, p, n = t("bpr_users"), t("bpr_pos"), t("bpr_neg")
+    B = u.numel()
+    a, b = dist.shard(B)
+    norm, share = dist.dp_scales(dist.shard_sizes(B))
+    loss = m.rec_step(u[a:b], p[a:b], n[a:b], norm_rows=norm, reg_share=share).view(1).double()
+    dist.all_reduce_(loss)
+    dist.all_reduce_(m.rec_slab.grad)
+    out["rec_loss"] = loss.cpu().numpy()
+    out["rec_grad"] = m.rec_slab.grad.cpu().numpy().copy()
+    # --- one diffusion step, Philox draws keyed by the global row
+    den = m.denoise_model_image
+    U = int(g["U"])
+    users = torch.arange(U, dtype=torch.int32, device=dev)
+    feats = torch.as_tensor(g["dif_feats"]).to(dev)
+    ie = torch.as_tensor(g["dif_item_embeds"]).to(dev)
+    a, b = dist.shard(U)
+    diff, gc = m.diffusion_step(den, users[a:b], feats, ie, 7, norm_rows=U, row0=a)
+    tot = torch.stack([diff.sum(), gc.sum()]).view(2)
+    dist.all_reduce_(tot)
+    dist.all_reduce_(den.slab.grad)
+    out["dif_loss"] = tot.cpu().numpy()
+    out["dif_grad"] = den.slab.grad.cpu().numpy().copy()
+    # --- trainer: diffusion phase + BPR epoch (UI graphs fixed to the golden ones)
+    cfg = tiny_config()
+    I = int(g["I"])
+    ds = RecDataset.from_arrays(cfg, g["train_rows"], g["train_cols"], np.zeros(len(g["train_rows"])), U, I,
+                                g["v_feat"], g["t_feat"])
+    tl = TrainDataLoader(cfg, ds, batch_size=cfg["train_batch_size"])
+    m2 = build_model(g)
+    tr = DiffMMTrainer(cfg, m2)
+    steps = tr.diffusion_phase(0)
+    out["dif_steps"] = np.array([steps])
+    out["dif_epoch_loss"] = tr._dloss.cpu().numpy()
+    out["den_img"] = m2.denoise_model_image.slab.data.cpu().numpy().copy()
+    out["den_txt"] = m2.denoise_model_text.slab.data.cpu().numpy().copy()
+    rec_loss, _ = Trainer._train_epoch(tr, tl, 0)
+    out["bpr_epoch_loss"] = np.array([rec_loss])
+    out["rec_params"] = m2.rec_slab.data.cpu().numpy().copy()
+    return out
+
+
+def _worker(rank, world, port, q):
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "generative-multimodal-recommendation_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, pth)
+    import torch.distributed as tdist
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        res = _case()
+        if rank == 0:
+            q.put(res)
+        tdist.barrier()
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_dp2_step_equals_single_process():
+    import torch.multiprocessing as mp
+    single = _case()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    dp = q.get(timeout=200)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    g = _golden()
+    # the single-process step is the reference's (golden) step
+    np.testing.assert_allclose(single["rec_loss"][0], g["rec_loss"], rtol=1e-5)
+    np.testing.assert_allclose(dp["rec_loss"], single["rec_loss"], rtol=1e-5)
+    np.testing.assert_allclose(dp["rec_grad"], single["rec_grad"], rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(dp["dif_loss"], single["dif_loss"], rtol=1e-5)
+    sc = float(np.abs(single["dif_grad"]).max())
+    np.testing.assert_allclose(dp["dif_grad"], single["dif_grad"], rtol=2e-4, atol=2e-6 * max(1.0, sc))
+    # epoch level: the same number of optimiser steps, parameters within the Adam-amplified fp32 noise
+    assert dp["dif_steps"][0] == single["dif_steps"][0]
+    np.testing.assert_allclose(dp["dif_epoch_loss"], single["dif_epoch_loss"], rtol=1e-5)
+    for k in ("den_img", "den_txt", "rec_params"):
+        np.testing.assert_allclose(dp[k], single[k], rtol=1e-3, atol=2e-5, err_msg=k)
+    np.testing.assert_allclose(dp["bpr_epoch_loss"], single["bpr_epoch_loss"], rtol=1e-5)

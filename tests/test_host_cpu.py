@@ -31,7 +31,7 @@ def test_library_exports_every_symbol():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     missing = [s for s in _header_symbols() if not hasattr(lib, s)]
     assert not missing, missing
-    assert lib.gmr_version() == 1
+    assert lib.gmr_version() == 2
     # pure host helpers are callable without a GPU
     f = lib.gmr_spmm_plan_words
     f.restype = ctypes.c_int64
