@@ -49,7 +49,8 @@ def _case():
     dev = "cuda"
     out = {}
     t = lambda k: torch.as_tensor(g[k].astype(np.int32)).to(dev)  # noqa: E731
-    # --- one rec step
+    # --- one rec step (the text denoiser keeps its seeded init: same CPU RNG state in every process)
+    torch.manual_seed(999)
     m = build_model(g)
     u, p, n = t("bpr_users"), t("bpr_pos"), t("bpr_neg")
     B = u.numel()
@@ -79,6 +80,7 @@ def _case():
     ds = RecDataset.from_arrays(cfg, g["train_rows"], g["train_cols"], np.zeros(len(g["train_rows"])), U, I,
                                 g["v_feat"], g["t_feat"])
     tl = TrainDataLoader(cfg, ds, batch_size=cfg["train_batch_size"])
+    torch.manual_seed(999)
     m2 = build_model(g)
     tr = DiffMMTrainer(cfg, m2)
     steps = tr.diffusion_phase(0)
