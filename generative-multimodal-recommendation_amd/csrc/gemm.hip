@@ -15,9 +15,14 @@
 // conflict-free ds_read_b32.  Register-staged double buffer, one barrier per k-tile.
 // Split-K (grid.z) writes fp32 partial slabs that a second pass sums in slab order
 // (deterministic) and then applies the epilogue.
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "gmr_common.h"
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -168,7 +173,17 @@ __device__ __forceinline__ float4 frag4(const float* s, int row, int h, int q) {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, bool VEC>
+// MF = 32: v_mfma_f32_32x32x2_f32 (lane l: row l&31, k half l>>5);
+// MF = 16: v_mfma_f32_16x16x4_f32 (lane l: row l&15, k quarter l>>4; k = 8*(l>>4) + step, so a
+// lane's 8 steps of a 32-deep tile are two float4 LDS reads).  Same tiles, loads and epilogue.
+// 16x16x4 fragment: rows [row], k = k0 .. k0 + 3
+template <bool KC, int LD>
+__device__ __forceinline__ float4 frag16(const float* s, int row, int k0) {
+  if (KC) return *reinterpret_cast<const float4*>(s + row * LD + k0);
+  return make_float4(s[(k0 + 0) * LD + row], s[(k0 + 1) * LD + row], s[(k0 + 2) * LD + row], s[(k0 + 3) * LD + row]);
+}
+
+template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, bool VEC, int MF>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t N, int64_t K,
                                                              const float* __restrict__ A, int64_t lda,
                                                              const float* __restrict__ B, int64_t ldb,
@@ -176,7 +191,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t
                                                              int64_t k_per_split, float* __restrict__ ws) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;  // wave tile
-  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int TM = WTM / MF, TN = WTN / MF;
+  using AccT = typename std::conditional<MF == 32, floatx16, floatx4>::type;
+  constexpr int NE = MF == 32 ? 16 : 4;
   using SA = Stage<BM, AKC, VEC, NT>;
   using SB = Stage<BN, BKC, VEC, NT>;
   __shared__ __attribute__((aligned(16))) float smem[2 * (SA::WORDS + SB::WORDS)];
@@ -195,15 +212,16 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int wm = w / WGN, wn = w % WGN;
-  const int h = lane >> 5, l32 = lane & 31;
+  const int h = MF == 32 ? lane >> 5 : lane >> 4;     // k group of the lane
+  const int l32 = MF == 32 ? lane & 31 : lane & 15;   // row / column of the lane inside a fragment
 
-  floatx16 acc[TM][TN];
+  AccT acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
 
   SA ra;
   SB rb;
@@ -223,22 +241,41 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t
     }
     const float* a_s = smem + cur * STAGE_WORDS;
     const float* b_s = a_s + SA::WORDS;
+    if constexpr (MF == 32) {
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      float4 fa[TM], fb[TN];
+      for (int qq = 0; qq < 4; ++qq) {
+        float4 fa[TM], fb[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = frag4<AKC, SA::LD>(a_s, wm * WTM + i * 32 + l32, h, qq);
+        for (int i = 0; i < TM; ++i) fa[i] = frag4<AKC, SA::LD>(a_s, wm * WTM + i * 32 + l32, h, qq);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = frag4<BKC, SB::LD>(b_s, wn * WTN + j * 32 + l32, h, qq);
+        for (int j = 0; j < TN; ++j) fb[j] = frag4<BKC, SB::LD>(b_s, wn * WTN + j * 32 + l32, h, qq);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].x, fb[j].x, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].y, fb[j].y, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].z, fb[j].z, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
-        }
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].x, fb[j].x, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].y, fb[j].y, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].z, fb[j].z, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
+          }
+      }
+    } else {
+      // k = 8h + 4g + s: frag16 reads the 4 consecutive k of step group g
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        float4 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = frag16<AKC, SA::LD>(a_s, wm * WTM + i * 16 + l32, 8 * h + 4 * g);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = frag16<BKC, SB::LD>(b_s, wn * WTN + j * 16 + l32, 8 * h + 4 * g);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+      }
     }
     if (more) {
       ra.store(smem + (cur ^ 1) * STAGE_WORDS);
@@ -254,11 +291,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int64_t n = n0 + wn * WTN + j * 32 + l32;
+        const int64_t n = n0 + wn * WTN + j * MF + l32;
         if (n >= N) continue;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int64_t m = m0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        for (int e = 0; e < NE; ++e) {
+          const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
           if (m < M) ws[((int64_t)blockIdx.z * M + m) * N + n] = acc[i][j][e];
         }
       }
@@ -271,12 +308,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int64_t n = n0 + wn * WTN + j * 32 + l32;
+        const int64_t n = n0 + wn * WTN + j * MF + l32;
         if (n >= N) continue;
         const float b = epi.bias ? epi.bias[n] : 0.f;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int64_t m = m0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        for (int e = 0; e < NE; ++e) {
+          const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
           if (m < M) C[m * ldc + n] = epi_fin(epi, acc[i][j][e], b, 0.f, 0.f, 0.f);
         }
       }
@@ -286,19 +323,19 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int64_t n = n0 + wn * WTN + j * 32 + l32;
+      const int64_t n = n0 + wn * WTN + j * MF + l32;
       if (n >= N) continue;
-      float bv[16], xv[16];
+      float bv[NE], xv[NE];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {  // all loads of the 16 elements first (no store in between)
-        const int64_t m = m0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      for (int e = 0; e < NE; ++e) {  // all loads of the 16 elements first (no store in between)
+        const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
         const bool ok = m < M;
         bv[e] = (epi.bias && ok) ? epi.bias[(epi.bias_row ? (int64_t)epi.bias_row[m] : 0) * epi.ld_bias + n] : 0.f;
         xv[e] = (rx && ok) ? *epi_x_ptr(epi, C, ldc, m, n) : 0.f;
       }
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int64_t m = m0 + wm * WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      for (int e = 0; e < NE; ++e) {
+        const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
         if (m < M) C[m * ldc + n] = epi_fin(epi, acc[i][j][e], bv[e], xv[e], epi_r1(epi, m), epi_r2(epi, m));
       }
     }
@@ -324,41 +361,65 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const flo
   C[m * ldc + n] = epi_apply(epi, s, m, n, C, ldc);
 }
 
-template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC>
+template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int MF>
 void launch_t(bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
               const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n, int64_t kps,
               float* ws) {
   const dim3 blk(64 * WGM * WGN);
   if (vec)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, AKC, BKC, true>), grid, blk, 0, st, M, N, K, A, lda, B, ldb, C,
-                       ldc, epi, tiles_n, kps, ws);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, AKC, BKC, true, MF>), grid, blk, 0, st, M, N, K, A, lda, B, ldb,
+                       C, ldc, epi, tiles_n, kps, ws);
   else
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, AKC, BKC, false>), grid, blk, 0, st, M, N, K, A, lda, B, ldb, C,
-                       ldc, epi, tiles_n, kps, ws);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, AKC, BKC, false, MF>), grid, blk, 0, st, M, N, K, A, lda, B, ldb,
+                       C, ldc, epi, tiles_n, kps, ws);
+}
+
+template <int BM, int BN, int WGM, int WGN, int MF>
+void launch_mf(int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A,
+               int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n,
+               int64_t kps, float* ws) {
+  // AKC = A is k-contiguous (not transposed); BKC = B is k-contiguous (transposed)
+  if (!ta && tb)
+    launch_t<BM, BN, WGM, WGN, true, true, MF>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+  else if (!ta && !tb)
+    launch_t<BM, BN, WGM, WGN, true, false, MF>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+  else if (ta && !tb)
+    launch_t<BM, BN, WGM, WGN, false, false, MF>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+  else
+    launch_t<BM, BN, WGM, WGN, false, true, MF>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
 }
 
 template <int BM, int BN, int WGM, int WGN>
-void launch_tile(int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A,
-                 int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n,
-                 int64_t kps, float* ws) {
-  // AKC = A is k-contiguous (not transposed); BKC = B is k-contiguous (transposed)
-  if (!ta && tb)
-    launch_t<BM, BN, WGM, WGN, true, true>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
-  else if (!ta && !tb)
-    launch_t<BM, BN, WGM, WGN, true, false>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
-  else if (ta && !tb)
-    launch_t<BM, BN, WGM, WGN, false, false>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+void launch_tile(int mf, int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K,
+                 const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi,
+                 int tiles_n, int64_t kps, float* ws) {
+  if (mf == 16)
+    launch_mf<BM, BN, WGM, WGN, 16>(ta, tb, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
   else
-    launch_t<BM, BN, WGM, WGN, false, true>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+    launch_mf<BM, BN, WGM, WGN, 32>(ta, tb, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
 }
 
-// Tile and split-K choice of gmr_gemm_f32 (tile / split_k = 0: automatic).
+// Tile, MFMA shape and split-K choice of gmr_gemm_f32 (tile / split_k = 0: automatic).
+// tile | GMR_GEMM_MFMA16 / GMR_GEMM_MFMA32 forces the MFMA shape; otherwise the environment variable
+// GMR_GEMM_MFMA (16 or 32, read once) or the built-in default.
 struct Plan {
-  int tile, bm, bn, splits;
+  int tile, bm, bn, splits, mf;
   int64_t tm, tn, kps;
 };
 
+int default_mfma() {
+  static int mf = [] {
+    const char* e = getenv("GMR_GEMM_MFMA");
+    return (e && atoi(e) == 16) ? 16 : 32;
+  }();
+  return mf;
+}
+
 Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int split_k) {
+  int mf = default_mfma();
+  if (tile & GMR_GEMM_MFMA16) mf = 16;
+  if (tile & GMR_GEMM_MFMA32) mf = 32;
+  tile &= ~(GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32);
   if (tile == 0) {
     // measured on MI355X (scripts/gemm_bench.py): 256^2 tiles win the long-K products of the
     // denoiser (M >= 2048, N >= 1000, K >= 4096; one 16-wave block per CU), 128^2 the wide
@@ -373,6 +434,7 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
     else tile = 64;
   }
   Plan p;
+  p.mf = mf;
   p.tile = tile;
   p.bm = tile == 256128 ? 256 : tile == 128256 ? 128 : tile;
   p.bn = tile == 256128 ? 128 : tile == 128256 ? 256 : tile;
@@ -413,8 +475,11 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
             epilogue == GMR_EPI_DRELU) || aux,
           "epilogue needs aux");
   GMR_ARG(epilogue != GMR_EPI_ROWSCALE_AUX || rowvec1, "epilogue needs rowvec1");
-  GMR_ARG(tile == 0 || tile == 64 || tile == 128 || tile == 256 || tile == 256128 || tile == 128256,
-          "tile must be 0 (auto), 64, 128, 256, 256128 or 128256");
+  {
+    const int t = tile & ~(GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32);
+    GMR_ARG(t == 0 || t == 64 || t == 128 || t == 256 || t == 256128 || t == 128256,
+            "tile must be 0 (auto), 64, 128, 256, 256128 or 128256 (| GMR_GEMM_MFMA16 / GMR_GEMM_MFMA32)");
+  }
   Epi e;
   e.kind = epilogue;
   e.alpha = alpha;
@@ -443,19 +508,19 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   dim3 grid((unsigned)(tm * tn), 1, (unsigned)splits);
   switch (tile) {
     case 256:
-      launch_tile<256, 256, 4, 4>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<256, 256, 4, 4>(pl.mf, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
       break;
     case 256128:
-      launch_tile<256, 128, 4, 2>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<256, 128, 4, 2>(pl.mf, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
       break;
     case 128256:
-      launch_tile<128, 256, 2, 4>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<128, 256, 2, 4>(pl.mf, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
       break;
     case 128:
-      launch_tile<128, 128, 2, 2>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<128, 128, 2, 2>(pl.mf, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
       break;
     default:
-      launch_tile<64, 64, 2, 2>(trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<64, 64, 2, 2>(pl.mf, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
   }
   GMR_LAUNCHED();
   if (ws) {

@@ -38,6 +38,8 @@ extern "C" {
 #define GMR_EPI_DTANH 5        /* C = alpha*acc * (1 - aux[m,n]^2)      tanh backward      */
 #define GMR_EPI_ROWSCALE_AUX 6 /* C = alpha*acc + bias + rv1[m]*aux[m,n]                  */
 #define GMR_EPI_BIAS_RELU 7    /* C = relu(alpha*acc + bias)        TransformerDecoderLayer FF */
+#define GMR_GEMM_MFMA16 (1 << 24)
+#define GMR_GEMM_MFMA32 (1 << 25)
 #define GMR_EPI_DRELU 8        /* C = aux[m,n] > 0 ? alpha*acc : 0  ReLU (+ dropout) backward  */
 
 const char* gmr_last_error_string(void);
@@ -132,7 +134,8 @@ int gmr_topk_to_user_csr(int64_t n_users, int32_t k, const int32_t* topk, int64_
  * C[M,N] = epilogue(alpha * op(A) op(B)); op(A) = A (M x K, lda) or A^T (A stored K x M);
  * op(B) = B (K x N, ldb) or B^T (B stored N x K).  bias[(bias_row ? bias_row[m] : 0)*ld_bias + n].
  * Replaces nn.Linear / torch.mm / matmul: diffmm.py:117,124,277,352-358,472-473; vbpr.py:70,105.
- * tile: 0 auto, 64, 128, 256, 256128 (256 x 128) or 128256; split_k: 0 auto, else >= 1.
+ * tile: 0 auto, 64, 128, 256, 256128 (256 x 128) or 128256, optionally | GMR_GEMM_MFMA16 (v_mfma_f32_16x16x4_f32)
+ * or | GMR_GEMM_MFMA32 (v_mfma_f32_32x32x2_f32) to force the matrix instruction; split_k: 0 auto, else >= 1.
  * gmr_gemm_workspace_floats returns the exact scratch the same call needs (splits*M*N floats of
  * split-K partials, 0 when it does not split). */
 int64_t gmr_gemm_workspace_floats(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, int32_t tile,

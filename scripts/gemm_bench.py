@@ -13,6 +13,8 @@ import torch  # noqa: E402
 
 from gmr import kernels as K  # noqa: E402
 
+MF_FLAG = {32: 1 << 25, 16: 1 << 24}  # GMR_GEMM_MFMA32 / GMR_GEMM_MFMA16 (include/gmr.h)
+
 # name, M, N, K, trans_a, trans_b, calls per epoch
 SHAPES = [
     ("square4096 (NT)", 4096, 4096, 4096, 0, 1, 0),
@@ -58,8 +60,10 @@ def run(args):
         B = torch.randn((N, r4(Kd)) if tb else (Kd, r4(N)), device=dev)[:, :(Kd if tb else N)]
         C = torch.empty((M, r4(N)), device=dev)[:, :N]
         best = None
-        for tile in args.tiles:
-          for split in args.splits:
+        for tile0 in args.tiles:
+          for mf in args.mfma:
+           tile = tile0 | (MF_FLAG[mf] if tile0 else 0)
+           for split in args.splits:
             for _ in range(3):
                 K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=split)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -70,7 +74,7 @@ def run(args):
             torch.cuda.synchronize()
             us = 1e3 * s.elapsed_time(e) / args.reps
             tf = 2.0 * M * N * Kd / (us * 1e-6) / 1e12
-            print(f"{name:26s} {tile:7d} s{split:<2d} {us:9.1f} {tf:7.1f} {us * calls / 1e3:9.2f}")
+            print(f"{name:26s} {tile0:7d} m{mf} s{split:<2d} {us:9.1f} {tf:7.1f} {us * calls / 1e3:9.2f}", flush=True)
             best = us if best is None else min(best, us)
         tot_ms += best * calls / 1e3
     print(f"total GEMM ms/epoch (best tile per shape): {tot_ms:.1f}")
@@ -82,7 +86,9 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--splits", default="0")
     ap.add_argument("--only", default="", help="substring filter on shape names")
+    ap.add_argument("--mfma", default="32", help="MFMA shapes to try: 32 (32x32x2) and/or 16 (16x16x4)")
     a = ap.parse_args()
     a.tiles = [int(t) for t in a.tiles.split(",")]
     a.splits = [int(t) for t in a.splits.split(",")]
+    a.mfma = [int(t) for t in a.mfma.split(",")]
     run(a)

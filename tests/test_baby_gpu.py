@@ -1,0 +1,188 @@
+"""DiffMM at the north-star shape (Amazon-baby-shaped synthetic data, SURVEY.md 8d: 19,445 users x
+7,050 items, H = 1,000, image 4,096-d, text 384-d) against the reference's own outputs on the same
+inputs (tests/golden/diffmm_baby.npz + diffmm_baby_meta.json, made by make_golden_baby.py by
+running the reference in the build container).
+
+Checked through the HIP path:
+  * D2   parameter initialisation: SHA-256 of every rec and denoiser parameter equals the
+         reference's after init_seed(999) (models/diffmm.py:42-79: the CPU RNG order) - bit-exact;
+  * D13/D17 p_sample (steps 0, no noise) of both denoisers over all users + top-1: the reference's
+         top-1 item for every user except inside near-tie groups of the reference's own values;
+  * D9/D19 full_sort_predict + mask + top-50 on the valid split: equal to the reference BY POSITION
+         except where our two candidates' scores tie within 1e-6 relative (fp32 summation order);
+         scores of the reference's top-50 within fp32 tolerance for the stored user sample;
+  * D21  Recall/NDCG/Precision/MAP@{5,10,20,50} (unrounded) within 1e-4 of the reference;
+  * (f)2 the test split with is_test=True: every extra of the reference (Pop/Niche, Cold/Warm,
+         Coverage/Gini/Tail%) within its 4-decimal rounding.
+The UI graphs for the eval checks are built from the reference's top-1 edges, so each check sees
+the reference's inputs.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def baby():
+    from gmr.configurator import Config
+    from gmr.dataloader import EvalDataLoader, TrainDataLoader
+    from gmr.quick_start import popularity_groups
+    from gmr.synthetic import make_dataset
+    from gmr.utils import get_model, get_trainer, init_seed
+    cfg = Config("DiffMM", "baby", {"synthetic": "baby", "save_recommended_topk": False, "epochs": 1})
+    ds = make_dataset(cfg, "baby", seed=0)
+    tr, va, te = ds.split()
+    pop, warm, _, _ = popularity_groups(cfg, tr)
+    cfg["pop_items"], cfg["warm_users"] = pop, warm
+    tl = TrainDataLoader(cfg, tr, batch_size=cfg["train_batch_size"], shuffle=True)
+    vl = EvalDataLoader(cfg, va, additional_dataset=tr, batch_size=cfg["eval_batch_size"])
+    tel = EvalDataLoader(cfg, te, additional_dataset=tr, batch_size=cfg["eval_batch_size"])
+    init_seed(999)
+    model = get_model("DiffMM")(cfg, tl)
+    trainer = get_trainer("DiffMM")(cfg, model)
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "diffmm_baby.npz"), allow_pickle=False))
+    with open(os.path.join(ROOT, "tests", "golden", "diffmm_baby_meta.json")) as f:
+        meta = json.load(f)
+    assert (model.n_users, model.n_items, tl.n_inter) == (meta["U"], meta["I"], meta["n_train"])
+    return {"cfg": cfg, "tl": tl, "vl": vl, "tel": tel, "model": model, "trainer": trainer, "g": g, "meta": meta}
+
+
+def _sha(t):
+    a = np.ascontiguousarray(t.detach().contiguous().cpu().numpy().astype(np.float32))
+    return hashlib.sha256(a.tobytes()).hexdigest()
+
+
+def test_init_matches_reference_bit_exact(baby):
+    m, want = baby["model"], baby["meta"]["param_sha256"]
+    s, U = m.rec_slab, m.n_users
+    got = {"uEmbeds": _sha(s.view("E0")[:U]), "iEmbeds": _sha(s.view("E0")[U:]),
+           "image_trans": _sha(s.view("image_trans")), "text_trans": _sha(s.view("text_trans")),
+           "modal_weight": _sha(s.view("modal_weight"))}
+    names = {"emb_layer.weight": "emb_W", "emb_layer.bias": "emb_b", "in_layers.0.weight": "W1",
+             "in_layers.0.bias": "b1", "out_layers.0.weight": "W2", "out_layers.0.bias": "b2"}
+    for mod in ("image", "text"):
+        den = getattr(m, "denoise_model_" + mod).slab
+        for ref_name, ours in names.items():
+            got[f"den_{mod}_{ref_name}"] = _sha(den.view(ours))
+    assert set(got) == set(want)
+    bad = [k for k in want if got[k] != want[k]]
+    assert not bad, f"parameters differing from the reference init: {bad}"
+
+
+def _near_tie_ok(vals_ref_row, idx_ref_row, ours_item, tol):
+    """ours_item may replace the reference's top-1 only if the reference itself scores it within tol."""
+    hit = np.nonzero(idx_ref_row == ours_item)[0]
+    return len(hit) > 0 and vals_ref_row[0] - vals_ref_row[hit[0]] <= tol * max(1.0, abs(float(vals_ref_row[0])))
+
+
+def test_p_sample_top1_all_users(baby):
+    from gmr import kernels as K
+    m, g = baby["model"], baby["g"]
+    U = m.n_users
+    for mod in ("image", "text"):
+        den = getattr(m, "denoise_model_" + mod)
+        idx = torch.empty((U, 5), dtype=torch.int32, device=DEV)
+        val = torch.empty((U, 5), dtype=torch.float32, device=DEV)
+        den.refresh_w1t()
+        for lo in range(0, U, 8192):
+            hi = min(U, lo + 8192)
+            xi = m.p_sample_topk(den, lo, hi, None, 1, w1t_fresh=True)
+            K.topk_rows(xi, 5, idx[lo:hi], val[lo:hi])
+        idx, val = idx.cpu().numpy(), val.cpu().numpy()
+        ri, rv = g[f"psample_{mod}_top5_idx"].astype(np.int64), g[f"psample_{mod}_top5_val"]
+        # the values of the five best items agree to fp32 accumulation-order tolerance
+        np.testing.assert_allclose(val, rv, rtol=2e-4, atol=2e-5, err_msg=mod)
+        diff = np.nonzero(idx[:, 0] != ri[:, 0])[0]
+        bad = [u for u in diff if not _near_tie_ok(rv[u], ri[u], idx[u, 0], 2e-5)]
+        assert not bad, f"{mod}: top-1 differs outside near ties for {len(bad)} users (first {bad[:5]})"
+        assert len(diff) <= max(5, U // 1000), f"{mod}: {len(diff)} near-tie top-1 swaps"
+
+
+@pytest.fixture(scope="module")
+def ref_graphs(baby):
+    """UI graphs from the reference's top-1 edges (trainer.py:545-576 with the reference's picks)."""
+    from gmr import kernels as K
+    m, g = baby["model"], baby["g"]
+    U, I = m.n_users, m.n_items
+    for mod in ("image", "text"):
+        top = torch.as_tensor(g[f"psample_{mod}_top5_idx"][:, :1].astype(np.int32)).to(DEV)
+        uptr = torch.empty(U + 1, dtype=torch.int32, device=DEV)
+        uitems = torch.empty(U, dtype=torch.int32, device=DEV)
+        K.topk_to_user_csr(top, uptr, uitems)
+        setattr(m, mod + "_UI_matrix", K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0))
+    return True
+
+
+def _eval_with_scores(m, ld, kmax=50, keep_scores=None):
+    """trainer.topk_all's loop (score -> mask -> top-k on the device), keeping score rows for ties."""
+    d = ld.to_device()
+    n, E = ld.pr_end, ld.step
+    usr, itm = m.forward_embeddings()
+    out = torch.empty((n, kmax), dtype=torch.int32, device=DEV)
+    sb = torch.empty((E, (m.n_items + 3) // 4 * 4), dtype=torch.float32, device=DEV)
+    rows_kept = []
+    for lo in range(0, n, E):
+        hi = min(n, lo + E)
+        m0, m1 = int(d["mask_ptr"][lo]), int(d["mask_ptr"][hi])
+        m.topk_from_embeddings(usr, itm, d["eval_u32"][lo:hi], d["mask_rows"][m0:m1] - lo, d["mask_cols"][m0:m1],
+                               kmax, out[lo:hi], sb)
+        rows_kept.append(sb[:hi - lo, :m.n_items].cpu().numpy() if keep_scores else None)
+    return out, (np.concatenate(rows_kept) if keep_scores else None)
+
+
+def test_valid_topk_by_position_and_scores(baby, ref_graphs):
+    m, g = baby["model"], baby["g"]
+    out, scores = _eval_with_scores(m, baby["vl"], keep_scores=True)
+    ours = out.cpu().numpy().astype(np.int64)
+    ref = g["valid_top50"].astype(np.int64)
+    assert ours.shape == ref.shape
+    # scores of the reference's picks (first SAMPLE users) agree to fp32 tolerance
+    S = g["valid_top50_val_sample"].shape[0]
+    mine = np.take_along_axis(scores[:S], ref[:S], 1)
+    np.testing.assert_allclose(mine, g["valid_top50_val_sample"], rtol=1e-5, atol=1e-6)
+    # position-wise equality except inside near-tie groups of our own scores
+    r, c = np.nonzero(ours != ref)
+    s_o = scores[r, ours[r, c]]
+    s_r = scores[r, ref[r, c]]
+    tie = np.abs(s_o - s_r) <= 1e-6 * np.maximum(np.abs(s_o), 1e-3)
+    assert tie.all(), (f"{int((~tie).sum())} top-50 positions differ outside near ties "
+                       f"(first rows {np.unique(r[~tie])[:5]}); {len(r)} differing positions in all")
+    baby["valid_topk"] = out
+
+
+def test_valid_metrics_unrounded(baby, ref_graphs):
+    tr, vl = baby["trainer"], baby["vl"]
+    out = baby.get("valid_topk")
+    if out is None:
+        out, _ = _eval_with_scores(baby["model"], vl)
+    sums = tr.evaluator.device_sums(out, vl).cpu().numpy().reshape(4, 8)
+    n = out.shape[0]
+    raw = baby["meta"]["valid"]["raw"]
+    for j, name in enumerate(["recall", "ndcg", "precision", "map"]):
+        for q, k in enumerate([5, 10, 20, 50]):
+            assert abs(sums[j, q] / n - raw[name][k - 1]) <= 1e-4, (name, k, sums[j, q] / n, raw[name][k - 1])
+    res = tr.evaluator.evaluate_device(out, vl)
+    want = baby["meta"]["valid"]["rounded"]
+    for k, v in want.items():
+        assert abs(res[k] - v) <= 1.01e-4, (k, res[k], v)
+
+
+def test_test_split_extras(baby, ref_graphs):
+    """is_test=True: pop/niche, cold/warm, coverage/gini/tail of the reference (topk_evaluator.py:122-270)."""
+    tr, tel = baby["trainer"], baby["tel"]
+    out, _ = _eval_with_scores(baby["model"], tel)
+    res = tr.evaluator.evaluate_device(out, tel, is_test=True)
+    want = baby["meta"]["test"]["rounded"]
+    missing = sorted(set(want) - set(res))
+    assert not missing, f"extras missing: {missing[:10]}"
+    bad = {k: (res[k], v) for k, v in want.items() if abs(float(res[k]) - float(v)) > 1.01e-4}
+    assert not bad, bad
