@@ -1,18 +1,32 @@
 """Benchmark: DiffMM on Amazon-baby-shaped synthetic data, train users/s (+ full-rank eval users/s).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model diffmm|diffrec|genrecv1] [--no-legs]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
 
-One "step" = one full DiffMM training epoch of the reference's DiffMMTrainer._train_epoch
-(common/trainer.py:487-585): diffusion training of both denoisers over all users, the graph
-rebuild (p_sample + top-1 + normalised UI graphs) and the BPR/contrastive phase over all train
-interactions.  value = users/s = U * steps / wall (max over ranks); after the timed epochs
-full-rank evaluation passes over the valid split are timed as eval users/s.
-Multi-GPU (N > 1): user/batch-sharded data parallelism (gmr/dist.py) — each epoch still covers
-the whole dataset once, split over the ranks (per-GPU batch = train_batch_size), with RCCL
-all-reduces of the gradients and an all-gather of the rebuilt top-k edges.
+One "step" = one full training epoch of the model's reference trainer.  For DiffMM (the headline,
+BASELINE.json) that is DiffMMTrainer._train_epoch (common/trainer.py:487-585): diffusion training
+of both denoisers over all users, the graph rebuild (p_sample + top-1 + normalised UI graphs) and
+the BPR/contrastive phase over all train interactions.  value = users/s = U * steps / wall (max
+over ranks); after the timed epochs full-rank evaluation passes over the valid split are timed
+as eval users/s.
+Multi-GPU (N > 1): data parallelism over the ranks (gmr/dist.py) with the reference's global
+batch: each train_batch_size batch is split over the ranks, RCCL all-reduces the gradients, the
+rebuilt top-k edges are all-gathered; total work per epoch is fixed ("scaling": "strong").
+
+Roofline: after the timed region one more epoch runs with the side streams off (GMR_SERIAL
+semantics, gmr/kernels.py Streams.SERIAL) and every GEMM / SpMM / InfoNCE launch timed by HIP
+events on its stream; per kernel class achieved = algorithmic work (SURVEY.md 8d formulas) /
+summed duration.  `rocprofv3 --kernel-trace --stats` of `GMR_SERIAL=1 python bench.py` gives the
+same per-kernel durations (profiles/).  Memory-side traffic and MFMA busy cycles come from
+rocprofv3 --pmc passes (scripts/pmc_collect.sh) recorded with the SHA-256 of the library they
+measured; a summary of another build is never used (traffic null then).
+
+With no --model the default run adds two legs measured in the same process: DiffRec on the
+baby shape (config 2: train epoch + 100-step p_sample eval) and GenRecV1 on the TikTok shape
+with the fp16 MFMA scoring GEMM (config 5).
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -26,18 +40,32 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "train users/sec + full-rank eval users/sec, DiffMM Amazon-baby, 1/2/4/8 MI355X"
-MODELS = {"diffmm": "DiffMM", "genrecv1": "GenRecV1"}
-DEFAULT_SHAPE = {"diffmm": "baby", "genrecv1": "tiktok"}
+MODELS = {"diffmm": "DiffMM", "genrecv1": "GenRecV1", "diffrec": "DiffRec"}
+DEFAULT_SHAPE = {"diffmm": "baby", "genrecv1": "tiktok", "diffrec": "baby"}
 STEP_DESC = {"diffmm": "one DiffMMTrainer epoch (diffusion train + graph rebuild + BPR/contrastive)",
              "genrecv1": "one GenRecV1Trainer epoch (flip-diffusion train of the transformer denoiser + "
-                         "graph rebuild with interest debiasing + BPR/contrastive)"}
+                         "graph rebuild with interest debiasing + BPR/contrastive)",
+             "diffrec": "one Trainer epoch of DiffRec (training_losses + backward per interaction batch, "
+                        "importance-sampled t)"}
 HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFS = 157.3
+KERNEL_NAMES = {"gemm": "gemm_kernel (fp32 MFMA v_mfma_f32_32x32x2_f32, XCD-aware tiles)",
+                "infonce": "cl_rows_kernel + cl_table_kernel (fused InfoNCE, fp32 MFMA)",
+                "spmm": "spmm_lane_kernel (CSR, XCD column slices, lane group per row; norm_adj packed plan)"}
 
 
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
+
+
+def lib_sha256():
+    from gmr import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
 
 
 def setup(args):
@@ -49,7 +77,7 @@ def setup(args):
 
     name = MODELS[args.model]
     over = {"synthetic": args.shape, "save_recommended_topk": False, "epochs": 1}
-    if args.scoring_dtype:
+    if getattr(args, "scoring_dtype", None):
         if args.model != "genrecv1":
             raise SystemExit("--scoring-dtype applies to GenRecV1 (config 5)")
         over["scoring_dtype"] = args.scoring_dtype
@@ -65,51 +93,48 @@ def setup(args):
     model = get_model(name)(cfg, tl)
     trainer = get_trainer(name)(cfg, model)
     torch.cuda.synchronize()
-    log(f"setup {time.time() - t0:.1f}s: U={ds.user_num} I={ds.item_num} train={len(tr)} valid users={vl.pr_end}")
+    log(f"setup {time.time() - t0:.1f}s: {name} U={ds.user_num} I={ds.item_num} train={len(tr)} "
+        f"valid users={vl.pr_end}")
     return cfg, ds, tr, tl, vl, model, trainer
 
 
-def pmc_traffic(model="diffmm", shape=None):
-    """HBM bytes per launch per kernel class from the newest committed PMC summary of this workload
-    (profiles/*_pmc_traffic.json for DiffMM at its default shape, *_pmc_traffic_<model>[_<shape>].json
-    otherwise; made by scripts/pmc_traffic.sh on the same command).  Another workload's counters are
-    never reused: traffic stays null without a summary of this one."""
+def pmc_summary(model="diffmm", shape=None):
+    """Per-kernel-class memory-side bytes and MFMA busy cycles of this workload from the newest
+    profiles/*_pmc_<tag>.json made by scripts/pmc_collect.sh, used only when it was measured on
+    the library now loaded (same SHA-256)."""
     import glob
-    default = shape in (None, DEFAULT_SHAPE.get(model))
-    tag = model if default else f"{model}_{shape}"
-    pat = "*_pmc_traffic.json" if tag == "diffmm" else f"*_pmc_traffic_{tag}.json"
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)))
+    tag = model if shape in (None, DEFAULT_SHAPE.get(model)) else f"{model}_{shape}"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{tag}.json")))
     if not files:
-        return {}, None
+        return {}, None, "no PMC summary of this workload in profiles/"
     with open(files[-1]) as f:
-        return json.load(f), os.path.relpath(files[-1], ROOT)
-
-
-def spmm_kernel_name():
-    from gmr import kernels as K
-    if K.SPMM_SEG_NNZ & K.SPMM_LANE_PLAN:
-        return (f"spmm_lane_kernel (CSR, XCD column slices, lane group per row, L={K.SPMM_SEG_NNZ & 0xFFFF}; "
-                "norm_adj on the packed lane plan)")
-    return "spmm_seg_kernel (CSR, wave/segment)"
+        d = json.load(f)
+    src = os.path.relpath(files[-1], ROOT)
+    if d.get("lib_sha256") != lib_sha256():
+        return {}, src, f"{src} measured another build (lib_sha256 differs): not used"
+    return d, src, None
 
 
 def summarize_probe(p, model="diffmm", shape=None):
     """Aggregate HIP-event timings per kernel class into roofline objects."""
     out = {}
-    pmc, pmc_src = pmc_traffic(model, shape)
+    pmc, pmc_src, pmc_why = pmc_summary(model, shape)
     for tag, recs in p.items():
         if not recs:
             continue
         ms = [s.elapsed_time(e) for s, e, _ in recs]
         tot_ms = float(np.sum(ms))
-        if tag == "gemm":
-            work = sum(2.0 * r[2][0] * r[2][1] * r[2][2] for r in recs)
+        if tag in ("gemm", "infonce"):
+            if tag == "gemm":
+                work = sum(2.0 * r[2][0] * r[2][1] * r[2][2] for r in recs)
+            else:  # rows pass S = P T^T and U = E T, table pass the same again: 4 B n 64 MACs
+                work = sum(8.0 * r[2][0] * r[2][1] * 64 for r in recs)
             achieved = work / (tot_ms * 1e-3) / 1e12
             out[tag] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": round(achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
                         "launches": len(recs), "avg_us": round(1e3 * tot_ms / len(recs), 2),
                         "total_ms": round(tot_ms, 3), "algorithmic_per_launch": work / len(recs),
-                        "kernel": "gemm_kernel (fp32 MFMA 32x32x2)"}
+                        "algorithmic_unit": "flop", "kernel": KERNEL_NAMES[tag]}
         else:
             # SURVEY.md 8(d): bytes = 8 nnz + 4 (n_rows+1) + 4 d n_cols (X once) + 4 d n_rows (Y once [+ read if beta])
             byts = 0.0
@@ -120,12 +145,18 @@ def summarize_probe(p, model="diffmm", shape=None):
             out[tag] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "launches": len(recs),
                         "avg_us": round(1e3 * tot_ms / len(recs), 2), "total_ms": round(tot_ms, 3),
-                        "algorithmic_per_launch": byts / len(recs), "kernel": spmm_kernel_name()}
+                        "algorithmic_per_launch": byts / len(recs), "algorithmic_unit": "bytes",
+                        "kernel": KERNEL_NAMES[tag]}
     for tag, o in out.items():
-        if tag in pmc:
-            o["traffic"] = round(pmc[tag]["traffic_per_launch"])
+        c = pmc.get(tag) if pmc else None
+        if c:
+            o["traffic"] = round(c["traffic_per_launch"])
             o["traffic_unit"] = "bytes/launch (memory side: 2 x FETCH_SIZE + WRITE_SIZE)"
-            o["traffic_source"] = pmc_src
+            if c.get("mfma_util") is not None:
+                o["mfma_util"] = round(c["mfma_util"], 4)
+            o["pmc_source"] = pmc_src
+        elif pmc_why:
+            o["pmc_note"] = pmc_why
     return out
 
 
@@ -145,9 +176,20 @@ def report_shapes(p):
             log(f"  {str(meta):44s} n={len(ms):4d} total={tot:8.2f} ms avg={1e3 * tot / len(ms):8.1f} us {extra}")
 
 
-def cpu_baseline(model, tl, budget_s=30.0):
+def _median_time(fn, reps):
+    fn()  # warm (allocator, MKL/oneDNN kernels)
+    ts = []
+    for _ in range(reps):
+        t0 = time.time()
+        fn()
+        ts.append(time.time() - t0)
+    return float(np.median(ts)), ts
+
+
+def cpu_baseline(model, tl, reps=3):
     """Oracle (torch-CPU restatement) timed on the host: one BPR step, one diffusion batch and one
-    p_sample batch at the baby shape, extrapolated to a full epoch (train users/s)."""
+    p_sample batch at the baby shape, each the median of `reps` timed runs after a warm run,
+    extrapolated to a full epoch (train users/s)."""
     from oracle import graph_ref, model_ref
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
@@ -168,10 +210,12 @@ def cpu_baseline(model, tl, budget_s=30.0):
     users = torch.as_tensor(rng.integers(0, U, B))
     pos = torch.as_tensor(rng.integers(0, I, B))
     neg = torch.as_tensor(rng.integers(0, I, B))
-    t0 = time.time()
-    loss = model_ref.rec_loss(p, feats, adj, iadj, tadj, users, pos, neg)
-    loss.backward()
-    t_bpr = time.time() - t0
+
+    def bpr():
+        for v in p.values():
+            v.grad = None
+        model_ref.rec_loss(p, feats, adj, iadj, tadj, users, pos, neg).backward()
+    t_bpr, s_bpr = _median_time(bpr, reps)
     den = model.denoise_model_image.slab
     w = {"emb_W": den.view("emb_W").cpu(), "emb_b": den.view("emb_b").cpu(), "W1": den.view("W1").cpu().contiguous(),
          "b1": den.view("b1").cpu(), "W2": den.view("W2").cpu().contiguous(), "b2": den.view("b2").cpu()}
@@ -181,82 +225,104 @@ def cpu_baseline(model, tl, budget_s=30.0):
     for b in range(B):
         x0[b, tl.uitems_np[tl.uptr_np[b]:tl.uptr_np[b + 1]]] = 1.0
     ts = rng.integers(0, 5, B)
-    t0 = time.time()
-    diff, gc = model_ref.diffmm_training_losses(w, tab, x0, ts, torch.randn(B, I), (torch.rand(B, I) < 0.5).float(),
-                                                p["iEmbeds"].detach(), torch.randn(I, 64))
-    (diff.mean() + 0.5 * gc.mean()).backward()
-    t_dif = 2 * (time.time() - t0)  # image + text denoisers
-    t0 = time.time()
-    with torch.no_grad():
-        model_ref.diffmm_p_sample({k: v.detach() for k, v in w.items()}, tab, x0)
-    t_ps = 2 * (time.time() - t0)
+    noise, keep, gfe = torch.randn(B, I), (torch.rand(B, I) < 0.5).float(), torch.randn(I, 64)
+
+    def dif():
+        for v in w.values():
+            v.grad = None
+        diff, gc = model_ref.diffmm_training_losses(w, tab, x0, ts, noise, keep, p["iEmbeds"].detach(), gfe)
+        (diff.mean() + 0.5 * gc.mean()).backward()
+    t_dif1, s_dif = _median_time(dif, reps)
+    t_dif = 2 * t_dif1  # image + text denoisers
+
+    def ps():
+        with torch.no_grad():
+            model_ref.diffmm_p_sample({k: v.detach() for k, v in w.items()}, tab, x0)
+    t_ps1, s_ps = _median_time(ps, reps)
+    t_ps = 2 * t_ps1
     n_bpr = -(-tl.n_inter // B)
     n_dif = -(-U // B)
     epoch = t_bpr * n_bpr + t_dif * n_dif + t_ps * n_dif
+    fmt = lambda xs: "/".join(f"{x:.2f}" for x in xs)  # noqa: E731
     return {"value": round(U / epoch, 2), "unit": "users/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (torch-CPU fp32 restatement): 1 BPR+contrastive step (B=2048, fwd+bwd) = {t_bpr:.2f}s, "
-                      f"1 diffusion batch x2 denoisers = {t_dif:.2f}s, 1 p_sample batch x2 = {t_ps:.2f}s; "
-                      f"extrapolated to {n_bpr} BPR + {n_dif} diffusion + {n_dif} p_sample batches = {epoch:.1f}s/epoch"}
+            "sample": f"oracle (torch-CPU fp32 restatement), median of {reps} timed runs after a warm run: "
+                      f"1 BPR+contrastive step (B=2048, fwd+bwd) = {t_bpr:.2f}s ({fmt(s_bpr)}), "
+                      f"1 diffusion batch x2 denoisers = {t_dif:.2f}s ({fmt(s_dif)} per denoiser), "
+                      f"1 p_sample batch x2 = {t_ps:.2f}s ({fmt(s_ps)} per denoiser); extrapolated to {n_bpr} BPR + "
+                      f"{n_dif} diffusion + {n_dif} p_sample batches = {epoch:.1f}s/epoch"}
 
 
-def cpu_baseline_genrec(model, tl, trainer):
-    """Oracle (oracle/genrec_ref.py, torch-CPU fp32) timed on the host: one BPR step, one diffusion
-    batch (training_losses fwd+bwd incl. its p_sample) and one rebuild p_sample batch at the shape,
-    extrapolated to a GenRecV1Trainer epoch (train users/s)."""
-    from oracle import genrec_ref, graph_ref, model_ref
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    U, I, B = model.n_users, model.n_items, 2048
-    N = U + I
-    s = model.rec_slab
-    p = {n: s.view(n).cpu().clone().requires_grad_(True) for n in model._pnames}
-    p["user_embedding_weight"] = s.view("E0")[:U].cpu().clone().requires_grad_(True)
-    p["item_id_embedding_weight"] = s.view("E0")[U:].cpu().clone().requires_grad_(True)
-    feats = {"image": model.v_feat.cpu(), "text": model.t_feat.cpu()}
-    rows = np.repeat(np.arange(U), np.diff(tl.uptr_np))
-    rng = np.random.default_rng(0)
-    sp = lambda c, n, m: model_ref.sparse_from_csr(*c, n, m)  # noqa: E731
-    graphs = {"norm_adj": sp(graph_ref.norm_adj_csr(U, I, rows, tl.uitems_np), N, N),
-              "R": sp(genrec_ref.user_item_csr(U, I, rows, tl.uitems_np), U, I)}
-    ui = graph_ref.ui_adj_csr(U, I, np.repeat(np.arange(U), 10), rng.integers(0, I, 10 * U))
-    graphs["ui_img"] = sp(genrec_ref.drop_edges_csr(*ui, rng.random(len(ui[1])) < 0.5), N, N)
-    for key, f in (("ii_img", feats["image"]), ("ii_txt", feats["text"])):
-        graphs[key] = sp(genrec_ref.knn_graph_csr(f.numpy(), 10)[0], I, I)
-    state = {n: (torch.zeros(64), torch.ones(64)) for n in
-             ["image_residual_project_1", "image_modal_project_1", "text_residual_project_1", "text_modal_project_1",
-              "caculate_common_1", "gate_image_modal_1", "gate_text_modal_1"]}
-    users = torch.as_tensor(rng.integers(0, U, B))
-    pos, neg = torch.as_tensor(rng.integers(0, I, B)), torch.as_tensor(rng.integers(0, I, B))
+def run_workload(args, dist_on, barrier, max_over_ranks, with_cpu_baseline):
+    """Setup, warmup, timed epochs, eval passes and the serial roofline epoch of one model."""
+    from gmr import kernels as K
+    cfg, ds, tr, tl, vl, model, trainer = setup(args)
+    U = model.n_users
+    for i in range(args.warmup):
+        t0 = time.time()
+        trainer._train_epoch(tl, i)
+        torch.cuda.synchronize()
+        log(f"warmup epoch {i}: {time.time() - t0:.3f}s")
+    barrier()
     t0 = time.time()
-    genrec_ref.calculate_loss(p, feats, graphs, state, users, pos, neg).backward()
-    t_bpr = time.time() - t0
-    den = model.denoise_model_image
-    w = {n: den.v(n).cpu().clone().requires_grad_(True) for n in den.names}
-    w["input_proj_weight"] = den.v("input_proj_weight").cpu().contiguous().clone().requires_grad_(True)
-    x0 = torch.zeros(B, I)
-    for b in range(B):
-        x0[b, tl.uitems_np[tl.uptr_np[b]:tl.uptr_np[b + 1]]] = 1.0
-    g, e = genrec_ref.flip_schedule(x0)
-    ts = rng.integers(0, 5, B)
-    flips = [(torch.rand(B, I) < 0.4).float().numpy() for _ in range(2)]
-    draws = [(torch.rand(B, I) < 0.3).float().numpy() for _ in range(5)]
+    for i in range(args.steps):
+        trainer._train_epoch(tl, args.warmup + i)
+    barrier()
+    dt = max_over_ranks(time.time() - t0)
+    train_ups = U * args.steps / dt
+
+    trainer.evaluate(vl)
+    barrier()
     t0 = time.time()
-    total = genrec_ref.training_losses(w, x0, ts, flips[0], p["item_id_embedding_weight"].detach(), torch.randn(I, 64),
-                                       flips[1], draws, g, e, den.L)[0]
-    total.backward()
-    t_dif = time.time() - t0
-    t0 = time.time()
-    with torch.no_grad():
-        genrec_ref.p_sample({k: v.detach() for k, v in w.items()}, x0, g, e, flips[0], draws, den.L)
-    t_ps = time.time() - t0
-    n_bpr = -(-tl.n_inter // B)
-    n_dif = -(-U // B)
-    epoch = t_bpr * n_bpr + (t_dif + t_ps) * n_dif
-    return {"value": round(U / epoch, 2), "unit": "users/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (torch-CPU fp32 restatement of GenRecV1): 1 BPR+InfoNCE step (B=2048, fwd+bwd) = "
-                      f"{t_bpr:.2f}s, 1 diffusion batch (training_losses incl. its p_sample, fwd+bwd) = {t_dif:.2f}s, "
-                      f"1 rebuild p_sample batch = {t_ps:.2f}s; extrapolated to {n_bpr} BPR + {n_dif} diffusion + "
-                      f"{n_dif} rebuild batches = {epoch:.1f}s/epoch"}
+    for _ in range(args.eval_passes):
+        res = trainer.evaluate(vl)
+    barrier()
+    et = max_over_ranks(time.time() - t0)
+    eval_ups = vl.pr_end * args.eval_passes / et
+
+    roof = None
+    if not args.no_probe:
+        # one more epoch, side streams off, every GEMM / SpMM / InfoNCE launch timed on its stream
+        serial = K.Streams.SERIAL
+        K.Streams.SERIAL = True
+        K.probe_begin(["gemm", "spmm", "infonce"])
+        t1 = time.time()
+        trainer._train_epoch(tl, args.warmup + args.steps)
+        torch.cuda.synchronize()
+        serial_ms = 1e3 * (time.time() - t1)
+        raw = K.probe_end()
+        K.Streams.SERIAL = serial
+        roof = summarize_probe(raw, args.model, args.shape)
+        if os.environ.get("GMR_PROBE_REPORT"):
+            report_shapes(raw)
+        mfma_flop = sum(o["algorithmic_per_launch"] * o["launches"] for o in roof.values() if o["bound"] == "mfma")
+        for o in roof.values():
+            o["probe_scope"] = ("one extra epoch after the timed region with the side streams off (GMR_SERIAL): "
+                                "HIP events around every launch of the class on its stream")
+        roof["_epoch"] = {"mfma_flop_per_epoch": mfma_flop, "serial_epoch_ms": round(serial_ms, 2),
+                          "epoch_mfma_frac": round(mfma_flop / (1e-3 * dt / args.steps) / 1e12 / FP32_MFMA_PEAK_TFS, 4),
+                          "note": "algorithmic GEMM + InfoNCE flop of one epoch / timed ms_per_step / fp32 MFMA peak"}
+    out = {"model": MODELS[args.model], "shape": args.shape, "U": U, "I": model.n_items, "n_inter": tl.n_inter,
+           "train_users_per_s": round(train_ups, 1), "ms_per_step": round(1e3 * dt / args.steps, 2),
+           "eval_users_per_s": round(eval_ups, 1), "eval_recall@20": res.get("recall@20"),
+           "eval_scoring_dtype": getattr(model, "scoring_dtype", "fp32"), "roofline_by_kernel": roof,
+           "global_batch": cfg["train_batch_size"], "eval_batch": cfg["eval_batch_size"]}
+    if with_cpu_baseline and args.model == "diffmm":
+        try:
+            out["cpu_baseline"] = cpu_baseline(model, tl)
+        except Exception as e:  # noqa: BLE001
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    del trainer, model
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def dominant(roof):
+    if not roof:
+        return None, None
+    cls = {k: v for k, v in roof.items() if not k.startswith("_")}
+    name = max(cls, key=lambda k: cls[k]["total_ms"])
+    return name, cls[name]
 
 
 def main():
@@ -264,14 +330,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--model", default="diffmm", choices=sorted(MODELS))
-    ap.add_argument("--shape", default=None, help="synthetic shape (default: baby for DiffMM, tiktok for GenRecV1)")
+    ap.add_argument("--model", default=None, choices=sorted(MODELS), help="default: DiffMM headline + legs")
+    ap.add_argument("--shape", default=None, help="synthetic shape (default: baby; tiktok for GenRecV1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-legs", action="store_true", help="headline only (no DiffRec / GenRecV1 legs)")
     ap.add_argument("--eval-passes", type=int, default=3)
-    ap.add_argument("--no-probe", action="store_true", help="no HIP-event probes (A/B timing only)")
+    ap.add_argument("--no-probe", action="store_true", help="no serial roofline epoch (A/B timing only)")
     ap.add_argument("--scoring-dtype", default=None, choices=["fp32", "fp16"],
                     help="GenRecV1 full-catalog scoring precision (config 5's fp16 MFMA scoring GEMM)")
     args = ap.parse_args()
+    legs = args.model is None and not args.no_legs
+    args.model = args.model or "diffmm"
     args.shape = args.shape or DEFAULT_SHAPE[args.model]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -284,95 +353,60 @@ def main():
             torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             torch.distributed.init_process_group(backend)
-    dist = world > 1
+    dist_on = world > 1
 
     def barrier():
-        if dist:
+        if dist_on:
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
     def max_over_ranks(x):
-        if not dist:
+        if not dist_on:
             return x
         t = torch.tensor([x], dtype=torch.float64, device="cuda")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         return float(t.item())
 
-    from gmr import kernels as K
-
-    cfg, ds, tr, tl, vl, model, trainer = setup(args)
-    U = model.n_users
-
-    # warmup (the first warmup epoch is also probed to rank the kernel classes)
-    probe_all = None
-    graphs = getattr(trainer, "_use_graphs", False)
-    for i in range(args.warmup):
-        probed = i == args.warmup - 1 and not args.no_probe
-        if probed:  # eager epoch: every launch individually timed
-            trainer._use_graphs = False
-            K.probe_begin(["gemm", "spmm"])
-        t0 = time.time()
-        trainer._train_epoch(tl, i)
-        torch.cuda.synchronize()
-        trainer._use_graphs = graphs
-        if probed:
-            raw = K.probe_end()
-            probe_all = summarize_probe(raw, args.model, args.shape)
-            if os.environ.get("GMR_PROBE_REPORT"):
-                report_shapes(raw)
-        log(f"warmup epoch {i}: {time.time() - t0:.3f}s")
-    dominant = max(probe_all, key=lambda k: probe_all[k]["total_ms"]) if probe_all else "gemm"
-
-    # timed epochs (live events around the dominant kernel class's launches; launches replayed
-    # inside the BPR-step HIP graphs are not individually timed)
-    if not args.no_probe:
-        K.probe_begin([dominant], every=4)  # 1-in-4 sample: keeps the events' own cost out of the epoch time
-    barrier()
-    t0 = time.time()
-    for i in range(args.steps):
-        trainer._train_epoch(tl, args.warmup + i)
-    barrier()
-    dt = max_over_ranks(time.time() - t0)
-    live = summarize_probe(K.probe_end(), args.model, args.shape) if not args.no_probe else {}
-    train_ups = U * args.steps / dt
-
-    # full-rank evaluation passes (valid split)
-    trainer.evaluate(vl)
-    barrier()
-    t0 = time.time()
-    for _ in range(args.eval_passes):
-        res = trainer.evaluate(vl)
-    barrier()
-    et = max_over_ranks(time.time() - t0)
-    eval_ups = vl.pr_end * args.eval_passes / et
+    head = run_workload(args, dist_on, barrier, max_over_ranks, world == 1 and not args.no_cpu_baseline)
+    leg_out = {}
+    if legs:
+        for key, m, shape, sd in (("diffrec", "diffrec", "baby", None), ("genrecv1_fp16", "genrecv1", "tiktok", "fp16")):
+            a2 = argparse.Namespace(**vars(args))
+            a2.model, a2.shape, a2.scoring_dtype, a2.steps, a2.warmup = m, shape, sd, max(2, args.steps), 1
+            try:
+                r = run_workload(a2, dist_on, barrier, max_over_ranks, False)
+                dn, dobj = dominant(r.get("roofline_by_kernel"))
+                r["roofline"], r["dominant_kernel"] = dobj, dn
+                r["step"] = STEP_DESC[m]
+                leg_out[key] = r
+            except Exception as e:  # noqa: BLE001  (a failing leg must not cost the headline line)
+                leg_out[key] = {"error": repr(e)}
 
     if rank == 0:
-        roof = live.get(dominant) or (probe_all or {}).get(dominant)
-        if roof is not None:
-            roof["probe_scope"] = ("timed epochs, launches outside the BPR-step HIP graphs" if graphs and dominant in live
-                                   else "timed epochs" if dominant in live else "last warmup epoch (eager)")
+        roof = head.pop("roofline_by_kernel")
+        dn, dobj = dominant(roof)
         line = {
             "metric": METRIC if args.model == "diffmm" else
-            "train users/sec + full-rank eval users/sec, GenRecV1 TikTok-shaped (config 5)", "value": round(train_ups, 1), "unit": "users/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 2),
+            f"train users/sec + full-rank eval users/sec, {MODELS[args.model]} {args.shape}-shaped",
+            "value": head["train_users_per_s"], "unit": "users/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
             "data": f"synthetic ({args.shape} shape, SURVEY.md 8d recipe; random-init weights)",
-            "config": {"workload": f"{MODELS[args.model]} {args.shape}-shaped synthetic: {U} users x {model.n_items} "
-                                   f"items, {tl.n_inter} train interactions; step = {STEP_DESC[args.model]}",
-                       "global_batch": cfg["train_batch_size"], "eval_batch": cfg["eval_batch_size"],
+            "config": {"workload": f"{head['model']} {args.shape}-shaped synthetic: {head['U']} users x {head['I']} "
+                                   f"items, {head['n_inter']} train interactions; step = {STEP_DESC[args.model]}",
+                       "global_batch": head["global_batch"], "eval_batch": head["eval_batch"],
                        "parallelism": f"dp{world}"},
-            "eval_users_per_s": round(eval_ups, 1), "eval_recall@20": res.get("recall@20"),
-            "eval_scoring_dtype": getattr(model, "scoring_dtype", "fp32"),
-            "roofline": roof, "roofline_by_kernel": probe_all, "dominant_kernel": dominant,
+            "eval_users_per_s": head["eval_users_per_s"], "eval_recall@20": head["eval_recall@20"],
+            "eval_scoring_dtype": head["eval_scoring_dtype"],
+            "roofline": dobj, "dominant_kernel": dn, "roofline_by_kernel": roof,
+            "lib_sha256": lib_sha256(),
         }
-        if world == 1 and not args.no_cpu_baseline:
-            try:
-                line["cpu_baseline"] = (cpu_baseline(model, tl) if args.model == "diffmm"
-                                        else cpu_baseline_genrec(model, tl, trainer))
-            except Exception as e:  # noqa: BLE001
-                line["cpu_baseline"] = {"value": None, "error": repr(e)}
+        if "cpu_baseline" in head:
+            line["cpu_baseline"] = head["cpu_baseline"]
+        if leg_out:
+            line["legs"] = leg_out
         print(json.dumps(line), flush=True)
-    if dist:
+    if dist_on:
         torch.distributed.destroy_process_group()
 
 

@@ -3,10 +3,14 @@
 // per epoch in a uniformly random order; the negative is drawn uniformly from the items
 // that occur in the training split (TrainDataLoader.all_items, :116) and redrawn while it
 // is in the user's history (:267-275).  The random streams are our own (Philox), so the
-// batches are statistically — not bitwise — equivalent to the reference's.
+// batches are statistically — not bitwise — equivalent to the reference's.  The reference redraws
+// without bound (it would never return for a user holding every item); here a row gives up after
+// kMaxDraws draws, keeps its last candidate and is counted in *n_fallback, so a caller can report it.
 #include "gmr_common.h"
 
 namespace {
+
+constexpr int kMaxDraws = 4096;
 
 // Balanced Feistel bijection on [0, 2^bits) (bits even), 4 rounds keyed by Philox output;
 // cycle-walking maps it to a bijection on [0, n).
@@ -52,7 +56,8 @@ __device__ bool has_item(const int* __restrict__ items, int beg, int end, int v)
 __global__ void sample_epoch_kernel(int n, int bits, const int* __restrict__ iu, const int* __restrict__ ii,
                                     const int* __restrict__ rowptr, const int* __restrict__ items,
                                     const int* __restrict__ all_items, int n_all, uint64_t seed, uint64_t epoch,
-                                    int* __restrict__ out_u, int* __restrict__ out_p, int* __restrict__ out_n) {
+                                    int* __restrict__ out_u, int* __restrict__ out_p, int* __restrict__ out_n,
+                                    int* __restrict__ n_fallback) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   const uint4 k = gmr::Philox::gen(seed, epoch, 0xFEED);
@@ -62,12 +67,14 @@ __global__ void sample_epoch_kernel(int n, int bits, const int* __restrict__ iu,
   out_p[p] = ii[j];
   const int beg = rowptr[u], end = rowptr[u + 1];
   int cand = 0;
-  for (int attempt = 0; attempt < 256; ++attempt) {
+  bool found = false;
+  for (int attempt = 0; attempt < kMaxDraws && !found; ++attempt) {
     const uint4 r = gmr::Philox::gen(seed ^ 0x5DEECE66Dull, (epoch << 32) | (uint32_t)attempt, (uint64_t)p);
     cand = all_items[(int)(((uint64_t)r.x * (uint64_t)n_all) >> 32)];
-    if (!has_item(items, beg, end, cand)) break;
+    found = !has_item(items, beg, end, cand);
   }
   out_n[p] = cand;
+  if (!found && n_fallback) atomicAdd(n_fallback, 1);
 }
 
 }  // namespace
@@ -75,7 +82,7 @@ __global__ void sample_epoch_kernel(int n, int bits, const int* __restrict__ iu,
 extern "C" int gmr_sample_epoch(int64_t n_inter, const int32_t* inter_user, const int32_t* inter_item,
                                 const int32_t* user_rowptr, const int32_t* user_items, const int32_t* all_items,
                                 int64_t n_all_items, uint64_t seed, uint64_t epoch, int32_t* out_users,
-                                int32_t* out_pos, int32_t* out_neg, void* stream) {
+                                int32_t* out_pos, int32_t* out_neg, int32_t* n_fallback, void* stream) {
   GMR_ARG(inter_user && inter_item && user_rowptr && user_items && all_items && out_users && out_pos && out_neg,
           "null pointer");
   GMR_ARG(n_inter > 0 && n_inter < (1ll << 31) && n_all_items > 0, "bad size");
@@ -84,7 +91,7 @@ extern "C" int gmr_sample_epoch(int64_t n_inter, const int32_t* inter_user, cons
   if (bits & 1) ++bits;  // even width keeps both Feistel halves equal
   hipLaunchKernelGGL(sample_epoch_kernel, dim3(gmr::grid_for(n_inter, 256)), dim3(256), 0, (hipStream_t)stream,
                      (int)n_inter, bits, inter_user, inter_item, user_rowptr, user_items, all_items, (int)n_all_items,
-                     seed, epoch, out_users, out_pos, out_neg);
+                     seed, epoch, out_users, out_pos, out_neg, n_fallback);
   GMR_LAUNCHED();
   return GMR_OK;
 }

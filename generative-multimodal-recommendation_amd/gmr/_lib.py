@@ -68,7 +68,7 @@ SIGNATURES = {
     "gmr_dmm_loss_total": (I32, [I64, P, F32, P, I64, F32, P, P, F32, P, P]),
     "gmr_sum_f64": (I32, [I64, P, F64, P, I32, P]),
     "gmr_colsum_f32": (I32, [I64, I64, P, I64, P, I32, P, I32, P]),
-    "gmr_sample_epoch": (I32, [I64, P, P, P, P, P, I64, U64, U64, P, P, P, P]),
+    "gmr_sample_epoch": (I32, [I64, P, P, P, P, P, I64, U64, U64, P, P, P, P, P]),
     "gmr_permutation": (I32, [I64, U64, U64, P, P]),
     "gmr_diff_sample_t": (I32, [I32, I32, U64, U64, I64, P, P]),
     "gmr_diff_qsample": (I32, [I32, I32, P, P, P, P, P, P, P, I64, P, I64, F32, I32, U64, U64, I64, P, I64, P]),

@@ -90,6 +90,7 @@ class TrainDataLoader:
                 "plan_cl": torch.empty((nb * W, _pow2(2 * sb)), dtype=torch.int64, device=d),
                 "key_add_bpr": t(np.array([0, self.n_users, self.n_users], np.int32)),
                 "key_add_cl": t(np.array([0, self.n_users], np.int32)),
+                "n_fallback": torch.zeros(1, dtype=torch.int32, device=d),
             }
         return self._dev
 
@@ -105,9 +106,10 @@ class TrainDataLoader:
         """Draw one epoch on the device: returns dict with 'sample' (3, n_inter) int32 and plans."""
         d = self.to_device()
         s = d["sample"]
+        _lib.call("gmr_zero", ptr(d["n_fallback"]), 4, stream())
         _lib.call("gmr_sample_epoch", self.n_inter, ptr(d["inter_user"]), ptr(d["inter_item"]), ptr(d["user_ptr"]),
                   ptr(d["user_items"]), ptr(d["all_items"]), len(self.all_items_np), self.seed, self._epoch,
-                  ptr(s[0]), ptr(s[1]), ptr(s[2]), stream())
+                  ptr(s[0]), ptr(s[1]), ptr(s[2]), ptr(d["n_fallback"]), stream())
         self._epoch += 1
         if with_plans:
             nb = d["n_batches"] * d["world"]  # one plan per (batch, rank) sub-batch
@@ -116,6 +118,11 @@ class TrainDataLoader:
             _lib.call("gmr_sort_batch_keys", nb, ptr(s), ptr(d["batch_offsets"]), ptr(d["key_add_cl"]), 2,
                       self.n_inter, ptr(d["plan_cl"]), d["plan_cl"].shape[1], d["plan_cl"].shape[1], stream())
         return d
+
+    def fallbacks(self):
+        """Rows of the last epoch draw whose negative is not a true negative (device read; 0 unless
+        a user holds nearly every item, see gmr_sample_epoch)."""
+        return int(self.to_device()["n_fallback"].item())
 
     def batches(self, d, rank=None):
         """Per batch b of the epoch draw: (b, global rows, users, pos, neg, plan_bpr, plan_cl) of this

@@ -140,9 +140,11 @@ class DiffMM(GeneralRecommender):
                                           seg_nnz=K.SPMM_NORM_ADJ)
         self.image_UI_matrix = None
         self.text_UI_matrix = None
+        self._ui_T = {}           # id(UI graph) -> its transpose when edge dropping made it asymmetric
         self._w = None
         self._dw = None
         self._step = 0
+        self._rebuilds = 0
         self._streams = K.Streams(2)
         self._sq_parts = int(_lib.load().gmr_sqnorm_nparts(self.N * 64))
 
@@ -299,8 +301,8 @@ class DiffMM(GeneralRecommender):
             _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
                       ptr(w["Rt"]), stream())
             with st.on(1):
-                tadj.spmm(w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)])
-            iadj.spmm(w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)])      # iadj symmetric
+                self._transpose_of(tadj).spmm(w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)])
+            self._transpose_of(iadj).spmm(w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)])
             st.join(1)
         adj.spmm(w["T2"], [(w["dE"][:, :64],), (w["dE"][:, 64:],)])
         _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
@@ -318,6 +320,19 @@ class DiffMM(GeneralRecommender):
         st.join(1)
         self._step += 1
         return loss[0]
+
+    def _transpose_of(self, g):
+        """A^T for the backward of a UI-graph product: A itself at keep_rate 1 (the normalised graph
+        is symmetric), else the transpose built from the same edge draws (set_ui_matrices)."""
+        return self._ui_T.get(id(g), g)
+
+    def set_ui_matrices(self, image, text, image_T=None, text_T=None):
+        """Install the (edge-dropped) UI graphs and, when dropping made them asymmetric, their transposes."""
+        self.image_UI_matrix, self.text_UI_matrix = image, text
+        self._ui_T = {}
+        for g, t in ((image, image_T), (text, text_T)):
+            if t is not None:
+                self._ui_T[id(g)] = t
 
     def graph_key(self):
         """Identity of every device buffer a captured rec_step bakes in besides its inputs."""
@@ -361,13 +376,31 @@ class DiffMM(GeneralRecommender):
         return [self.rec_slab]
 
     def extra_state(self):
-        """The generated UI graphs (not parameters; the reference does not save them, diffmm.py:263-274)."""
-        out = {}
+        """The generated UI graphs (not parameters; the reference does not save them, diffmm.py:263-274),
+        their transposes when edge dropping made them asymmetric, and the rebuild / step counters."""
+        out = {"counters": {"rebuilds": self._rebuilds, "step": self._step}}
         for n in ("image_UI_matrix", "text_UI_matrix"):
             g = getattr(self, n)
             if g is not None:
                 out[n] = {"rowptr": g.rowptr.cpu(), "col": g.col.cpu(), "val": g.val.cpu()}
+                t = self._ui_T.get(id(g))
+                if t is not None:
+                    out[n + "_T"] = {"rowptr": t.rowptr.cpu(), "col": t.col.cpu(), "val": t.val.cpu()}
         return out
+
+    def load_extra_state(self, st):
+        """Inverse of extra_state: reinstall the generated graphs (with their SpMM plans)."""
+        def csr(d):
+            if d is None:
+                return None
+            dev = self.device
+            return K.CSR(d["rowptr"].to(dev), d["col"].to(dev), d["val"].to(dev), symmetric=False)
+        gi, gt = csr(st.get("image_UI_matrix")), csr(st.get("text_UI_matrix"))
+        if gi is not None and gt is not None:
+            self.set_ui_matrices(gi, gt, csr(st.get("image_UI_matrix_T")), csr(st.get("text_UI_matrix_T")))
+        c = st.get("counters") or {}
+        self._rebuilds = int(c.get("rebuilds", self._rebuilds))
+        self._step = int(c.get("step", self._step))
 
     def grad_view(self, name):
         s, U = self.rec_slab, self.n_users
@@ -527,11 +560,17 @@ class DiffMM(GeneralRecommender):
             sample(1)
         sample(0)
         st.join(1)
-        for topk in topks:
+        for j, topk in enumerate(topks):
             dist.all_gather_rows_(topk, size)
             K.topk_to_user_csr(topk[:U], uptr, uitems)
             g = K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0)
             if self.keepRate != 1:
-                raise NotImplementedError("SpAdjDropEdge with keep_rate < 1 (DiffMM.yaml uses keep_rate = 1)")
-            graphs.append(g)
-        self.image_UI_matrix, self.text_UI_matrix = graphs
+                # SpAdjDropEdge (diffmm.py:287-301): entry kept iff floor(u + keep) >= 1, value / keep;
+                # the same Philox draws give the transpose for the backward (same on every rank)
+                st_id = 6000 + 2 * self._rebuilds + j
+                graphs.append((K.csr_drop_edges(g, self.keepRate, seed=self.seed, step=st_id),
+                               K.csr_drop_edges(g, self.keepRate, seed=self.seed, step=st_id, transposed=True)))
+            else:
+                graphs.append((g, None))
+        self._rebuilds += 1
+        self.set_ui_matrices(graphs[0][0], graphs[1][0], graphs[0][1], graphs[1][1])

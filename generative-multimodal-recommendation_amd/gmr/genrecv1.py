@@ -529,7 +529,21 @@ class GenRecV1(GeneralRecommender):
         if self.image_UI_matrix is not None:
             g = self.image_UI_matrix
             out["image_UI_matrix"] = {"rowptr": g.rowptr.cpu(), "col": g.col.cpu(), "val": g.val.cpu()}
+            t = self.image_UI_matrix_T
+            out["image_UI_matrix_T"] = {"rowptr": t.rowptr.cpu(), "col": t.col.cpu(), "val": t.val.cpu()}
         return out
+
+    def load_extra_state(self, st):
+        """Inverse of extra_state: BatchNorm running statistics and the rebuilt (dropped) UI graph."""
+        for k, (mean, var) in (st.get("bn_state") or {}).items():
+            self.bn_state[k][0].copy_(mean)
+            self.bn_state[k][1].copy_(var)
+        g = st.get("image_UI_matrix")
+        if g is not None:
+            dev = self.device
+            mk = lambda d: K.CSR(d["rowptr"].to(dev), d["col"].to(dev), d["val"].to(dev), symmetric=False)  # noqa: E731
+            t = st.get("image_UI_matrix_T")
+            self.set_image_ui_matrix(mk(g), mk(t) if t is not None else None)
 
 
 class FlipDiffusion:

@@ -94,6 +94,11 @@ class FlatAdam:
                           for st in self.state], "param_groups": self.param_groups}
 
     def load_state_dict(self, sd):
+        if len(sd["state"]) != len(self.state):
+            raise ValueError("optimizer state holds a different number of slabs")
+        if sd.get("param_groups"):
+            self.lr = float(sd["param_groups"][0]["lr"])
+            self.param_groups[0]["lr"] = self.lr
         for st, src in zip(self.state, sd["state"]):
             st["step"] = src["step"]
             st["exp_avg"].copy_(src["exp_avg"])

@@ -106,6 +106,10 @@ class Trainer:
             self.optimizer.step()
         dist.all_reduce_(acc)
         total = float(acc[0].item())
+        fb = train_data.fallbacks() if hasattr(train_data, "fallbacks") else 0
+        if fb:
+            self.logger.warning(f"epoch {epoch_idx}: {fb} BPR rows kept a negative from the user's history "
+                                f"(no true negative in 4096 draws)")
         if np.isnan(total):
             self.logger.info("Loss is nan at epoch: {}. Exiting.".format(epoch_idx))
             return torch.tensor(float("nan")), []
@@ -150,6 +154,7 @@ class Trainer:
         return score, res
 
     def fit(self, train_data, valid_data=None, test_data=None, saved=False, verbose=True):
+        self._train_data = train_data
         for epoch_idx in range(self.start_epoch, self.epochs):
             t0 = time()
             self.model.pre_epoch_processing()
@@ -202,15 +207,69 @@ class Trainer:
         d = self.config["checkpoint_dir"] or "saved"
         os.makedirs(d, exist_ok=True)
         path = os.path.join(d, "{}-{}.pth".format(self.config["model"], self.config["dataset"]))
-        state = {"config": {k: v for k, v in self.config.final_config_dict.items() if k not in ("device",)},
+        torch.save(self.checkpoint_state(epoch), path)
+        self.logger.info("Saved best model to {}".format(path))
+        dist.barrier()
+
+    def checkpoint_state(self, epoch):
+        """The reference's checkpoint keys (trainer.py:345-366: config, epoch, state_dict, optimizer,
+        best_valid_score) plus what a resume needs to continue the same run: the generated UI graphs
+        (the reference does not save them, diffmm.py:263-274), the denoiser optimisers, and the
+        positions of the device random streams (sampler epoch, diffusion permutations)."""
+        def plain(v):
+            if isinstance(v, (set, frozenset)):
+                return sorted(plain(x) for x in v)
+            if isinstance(v, (list, tuple)):
+                return [plain(x) for x in v]
+            if isinstance(v, dict):
+                return {str(k): plain(x) for k, x in v.items()}
+            return v if isinstance(v, (str, int, float, bool, type(None))) else str(v)
+        state = {"config": {k: plain(v) for k, v in self.config.final_config_dict.items() if k != "device"},
                  "epoch": epoch, "state_dict": {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
                  "optimizer": self.optimizer.state_dict(), "best_valid_score": self.best_valid_score}
         extra = getattr(self.model, "extra_state", None)
         if callable(extra):
             state["generated_graphs"] = extra()
-        torch.save(state, path)
-        self.logger.info("Saved best model to {}".format(path))
-        dist.barrier()
+        state["denoise_optimizers"] = {n: getattr(self, n).state_dict() for n in ("denoise_opt_image", "denoise_opt_text")
+                                       if hasattr(self, n)}
+        td = getattr(self, "_train_data", None)
+        state["trainer_state"] = {"sched_epoch": self._sched_epoch, "cur_step": self.cur_step,
+                                  "epoch_ctr": getattr(self, "_epoch_ctr", 0),
+                                  "sampler_epoch": getattr(td, "_epoch", None),
+                                  "best_valid_result": plain(self.best_valid_result),
+                                  "best_test_upon_valid": plain(self.best_test_upon_valid)}
+        return state
+
+    def resume_checkpoint(self, path, train_data=None):
+        """Continue a run from a checkpoint written by _save_checkpoint: parameters, optimisers,
+        generated graphs and random-stream positions are restored, so the next epoch is the one the
+        uninterrupted run would have trained (tests/test_resume_gpu.py)."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        self.load_checkpoint_state(ck, train_data)
+
+    def load_checkpoint_state(self, ck, train_data=None):
+        with torch.no_grad():
+            self.model.load_state_dict({k: v.to(self.device) for k, v in ck["state_dict"].items()})
+        self.optimizer.load_state_dict(ck["optimizer"])
+        for n, sd in (ck.get("denoise_optimizers") or {}).items():
+            getattr(self, n).load_state_dict(sd)
+        load_extra = getattr(self.model, "load_extra_state", None)
+        if callable(load_extra) and ck.get("generated_graphs"):
+            load_extra(ck["generated_graphs"])
+        ts = ck.get("trainer_state") or {}
+        self.start_epoch = int(ck["epoch"]) + 1
+        self.best_valid_score = ck["best_valid_score"]
+        self._sched_epoch = int(ts.get("sched_epoch", self.start_epoch))
+        self.optimizer.set_lr_factor(self.lr_factor(self._sched_epoch))
+        self.cur_step = int(ts.get("cur_step", 0))
+        if hasattr(self, "_epoch_ctr"):
+            self._epoch_ctr = int(ts.get("epoch_ctr", self._epoch_ctr))
+        if train_data is not None and ts.get("sampler_epoch") is not None:
+            train_data._epoch = int(ts["sampler_epoch"])
+        if ts.get("best_valid_result"):
+            self.best_valid_result = ts["best_valid_result"]
+            self.best_test_upon_valid = ts.get("best_test_upon_valid", self.best_test_upon_valid)
+        self.logger.info("Resumed from epoch {} (next epoch {})".format(ck["epoch"], self.start_epoch))
 
     # ------------------------------------------------------------------ evaluation
     @torch.no_grad()

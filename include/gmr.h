@@ -234,10 +234,13 @@ int gmr_colsum_split_f32(int64_t rows, int64_t cols, const float* x, int64_t ld,
                          float* workspace, int64_t workspace_floats, void* stream);
 
 /* ---------------------------------------------------------------- BPR epoch sampler (dataloader.py:218-275)
- * shuffled interactions + one rejection-sampled negative from `all_items` per interaction */
+ * shuffled interactions + one rejection-sampled negative from `all_items` per interaction (redrawn while
+ * in the user's history); rows still without a true negative after 4096 draws are added to
+ * *n_fallback (may be NULL; the caller zeroes it) and keep their last draw. */
 int gmr_sample_epoch(int64_t n_inter, const int32_t* inter_user, const int32_t* inter_item, const int32_t* user_rowptr,
                      const int32_t* user_items, const int32_t* all_items, int64_t n_all_items, uint64_t seed,
-                     uint64_t epoch, int32_t* out_users, int32_t* out_pos, int32_t* out_neg, void* stream);
+                     uint64_t epoch, int32_t* out_users, int32_t* out_pos, int32_t* out_neg, int32_t* n_fallback,
+                     void* stream);
 /* random permutation of [0, n) (DataLoader(shuffle=True) over users, trainer.py:462) */
 int gmr_permutation(int64_t n, uint64_t seed, uint64_t epoch, int32_t* out, void* stream);
 

@@ -179,3 +179,60 @@ def test_train_epoch_runs(golden):
     assert np.isfinite(loss)
     res = trainer.evaluate(vl)
     assert 0.0 <= res["recall@20"] <= 1.0
+
+
+def test_rec_step_edge_dropped_ui_graphs(golden):
+    """D10 SpAdjDropEdge at keep_rate 0.5 (models/diffmm.py:287-301): the dropped UI graphs are no
+    longer symmetric, so the backward runs on their transposes (same draws).  Loss and every rec
+    gradient against the oracle's autograd on the same dropped graphs."""
+    from oracle import model_ref
+    from gmr import kernels as K
+    g = golden("diffmm_tiny")
+    m = build_model(g)
+    U, I = int(g["U"]), int(g["I"])
+    N = U + I
+    drop = {}
+    for name in ("image_UI_matrix", "text_UI_matrix"):
+        a = getattr(m, name)
+        d = K.csr_drop_edges(a, 0.5, seed=11, step=3 + len(drop))
+        dt = K.csr_drop_edges(a, 0.5, seed=11, step=3 + len(drop), transposed=True)
+        rp, cl, vl = (x.cpu().numpy() for x in (d.rowptr, d.col, d.val))
+        assert 0 < d.nnz < a.nnz
+        dense = graph_ref.csr_to_dense(rp, cl, vl, N)
+        dense_t = graph_ref.csr_to_dense(*(x.cpu().numpy() for x in (dt.rowptr, dt.col, dt.val)), N)
+        assert np.array_equal(dense.T, dense_t)          # the transpose holds the same draws
+        kept = dense[dense != 0]
+        assert np.allclose(kept, graph_ref.csr_to_dense(*(x.cpu().numpy() for x in (a.rowptr, a.col, a.val)),
+                                                        N)[dense != 0] / 0.5)
+        drop[name] = (d, dt, model_ref.sparse_from_csr(rp, cl, vl, N))
+    m.set_ui_matrices(drop["image_UI_matrix"][0], drop["text_UI_matrix"][0], drop["image_UI_matrix"][1],
+                      drop["text_UI_matrix"][1])
+    t = lambda k: torch.as_tensor(g[k].astype(np.int32)).to(DEV)  # noqa: E731
+    loss = m.rec_step(t("bpr_users"), t("bpr_pos"), t("bpr_neg"))
+    adj = model_ref.sparse_from_csr(*graph_ref.norm_adj_csr(U, I, g["train_rows"], g["train_cols"]), N)
+    names = ["uEmbeds", "iEmbeds", "image_trans", "text_trans", "modal_weight"]
+    p = {k: torch.tensor(g["p_" + k], requires_grad=True) for k in names}
+    feats = {"v": torch.as_tensor(g["v_feat"]), "t": torch.as_tensor(g["t_feat"])}
+    want = model_ref.rec_loss(p, feats, adj, drop["image_UI_matrix"][2], drop["text_UI_matrix"][2],
+                              *(torch.as_tensor(g[k]) for k in ("bpr_users", "bpr_pos", "bpr_neg")))
+    want.backward()
+    np.testing.assert_allclose(loss.item(), want.item(), rtol=1e-5)
+    gE0 = m.rec_slab.gview("E0").cpu().numpy()
+    np.testing.assert_allclose(gE0[:U], p["uEmbeds"].grad.numpy(), rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(gE0[U:], p["iEmbeds"].grad.numpy(), rtol=1e-4, atol=1e-7)
+    for n in ("image_trans", "text_trans", "modal_weight"):
+        np.testing.assert_allclose(m.rec_slab.gview(n).cpu().numpy(), p[n].grad.numpy(), rtol=1e-4, atol=1e-7)
+
+
+def test_rebuild_with_edge_drop(golden):
+    """DiffMMTrainer graph rebuild at keep_rate < 1 installs dropped graphs and their transposes."""
+    g = golden("diffmm_tiny")
+    m = build_model(g)
+    m.keepRate = 0.5
+    m.rebuild_ui_graphs()
+    for a in (m.image_UI_matrix, m.text_UI_matrix):
+        at = m._transpose_of(a)
+        assert at is not a and at.nnz == a.nnz
+        d = graph_ref.csr_to_dense(*(x.cpu().numpy() for x in (a.rowptr, a.col, a.val)), a.n_rows)
+        dt = graph_ref.csr_to_dense(*(x.cpu().numpy() for x in (at.rowptr, at.col, at.val)), a.n_rows)
+        assert np.array_equal(d.T, dt)
