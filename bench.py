@@ -299,7 +299,7 @@ def run_workload(args, dist_on, barrier, max_over_ranks, with_cpu_baseline):
             o["probe_scope"] = ("one extra epoch after the timed region with the side streams off (GMR_SERIAL): "
                                 "HIP events around every launch of the class on its stream")
         roof["_epoch"] = {"mfma_flop_per_epoch": mfma_flop, "serial_epoch_ms": round(serial_ms, 2),
-                          "epoch_mfma_frac": round(mfma_flop / (1e-3 * dt / args.steps) / 1e12 / FP32_MFMA_PEAK_TFS, 4),
+                          "epoch_mfma_frac": round(mfma_flop / (dt / args.steps) / 1e12 / FP32_MFMA_PEAK_TFS, 4),
                           "note": "algorithmic GEMM + InfoNCE flop of one epoch / timed ms_per_step / fp32 MFMA peak"}
     out = {"model": MODELS[args.model], "shape": args.shape, "U": U, "I": model.n_items, "n_inter": tl.n_inter,
            "train_users_per_s": round(train_ups, 1), "ms_per_step": round(1e3 * dt / args.steps, 2),
