@@ -717,6 +717,325 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
   }
 }
 
+
+// ----------------------------------------------------------------------------------------
+// Chunk plan (seg_nnz = GMR_SPMM_CHUNK_PLAN).  The lane plan gives each lane group one row per
+// pass, so a row of degree 2 (every user row of a rebuilt UI graph) leaves 6 of the group's 8
+// gather slots idle and a row of degree 9 (a typical norm_adj row) takes two dependent rounds.
+// Here the rows of degree 1..128 are cut, in row order, into tasks of whole rows holding at most
+// 128 entries; a wave owns a task and its lane groups each take 128 / NG consecutive entries,
+// whatever rows they belong to, so every gather slot is used and a task is ONE round of gathers.
+// Row sums that cross lane groups meet in LDS in group order (the group where the row starts adds
+// the continuations), so each row is summed in a fixed order: deterministic.  Rows of degree
+// > 128 (hubs) take a whole 1024-thread workgroup as in the lane plan; empty rows are listed.
+// The X slicing (one column slice per XCD, kept in its L2) is the lane plan's.
+// Plan: hdr {n_hub, n_task, n_empty, n_packed}, hub int4 {row, beg, end, 0}[HC],
+//       task int2 {first packed entry, entries}[TC], empty rows [n_rows], row start in the
+//       packed arrays [n_rows], then pcol[nnz], pval[nnz], prow[nnz] (rows of degree 1..128).
+constexpr int kChunkThreads = 1024;
+constexpr int kChunkTask = 128;  // entries per task = hub threshold
+
+__host__ __device__ inline int64_t r4(int64_t w) { return (w + 3) / 4 * 4; }
+__host__ __device__ inline int64_t chunk_hub_cap(int64_t n_rows, int64_t nnz) {
+  const int64_t h = nnz / (kChunkTask + 1) + 1;
+  return h < n_rows ? h : n_rows;
+}
+struct ChunkView {
+  int* hdr;
+  int4* hub;
+  int2* task;
+  int* empty;
+  int* vstart;
+  int* pcol;
+  float* pval;
+  int* prow;
+};
+__host__ __device__ inline ChunkView chunk_view(int32_t* p, int64_t n_rows, int64_t nnz) {
+  ChunkView v;
+  v.hdr = p;
+  int64_t o = kPlanHdr;
+  v.hub = reinterpret_cast<int4*>(p + o);
+  o += 4 * chunk_hub_cap(n_rows, nnz);
+  v.task = reinterpret_cast<int2*>(p + o);
+  o += r4(2 * n_rows);
+  v.empty = p + o;
+  o += r4(n_rows);
+  v.vstart = p + o;
+  o += r4(n_rows);
+  v.pcol = p + o;
+  o += r4(nnz);
+  v.pval = reinterpret_cast<float*>(p + o);
+  o += r4(nnz);
+  v.prow = p + o;
+  return v;
+}
+__host__ __device__ inline int64_t chunk_plan_words(int64_t n_rows, int64_t nnz) {
+  return kPlanHdr + 4 * chunk_hub_cap(n_rows, nnz) + r4(2 * n_rows) + 2 * r4(n_rows) + 3 * r4(nnz);
+}
+
+// exclusive scan of one int per thread of a 1024-thread block (Hillis-Steele in LDS)
+__device__ int block_excl_scan(int v, int* s, int* total) {
+  const int t = threadIdx.x;
+  s[t] = v;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int a = t >= o ? s[t - o] : 0;
+    __syncthreads();
+    s[t] += a;
+    __syncthreads();
+  }
+  const int incl = s[t];
+  *total = s[1023];
+  __syncthreads();
+  return incl - v;
+}
+
+// One workgroup: thread t owns rows [t R, (t+1) R) and packs its short rows greedily into tasks of
+// <= 128 entries (tasks never cross thread ranges); counts, scans, then writes the descriptors.
+__global__ void __launch_bounds__(1024) chunk_plan_kernel(const int* __restrict__ rowptr, int n_rows, int64_t nnz,
+                                                          int* __restrict__ plan) {
+  __shared__ int s_scan[1024];
+  ChunkView pv = chunk_view(plan, n_rows, nnz);
+  const int t = threadIdx.x;
+  const int R = (n_rows + 1023) / 1024;
+  const int r0 = min(n_rows, t * R), r1 = min(n_rows, r0 + R);
+  int nh = 0, ne = 0, nt = 0, nv = 0, run = 0;
+  for (int r = r0; r < r1; ++r) {
+    const int d = rowptr[r + 1] - rowptr[r];
+    if (d == 0) {
+      ++ne;
+    } else if (d > kChunkTask) {
+      ++nh;
+    } else {
+      nv += d;
+      if (run == 0 || run + d > kChunkTask) {
+        ++nt;
+        run = d;
+      } else {
+        run += d;
+      }
+    }
+  }
+  int th, te, tt, tv;
+  int oh = block_excl_scan(nh, s_scan, &th);
+  int oe = block_excl_scan(ne, s_scan, &te);
+  int ot = block_excl_scan(nt, s_scan, &tt);
+  int ov = block_excl_scan(nv, s_scan, &tv);
+  int tb = -1;  // first packed entry of the open task
+  run = 0;
+  for (int r = r0; r < r1; ++r) {
+    const int beg = rowptr[r], end = rowptr[r + 1], d = end - beg;
+    if (d == 0) {
+      pv.empty[oe++] = r;
+      pv.vstart[r] = -1;
+    } else if (d > kChunkTask) {
+      pv.hub[oh++] = make_int4(r, beg, end, 0);
+      pv.vstart[r] = -1;
+    } else {
+      if (run == 0 || run + d > kChunkTask) {
+        if (run > 0) pv.task[ot++] = make_int2(tb, run);
+        tb = ov;
+        run = d;
+      } else {
+        run += d;
+      }
+      pv.vstart[r] = ov;
+      ov += d;
+    }
+  }
+  if (run > 0) pv.task[ot++] = make_int2(tb, run);
+  if (t == 0) {
+    pv.hdr[0] = th;
+    pv.hdr[1] = tt;
+    pv.hdr[2] = te;
+    pv.hdr[3] = tv;
+  }
+}
+
+// copies the short rows' col / val (and their row ids) into the packed arrays
+__global__ void __launch_bounds__(256) chunk_pack_kernel(const int* __restrict__ rowptr, const int* __restrict__ col,
+                                                         const float* __restrict__ val, int n_rows, int64_t nnz,
+                                                         int* __restrict__ plan) {
+  ChunkView pv = chunk_view(plan, n_rows, nnz);
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n_rows; r += gridDim.x * blockDim.x) {
+    const int v = pv.vstart[r];
+    if (v < 0) continue;
+    const int beg = rowptr[r], d = rowptr[r + 1] - beg;
+    for (int q = 0; q < d; ++q) {
+      pv.pcol[v + q] = col[beg + q];
+      pv.pval[v + q] = val[beg + q];
+      pv.prow[v + q] = r;
+    }
+  }
+}
+
+template <int LPR>
+__global__ void __launch_bounds__(kChunkThreads) spmm_chunk_kernel(const int* __restrict__ col,
+                                                                   const float* __restrict__ val,
+                                                                   const int* __restrict__ plan, int n_rows,
+                                                                   int64_t nnz, int S, int wpx, Src src, float alpha,
+                                                                   float beta, Dst dst) {
+  constexpr int NW = kChunkThreads / 64;  // waves per workgroup
+  constexpr int NG = 64 / LPR;            // lane groups per wave
+  constexpr int EB = kChunkTask / NG;     // entries per lane group and task (8 or 16)
+  constexpr int EPL = EB / LPR;           // entry words per lane (2)
+  __shared__ float4 s_red[NW][LPR];
+  __shared__ float4 s_cacc[NW][NG][LPR];  // continuation partial of each lane group's first row
+  __shared__ int s_crow[NW][NG];          // that row, or -1 when the group's first row starts in it
+  __shared__ int s_cend[NW][NG];          // 1 when that continuation ends inside the group
+  const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+  const int slice = xcd % S, part = xcd / S, P = 8 / S;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = lane / LPR, sub = lane % LPR, gbase = grp * LPR;
+  const ChunkView pv = chunk_view(const_cast<int*>(plan), n_rows, nnz);
+  const int n_hub = plan[0], n_task = plan[1], n_empty = plan[2];
+  const int c0 = slice * 4 * LPR;  // first column of the slice
+  const int blk = c0 >> 6, cin = (c0 & 63) + sub * 4;
+  const bool panel = src.panel_rows > 0;
+  const float* lo = panel ? src.lo[0] + (int64_t)slice * src.panel_rows * (4 * LPR) + sub * 4 : src.lo[blk] + cin;
+  const float* hi = panel ? lo : src.hi[blk] + cin;
+  const int64_t ldl = panel ? 4 * LPR : src.ld_lo[blk], ldh = panel ? 4 * LPR : src.ld_hi[blk];
+  const int64_t split = panel ? src.panel_rows : src.split;
+  float* yc = dst.y[blk] + (c0 & 63) + sub * 4;
+  const int64_t ldy = dst.ld[blk];
+  auto gather = [&](int c) -> float4 {
+    return *reinterpret_cast<const float4*>(c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh);
+  };
+  auto store = [&](int row, float4 acc) {
+    float* yp = yc + (int64_t)row * ldy;
+    float4 o = gmr::f4_scale(alpha, acc);
+    if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
+    *reinterpret_cast<float4*>(yp) = o;
+  };
+  const int wg = part * wpx + k, n_wg = P * wpx;
+
+  // hub rows: one workgroup each, every lane group strides over EB-entry batches
+  for (int hb = wg; hb < n_hub; hb += n_wg) {
+    const int4 d = pv.hub[hb];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e0 = d.y + (wid * NG + grp) * EB; e0 < d.z; e0 += NW * NG * EB) {
+      int cc[EPL];
+      float vv[EPL];
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        const int i = e0 + q * LPR + sub;
+        cc[q] = i < d.z ? col[i] : 0;
+        vv[q] = i < d.z ? val[i] : 0.f;
+      }
+      float4 xs[EB];
+      float vs[EB];
+#pragma unroll
+      for (int u = 0; u < EB; ++u) {
+        const int c = __shfl(cc[u / LPR], gbase + u % LPR);
+        vs[u] = __shfl(vv[u / LPR], gbase + u % LPR);
+        xs[u] = e0 + u < d.z ? gather(c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < EB; ++u) acc = gmr::f4_fma(vs[u], xs[u], acc);
+    }
+#pragma unroll
+    for (int m = LPR; m < 64; m <<= 1) acc = gmr::f4_add(acc, gmr::shfl_xor_f4(acc, m));
+    if (grp == 0) s_red[wid][sub] = acc;
+    __syncthreads();
+    if (threadIdx.x < LPR) {
+      float4 s = s_red[0][sub];
+#pragma unroll
+      for (int q = 1; q < NW; ++q) s = gmr::f4_add(s, s_red[q][sub]);
+      store(d.x, s);
+    }
+    __syncthreads();
+  }
+  // empty rows: Y = beta * Y
+  for (int i = wg * (kChunkThreads / LPR) + threadIdx.x / LPR; i < n_empty; i += n_wg * (kChunkThreads / LPR))
+    store(pv.empty[i], make_float4(0.f, 0.f, 0.f, 0.f));
+
+  // tasks: one per wave and pass
+  const int* __restrict__ pcol = pv.pcol;
+  const float* __restrict__ pval = pv.pval;
+  const int* __restrict__ prow = pv.prow;
+  for (int t = wg * NW + wid; t < n_task; t += n_wg * NW) {
+    const int2 td = pv.task[t];
+    const int tend = td.x + td.y;
+    const int g0 = td.x + grp * EB, g1 = min(tend, g0 + EB);
+    int cc[EPL], rr[EPL];
+    float vv[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+      const int i = g0 + q * LPR + sub;
+      const bool ok = i < g1;
+      cc[q] = ok ? pcol[i] : 0;
+      vv[q] = ok ? pval[i] : 0.f;
+      rr[q] = ok ? prow[i] : -1;
+    }
+    // does the group's first row start before it / its last row continue after it?
+    const int prev_row = (g0 > td.x && g0 < g1) ? prow[g0 - 1] : -1;
+    const int next_row = (g1 < tend && g0 < g1) ? prow[g1] : -1;
+    float4 xs[EB];
+    float vs[EB];
+    int rs[EB];
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const int c = __shfl(cc[u / LPR], gbase + u % LPR);
+      vs[u] = __shfl(vv[u / LPR], gbase + u % LPR);
+      rs[u] = __shfl(rr[u / LPR], gbase + u % LPR);
+      xs[u] = g0 + u < g1 ? gather(c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int first = rs[0];
+    const bool cont = first >= 0 && first == prev_row;  // first row began in an earlier group
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 cacc = acc;
+    int cur = first, cend = 0;
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      if (rs[u] < 0) break;
+      if (rs[u] != cur) {  // cur ends inside this group
+        if (cont && cur == first) {
+          cacc = acc;
+          cend = 1;
+        } else {
+          store(cur, acc);
+        }
+        acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        cur = rs[u];
+      }
+      acc = gmr::f4_fma(vs[u], xs[u], acc);
+    }
+    // cur = last row of the group (or -1 if empty)
+    const bool last_open = cur >= 0 && cur == next_row;  // continues into the next group
+    if (cur >= 0 && !last_open) {
+      if (cont && cur == first) {  // the whole group is the tail of a row begun earlier
+        cacc = acc;
+        cend = 1;
+      } else {
+        store(cur, acc);
+      }
+    }
+    const bool whole = cont && cur == first && last_open;  // group inside one spanning row
+    if (whole) cacc = acc;
+    if (sub == 0) {
+      s_crow[wid][grp] = cont ? first : -1;
+      s_cend[wid][grp] = cend;
+    }
+    s_cacc[wid][grp][sub] = cacc;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the group where a spanning row starts adds the continuations of the next groups, in order
+    if (last_open && !(cont && cur == first)) {
+      float4 s = acc;
+      for (int j = grp + 1; j < NG; ++j) {
+        if (s_crow[wid][j] != cur) break;
+        s = gmr::f4_add(s, s_cacc[wid][j][sub]);
+        if (s_cend[wid][j]) break;
+      }
+      store(cur, s);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 }  // namespace
 
 static inline int lane_l(int32_t seg_nnz) {  // longest short row of a lane plan, 0 if seg_nnz is invalid
@@ -765,7 +1084,10 @@ static int lane_wpx_cap_packed() {  // the packed kernel pipelines passes, so it
   return cap;
 }
 
+static inline bool is_chunk(int32_t seg_nnz) { return seg_nnz == GMR_SPMM_CHUNK_PLAN; }
+
 extern "C" int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_nnz) {
+  if (is_chunk(seg_nnz)) return chunk_plan_words(n_rows, nnz);
   if (seg_nnz & GMR_SPMM_LANE_PLAN) {
     if (!lane_l(seg_nnz)) return -1;
     return lane_packed(seg_nnz) ? pack_off(n_rows) + 2 * nnz : kPlanHdr + 4 * n_rows;
@@ -776,6 +1098,7 @@ extern "C" int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_
 }
 
 extern "C" int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t seg_nnz) {
+  if (is_chunk(seg_nnz)) return 1;  // spanning rows meet in LDS
   if (seg_nnz & GMR_SPMM_LANE_PLAN) return lane_l(seg_nnz) ? 1 : -1;  // hub rows are combined in LDS
   if (seg_nnz <= 0) return -1;
   if (seg_nnz >= 512) return 1;  // the blocked variant combines in LDS
@@ -786,6 +1109,12 @@ extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_
                                    int32_t* plan, void* stream) {
   GMR_ARG(rowptr && plan, "null pointer");
   GMR_ARG(n_rows > 0 && n_rows < (1ll << 31) && nnz >= 0 && nnz < (1ll << 31), "bad size");
+  if (is_chunk(seg_nnz)) {
+    GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
+    hipLaunchKernelGGL(chunk_plan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, (int)n_rows, nnz, plan);
+    GMR_LAUNCHED();
+    return GMR_OK;
+  }
   if (seg_nnz & GMR_SPMM_LANE_PLAN) {
     const int L = lane_l(seg_nnz);
     GMR_ARG(L, "lane plans take seg_nnz = GMR_SPMM_LANE_PLAN | 32, 64 or 128 (packed: 32)");
@@ -812,10 +1141,18 @@ extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_
   return GMR_OK;
 }
 
-extern "C" int gmr_spmm_plan_pack(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, int32_t seg_nnz,
-                                  int32_t* plan, void* stream) {
+extern "C" int gmr_spmm_plan_pack(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
+                                  int64_t nnz, int32_t seg_nnz, int32_t* plan, void* stream) {
   GMR_ARG(plan && (nnz == 0 || (col && val)), "null pointer");
   GMR_ARG(n_rows > 0 && n_rows < (1ll << 29) && nnz >= 0 && nnz < (1ll << 31), "bad size");
+  if (is_chunk(seg_nnz)) {
+    GMR_ARG(rowptr, "chunk plans are packed from the CSR: rowptr needed");
+    const int grid = (int)std::min<int64_t>((n_rows + 255) / 256, 2048);
+    hipLaunchKernelGGL(chunk_pack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, rowptr, col, val, (int)n_rows,
+                       nnz, plan);
+    GMR_LAUNCHED();
+    return GMR_OK;
+  }
   GMR_ARG(lane_l(seg_nnz) && lane_packed(seg_nnz), "not a packed lane plan");
   const int grid = (int)std::min<int64_t>((n_rows + 255) / 256, 2048);
   hipLaunchKernelGGL(lane_pack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, col, val, (int)n_rows, nnz, plan);
@@ -839,7 +1176,7 @@ extern "C" int gmr_spmm_panel_f32(const int32_t* col, const float* val, int64_t 
                                   const int32_t* plan, int32_t seg_nnz, int32_t n_blocks, const float* x_panel,
                                   int64_t panel_rows, float alpha, float beta, float* y, int64_t ldy, void* stream) {
   GMR_ARG(plan && y && x_panel && (nnz == 0 || (col && val)), "null pointer");
-  GMR_ARG(lane_l(seg_nnz), "column-panel sources need a lane plan");
+  GMR_ARG(lane_l(seg_nnz) || is_chunk(seg_nnz), "column-panel sources need a lane or chunk plan");
   GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "n_blocks must be 1, 2 or 4");
   GMR_ARG(n_rows > 0 && panel_rows > 0 && ldy >= 64 * n_blocks && ldy % 4 == 0, "bad shape");
   GMR_ARG((((uintptr_t)y | (uintptr_t)x_panel | (uintptr_t)plan) & 15) == 0, "pointers must be 16-byte aligned");
@@ -863,9 +1200,38 @@ extern "C" int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* 
   return GMR_OK;
 }
 
+static int chunk_wpx_cap() {  // workgroups per XCD of a chunk-plan launch (GMR_SPMM_CHUNK_WPX: tuning)
+  static const int cap = [] {
+    const char* s = getenv("GMR_SPMM_CHUNK_WPX");
+    const int v = s ? atoi(s) : 0;
+    return v > 0 && v <= 1024 ? v : 32;
+  }();
+  return cap;
+}
+
+static int chunk_launch(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
+                        int32_t n_blocks, const Src& s, float alpha, float beta, const Dst& d, hipStream_t st0) {
+  const int lpr = n_blocks == 4 ? 8 : 4;  // slices of 16 (d = 64, 128) or 32 (d = 256) columns
+  const int S = 16 * n_blocks / lpr;
+  const int64_t tasks = nnz / kChunkTask + 1;  // about one wave-task per 128 entries
+  const int64_t waves = (tasks + (8 / S) - 1) / (8 / S);
+  const int wpx = (int)std::max<int64_t>(1, std::min<int64_t>((waves + kChunkThreads / 64 - 1) / (kChunkThreads / 64),
+                                                              chunk_wpx_cap()));
+  const dim3 grid((unsigned)(8 * wpx));
+  if (lpr == 8)
+    hipLaunchKernelGGL(spmm_chunk_kernel<8>, grid, dim3(kChunkThreads), 0, st0, col, val, plan, (int)n_rows, nnz, S, wpx,
+                       s, alpha, beta, d);
+  else
+    hipLaunchKernelGGL(spmm_chunk_kernel<4>, grid, dim3(kChunkThreads), 0, st0, col, val, plan, (int)n_rows, nnz, S, wpx,
+                       s, alpha, beta, d);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
 static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
                        int32_t seg_nnz, int32_t n_blocks, const Src& s, float alpha, float beta, const Dst& d,
                        hipStream_t st0) {
+  if (is_chunk(seg_nnz)) return chunk_launch(col, val, n_rows, nnz, plan, n_blocks, s, alpha, beta, d, st0);
   // lanes per row: a slice is 4 * lpr columns (column panels are 16 wide below d = 256)
   const int lpr = s.panel_rows > 0 ? (n_blocks == 4 ? 8 : 4) : lane_lpr(n_blocks);
   const int S = 16 * n_blocks / lpr;      // column slices: 4 (d = 64), 8 (d = 128, 256)
@@ -895,7 +1261,7 @@ extern "C" int gmr_spmm_multi_f32(const int32_t* col, const float* val, int64_t 
                                   const int64_t* ld_lo, const float* const* x_hi, const int64_t* ld_hi, int64_t split,
                                   float alpha, float beta, float* const* y_blocks, const int64_t* ld_y, void* stream) {
   GMR_ARG(plan && x_lo && ld_lo && y_blocks && ld_y && (nnz == 0 || (col && val)), "null pointer");
-  GMR_ARG(lane_l(seg_nnz), "per-block outputs need a lane plan");
+  GMR_ARG(lane_l(seg_nnz) || is_chunk(seg_nnz), "per-block outputs need a lane or chunk plan");
   GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "n_blocks must be 1, 2 or 4");
   GMR_ARG(n_rows > 0 && nnz >= 0 && ((uintptr_t)plan & 15) == 0, "bad shape");
   Src s;
@@ -940,6 +1306,11 @@ extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const
     GMR_ARG(s.ld_lo[b] % 4 == 0 && s.ld_hi[b] % 4 == 0, "source ld must be a multiple of 4");
   }
   hipStream_t st0 = (hipStream_t)stream;
+  if (is_chunk(seg_nnz)) {
+    GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
+    return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, dst_rowmajor(y, ldy, n_blocks),
+                       st0);
+  }
   if (seg_nnz & GMR_SPMM_LANE_PLAN) {
     GMR_ARG(lane_l(seg_nnz), "bad lane plan seg_nnz");
     GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");

@@ -235,6 +235,7 @@ SPMM_SEG_NNZ = SPMM_LANE_PLAN | 32
 # bit-identical sums, 4-7 % faster there at d = 128/256 and slower on the small rebuilt UI graphs
 # (scripts/spmm_bench.py, profiles/r01g_spmm_packed_bench.txt)
 SPMM_NORM_ADJ = SPMM_PACKED | SPMM_LANE_PLAN | 32
+SPMM_CHUNK = 1 << 18  # chunk plan: whole-row tasks of <= 128 entries, one gather round per wave (include/gmr.h)
 
 
 class CSR:
@@ -254,9 +255,9 @@ class CSR:
         prow = _lib.load().gmr_spmm_partial_rows(self.n_rows, self.nnz, seg_nnz)
         self.partial = torch.zeros((prow, 256), dtype=torch.float32, device=dev)
         _lib.call("gmr_spmm_plan_build", ptr(rowptr), self.n_rows, self.nnz, seg_nnz, ptr(self.plan), stream())
-        if seg_nnz & SPMM_PACKED:  # col/val are final here (every CSR is built before it is wrapped)
-            _lib.call("gmr_spmm_plan_pack", ptr(col), ptr(val), self.n_rows, self.nnz, seg_nnz, ptr(self.plan),
-                      stream())
+        if seg_nnz & SPMM_PACKED or seg_nnz == SPMM_CHUNK:  # col/val are final here (built before wrapping)
+            _lib.call("gmr_spmm_plan_pack", ptr(rowptr), ptr(col), ptr(val), self.n_rows, self.nnz, seg_nnz,
+                      ptr(self.plan), stream())
         hdr = (ctypes.c_int32 * 4)()
         _lib.call("gmr_spmm_plan_info", ptr(self.plan), hdr, stream())  # one sync per graph build
         self.plan_header = tuple(hdr)

@@ -73,11 +73,17 @@ int gmr_stream_fork(void* from, void* to, void* ev);
  *            gmr_spmm_plan_build, and again whenever col/val change): a row's entries are found
  *            from a degree-bucket table, so no descriptor load sits on the gather chain and the
  *            next rows' entries load while the current gathers land.  Same sums, bit for bit.
+ *   GMR_SPMM_CHUNK_PLAN: chunk plan — rows of degree 1..128 cut in row order into tasks of whole
+ *            rows holding <= 128 entries; a wave gathers a task's entries in one round whatever
+ *            rows they belong to (no idle gather slots on short rows), row sums crossing lane
+ *            groups meet in LDS in a fixed order; rows of degree > 128 take a workgroup each;
+ *            X sliced per XCD as in the lane plan.  Needs gmr_spmm_plan_pack after the build.
  * All are deterministic.  flags: GMR_SPMM_NO_SPLIT_ROWS when the segment plan has no row
  * longer than seg_nnz (gmr_spmm_plan_info header word 1 == 0): the combine pass is skipped. */
 #define GMR_SPMM_NO_SPLIT_ROWS 1
 #define GMR_SPMM_LANE_PLAN (1 << 16)
 #define GMR_SPMM_PACKED (1 << 17)
+#define GMR_SPMM_CHUNK_PLAN (1 << 18)
 int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_nnz);
 int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t seg_nnz);
 int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t seg_nnz, int32_t* plan,
@@ -85,8 +91,8 @@ int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int3
 /* Copies the 4-word plan header to the host (synchronises the stream): segment plan
  * {n_segments, n_split_rows, n_partials, 0}; blocked plan {n_blocks, 0, 0, seg_nnz};
  * lane plan {n_hub_rows, n_short_rows, packed (0/1), L}. */
-int gmr_spmm_plan_pack(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, int32_t seg_nnz,
-                       int32_t* plan, void* stream);
+int gmr_spmm_plan_pack(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
+                       int32_t seg_nnz, int32_t* plan, void* stream);
 /* Lane-plan SpMM with X in column-panel layout: S contiguous panels of panel_rows x W floats
  * (W = 16 for n_blocks 1 and 2, 32 for 4; S = 64 * n_blocks / W), panel s holding columns
  * [s*W, (s+1)*W) of X, so each XCD's slice occupies whole cache lines.  Same sums as

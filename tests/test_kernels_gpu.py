@@ -89,8 +89,9 @@ def test_bipartite_build_many_items(K):
     assert np.array_equal(csr.val.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
 
 
-LANE32, PACKED32 = (1 << 16) | 32, (1 << 17) | (1 << 16) | 32
-SPMM_SEGS = [64, 128, 512, 2048, LANE32, (1 << 16) | 64, (1 << 16) | 128, PACKED32]  # segment, blocked, lane, packed
+LANE32, PACKED32, CHUNK = (1 << 16) | 32, (1 << 17) | (1 << 16) | 32, 1 << 18
+# segment, blocked, lane, packed lane, chunk plans
+SPMM_SEGS = [64, 128, 512, 2048, LANE32, (1 << 16) | 64, (1 << 16) | 128, PACKED32, CHUNK]
 
 
 @pytest.mark.parametrize("seg", SPMM_SEGS)
@@ -164,7 +165,7 @@ def test_spmm_packed_bit_exact_vs_lane(K, nb):
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
 
 
-@pytest.mark.parametrize("seg", [LANE32, PACKED32])
+@pytest.mark.parametrize("seg", [LANE32, PACKED32, CHUNK])
 @pytest.mark.parametrize("nb", [1, 2, 4])
 def test_spmm_panel_sources_bit_exact(K, nb, seg):
     """gmr_spmm_panel_f32: X as column panels gives the row-major product bit for bit."""
@@ -236,7 +237,7 @@ def test_spmm_multi_outputs_bit_exact(K, seg):
     np.testing.assert_allclose(K2.cpu().numpy(), K1.cpu().numpy(), rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("seg", [128, LANE32, (1 << 16) | 128, PACKED32])
+@pytest.mark.parametrize("seg", [128, LANE32, (1 << 16) | 128, PACKED32, CHUNK])
 def test_spmm_empty_runs_and_repeat(K, seg):
     """Long runs of empty rows, a tiny and an empty matrix,
     and repeated products: bit-identical
@@ -424,3 +425,34 @@ def test_contrast_fused_vs_fp64(K, B, n):
     got_dt = dbuf[off:off + n, 64:].cpu().numpy()
     np.testing.assert_allclose(got_dt, want_dt, rtol=2e-4, atol=2e-4 * np.abs(want_dt).max())
     assert np.isnan(dbuf[:off].cpu().numpy()).all() and np.isnan(dbuf[off:off + n, :64].cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("nb", [1, 2, 4])
+def test_spmm_chunk_rows_spanning_groups(K, nb):
+    """Chunk plan: rows of degree 1..128 packed into 128-entry tasks, many of them crossing the
+    8- / 16-entry lane-group boundaries (degrees 1, 2, 7, 9, 15, 17, 33, 64, 100, 127, 128, 129),
+    hub rows of thousands and empty rows; against fp64 and bit-identical across repeats."""
+    rng = _rng(11)
+    n = 5000
+    degs = np.array([1, 2, 7, 9, 15, 17, 33, 64, 100, 127, 128, 129, 0, 3000])
+    deg = rng.choice(degs, size=n, p=[.2, .2, .1, .1, .05, .05, .05, .05, .05, .04, .04, .03, .03, .01])
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    col = rng.integers(0, n, size=int(rp[-1])).astype(np.int32)
+    val = rng.standard_normal(col.size).astype(np.float32)
+    g = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=CHUNK)
+    hdr = g.plan_header
+    assert hdr[0] == int((deg > 128).sum()) and hdr[2] == int((deg == 0).sum())
+    assert hdr[3] == int(deg[(deg > 0) & (deg <= 128)].sum())
+    X = rng.standard_normal((n, 64 * nb)).astype(np.float32)
+    Y0 = rng.standard_normal((n, 64 * nb)).astype(np.float32)
+    Xd = _dev(X)
+    outs = []
+    for _ in range(2):
+        Yd = _dev(Y0)
+        g.spmm(Yd, [(Xd[:, 64 * b:64 * (b + 1)],) for b in range(nb)], alpha=0.8, beta=0.4)
+        outs.append(Yd.cpu().numpy())
+    A = np.zeros((n, n))
+    np.add.at(A, (np.repeat(np.arange(n), deg), col), val.astype(np.float64))
+    want = 0.8 * (A @ X.astype(np.float64)) + 0.4 * Y0
+    np.testing.assert_allclose(outs[0], want, rtol=1e-5, atol=1e-4)
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
