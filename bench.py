@@ -266,6 +266,8 @@ def run_workload(args, dist_on, barrier, max_over_ranks, with_cpu_baseline):
     t0 = time.time()
     for i in range(args.steps):
         trainer._train_epoch(tl, args.warmup + i)
+        if getattr(trainer, "phase_ms", None):
+            log("phases [ms]: diffusion %.2f, rebuild %.2f, bpr %.2f" % trainer.phase_ms)
     barrier()
     dt = max_over_ranks(time.time() - t0)
     train_ups = U * args.steps / dt

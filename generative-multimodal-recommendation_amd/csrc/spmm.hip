@@ -457,23 +457,45 @@ __global__ void __launch_bounds__(kBlkThreads) spmm_blk_kernel(const int* __rest
 //   * the grid is a bounded number of workgroups per XCD that loop over the work, so few waves
 //     are launched.  One launch, no partial buffer; every row is summed in a fixed order
 //     wherever it lands, so results are deterministic.
-// Plan: hdr {n_hub, n_short, 0, L}, then n_rows x int4 {row, beg, end, 0}: hub rows (longest
-// first by power of two), then the others by descending degree (rows of one class in any order).
+// Plan: hdr {n_hub_desc, n_short, packed | n_split << 1, L}, then int4 {row, beg, end, slot}
+// descriptors: hub segments (rows longest first by power of two), then the short rows by
+// descending degree (rows of one class in any order).  A hub row longer than kHubSeg entries is
+// cut into kHubSeg-entry segments, each its own workgroup (the rebuilt UI graphs can have one
+// item row holding most users: a single workgroup walking it was the launch's whole tail); the
+// segments write partial sums to partial[slot] and a fixup pass adds them in segment order
+// (lane_fix list {row, first slot, n_segments, 0}), so the sum order stays fixed.
 constexpr int kLaneThreads = 256;
 constexpr int kPackTab = 34;  // packed lane plan: bucket-table entries per column (see below)
 constexpr int kLaneMaxBuckets = 160;
+constexpr int kHubSeg = 1024;  // entries per hub segment
+
+__host__ __device__ inline int64_t lane_desc_cap(int64_t n_rows, int64_t nnz) { return n_rows + nnz / kHubSeg + 1; }
+__host__ __device__ inline int64_t lane_fix_cap(int64_t nnz) { return nnz / kHubSeg + 1; }
+__host__ __device__ inline int64_t lane_fix_off(int64_t n_rows, int64_t nnz) {
+  return kPlanHdr + 4 * lane_desc_cap(n_rows, nnz);
+}
+__host__ __device__ inline int64_t lane_tab_off(int64_t n_rows, int64_t nnz) {
+  return lane_fix_off(n_rows, nnz) + 4 * lane_fix_cap(nnz);
+}
 
 __device__ __forceinline__ int lane_bucket(int deg, int L, int HB) {
   return deg > L ? 30 - (31 - __clz(deg)) : HB + (L - deg);
 }
 
-__global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__ rowptr, int n_rows, int L, int HB,
-                                                         int packed, int* __restrict__ plan) {
+__host__ __device__ inline int hub_segs(int deg) { return (deg + kHubSeg - 1) / kHubSeg; }
+
+__global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__ rowptr, int n_rows, int64_t nnz, int L,
+                                                         int HB, int packed, int* __restrict__ plan) {
   __shared__ int s_cnt[kLaneMaxBuckets], s_off[kLaneMaxBuckets];
+  __shared__ int s_slot, s_nfix;
   const int t = threadIdx.x, nbk = HB + L + 1;
   for (int i = t; i < nbk; i += 1024) s_cnt[i] = 0;
+  if (t == 0) s_slot = s_nfix = 0;
   __syncthreads();
-  for (int r = t; r < n_rows; r += 1024) atomicAdd(&s_cnt[lane_bucket(rowptr[r + 1] - rowptr[r], L, HB)], 1);
+  for (int r = t; r < n_rows; r += 1024) {
+    const int deg = rowptr[r + 1] - rowptr[r];
+    atomicAdd(&s_cnt[lane_bucket(deg, L, HB)], deg > L ? hub_segs(deg) : 1);  // one descriptor per hub segment
+  }
   __syncthreads();
   if (t == 0) {
     int o = 0, n_hub = 0;
@@ -483,26 +505,56 @@ __global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__
       if (b == HB - 1) n_hub = o;
     }
     plan[0] = n_hub;
-    plan[1] = n_rows - n_hub;
-    plan[2] = packed;
+    plan[1] = o - n_hub;
     plan[3] = L;
     if (packed) {  // bucket j = degree L - j: first plan index and first packed entry
-      int* tb = plan + kPlanHdr + 4 * n_rows;
+      int* tb = plan + lane_tab_off(n_rows, nnz);
       int e = 0;
       for (int j = 0; j <= L; ++j) {
         tb[j] = s_off[HB + j];
         tb[kPackTab + j] = e;
         e += s_cnt[HB + j] * (L - j);
       }
-      tb[L + 1] = n_rows;
+      tb[L + 1] = o;
       tb[kPackTab + L + 1] = e;
     }
   }
   __syncthreads();
   int4* desc = reinterpret_cast<int4*>(plan + kPlanHdr);
+  int4* fix = reinterpret_cast<int4*>(plan + lane_fix_off(n_rows, nnz));
   for (int r = t; r < n_rows; r += 1024) {
-    const int beg = rowptr[r], end = rowptr[r + 1];
-    desc[atomicAdd(&s_off[lane_bucket(end - beg, L, HB)], 1)] = make_int4(r, beg, end, 0);
+    const int beg = rowptr[r], end = rowptr[r + 1], deg = end - beg;
+    const int ns = deg > L ? hub_segs(deg) : 1;
+    const int d0 = atomicAdd(&s_off[lane_bucket(deg, L, HB)], ns);
+    if (ns == 1) {
+      desc[d0] = make_int4(r, beg, end, -1);
+    } else {  // segments j of the row write partial[slot0 + j]; the fixup adds them in j order
+      const int slot0 = atomicAdd(&s_slot, ns);
+      fix[atomicAdd(&s_nfix, 1)] = make_int4(r, slot0, ns, 0);
+      for (int j = 0; j < ns; ++j)
+        desc[d0 + j] = make_int4(r, beg + j * kHubSeg, min(end, beg + (j + 1) * kHubSeg), slot0 + j);
+    }
+  }
+  __syncthreads();
+  if (t == 0) plan[2] = packed | (s_nfix << 1);
+}
+
+// hub-segment fixup: y[row] = alpha * sum_j partial[slot0 + j] + beta * y[row], j in order
+__global__ void __launch_bounds__(256) lane_fix_kernel(const int* __restrict__ plan, int64_t n_rows, int64_t nnz,
+                                                       int ncols, const float* __restrict__ part, float alpha,
+                                                       float beta, Dst dst) {
+  const int n_fix = plan[2] >> 1;
+  const int4* fix = reinterpret_cast<const int4*>(plan + lane_fix_off(n_rows, nnz));
+  const int c4n = ncols / 4;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_fix * c4n; i += gridDim.x * blockDim.x) {
+    const int f = i / c4n, c = (i % c4n) * 4;
+    const int4 fx = fix[f];
+    float4 s = *reinterpret_cast<const float4*>(part + (int64_t)fx.y * 256 + c);
+    for (int j = 1; j < fx.z; ++j) s = gmr::f4_add(s, *reinterpret_cast<const float4*>(part + (int64_t)(fx.y + j) * 256 + c));
+    float* yp = dst.y[c >> 6] + (int64_t)fx.x * dst.ld[c >> 6] + (c & 63);
+    float4 o = gmr::f4_scale(alpha, s);
+    if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
+    *reinterpret_cast<float4*>(yp) = o;
   }
 }
 
@@ -512,16 +564,18 @@ __global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__
 // the critical path), and the next pass's col/val are in flight while the current gathers land.
 // Plan words after the descriptors: table {first plan index}[34] {first entry}[34], then
 // pcol[nnz], pval[nnz].  Entries keep their CSR order, so sums are bit-identical to the lane plan.
-__host__ __device__ inline int64_t pack_off(int64_t n_rows) { return kPlanHdr + 4 * n_rows + 2 * kPackTab; }
+__host__ __device__ inline int64_t pack_off(int64_t n_rows, int64_t nnz) {
+  return lane_tab_off(n_rows, nnz) + 2 * kPackTab;
+}
 
 __global__ void __launch_bounds__(256) lane_pack_kernel(const int* __restrict__ col, const float* __restrict__ val,
                                                         int n_rows, int64_t nnz, int* __restrict__ plan) {
-  const int n_hub = plan[0], L = plan[3];
-  const int* tb = plan + kPlanHdr + 4 * n_rows;
+  const int n_hub = plan[0], L = plan[3], n_desc = plan[0] + plan[1];
+  const int* tb = plan + lane_tab_off(n_rows, nnz);
   const int4* desc = reinterpret_cast<const int4*>(plan + kPlanHdr);
-  int* pcol = plan + pack_off(n_rows);
+  int* pcol = plan + pack_off(n_rows, nnz);
   float* pval = reinterpret_cast<float*>(pcol + nnz);
-  for (int k = n_hub + blockIdx.x * blockDim.x + threadIdx.x; k < n_rows; k += gridDim.x * blockDim.x) {
+  for (int k = n_hub + blockIdx.x * blockDim.x + threadIdx.x; k < n_desc; k += gridDim.x * blockDim.x) {
     const int4 d = desc[k];
     const int deg = d.z - d.y, j = L - deg;
     const int e0 = tb[kPackTab + j] + (k - tb[j]) * deg;
@@ -537,7 +591,7 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
                                                                   const float* __restrict__ val,
                                                                   const int* __restrict__ plan, int S, int wpx, Src src,
                                                                   float alpha, float beta, Dst dst, int n_rows,
-                                                                  int64_t nnz) {
+                                                                  int64_t nnz, float* __restrict__ hub_part) {
   constexpr int NW = kLaneThreads / 64;  // waves per workgroup
   constexpr int NG = 64 / LPR;           // lane groups per wave
   constexpr int EPL = EB / LPR;          // col/val words per lane per batch
@@ -603,7 +657,7 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
   const int wg = part * wpx + k, n_wg = P * wpx;
   __shared__ int s_tb[2 * kPackTab];
   if (PACKED) {
-    if (threadIdx.x < 2 * kPackTab) s_tb[threadIdx.x] = plan[kPlanHdr + 4 * n_rows + threadIdx.x];
+    if (threadIdx.x < 2 * kPackTab) s_tb[threadIdx.x] = plan[lane_tab_off(n_rows, nnz) + threadIdx.x];
     __syncthreads();
   }
   // hub rows: one workgroup each; group partials meet in a fixed butterfly + LDS order
@@ -618,7 +672,10 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
       float4 s = s_red[0][sub];
 #pragma unroll
       for (int q = 1; q < NW; ++q) s = gmr::f4_add(s, s_red[q][sub]);
-      store(d.x, s);
+      if (d.w < 0)
+        store(d.x, s);
+      else  // a segment of a split hub row: partial row d.w, full-width columns (lane_fix_kernel adds them)
+        *reinterpret_cast<float4*>(hub_part + (int64_t)d.w * 256 + c0 + sub * 4) = s;
     }
     __syncthreads();
   }
@@ -628,7 +685,7 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
   int base = (wg * NW + wid) * NG;
   if constexpr (PACKED) {
     constexpr int EM = 32 / LPR;  // col/val words per lane of a degree-32 row
-    const int* __restrict__ pcol = plan + pack_off(n_rows);
+    const int* __restrict__ pcol = plan + pack_off(n_rows, nnz);
     const float* __restrict__ pval = reinterpret_cast<const float*>(pcol + nnz);
     const int* __restrict__ drow = plan + kPlanHdr;  // desc[k].x = plan + kPlanHdr + 4k
     // row, degree and entries of short row `base + grp` (bucket j: largest j with s_tb[j] <= k)
@@ -1090,7 +1147,7 @@ extern "C" int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_
   if (is_chunk(seg_nnz)) return chunk_plan_words(n_rows, nnz);
   if (seg_nnz & GMR_SPMM_LANE_PLAN) {
     if (!lane_l(seg_nnz)) return -1;
-    return lane_packed(seg_nnz) ? pack_off(n_rows) + 2 * nnz : kPlanHdr + 4 * n_rows;
+    return lane_packed(seg_nnz) ? pack_off(n_rows, nnz) + 2 * nnz : lane_tab_off(n_rows, nnz);
   }
   if (seg_nnz <= 0) return -1;
   if (seg_nnz >= 512) return kPlanHdr + 2 * (blk_max_blocks(n_rows, nnz, seg_nnz) + 1);
@@ -1099,7 +1156,8 @@ extern "C" int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_
 
 extern "C" int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t seg_nnz) {
   if (is_chunk(seg_nnz)) return 1;  // spanning rows meet in LDS
-  if (seg_nnz & GMR_SPMM_LANE_PLAN) return lane_l(seg_nnz) ? 1 : -1;  // hub rows are combined in LDS
+  // split hub rows: one 256-float partial row per segment (lane_fix_kernel)
+  if (seg_nnz & GMR_SPMM_LANE_PLAN) return lane_l(seg_nnz) ? 2 * (nnz / kHubSeg) + 2 : -1;
   if (seg_nnz <= 0) return -1;
   if (seg_nnz >= 512) return 1;  // the blocked variant combines in LDS
   return 2 * ((nnz + seg_nnz - 1) / seg_nnz) + 2;
@@ -1119,7 +1177,7 @@ extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_
     const int L = lane_l(seg_nnz);
     GMR_ARG(L, "lane plans take seg_nnz = GMR_SPMM_LANE_PLAN | 32, 64 or 128 (packed: 32)");
     GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
-    hipLaunchKernelGGL(lane_plan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, (int)n_rows, L,
+    hipLaunchKernelGGL(lane_plan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, (int)n_rows, nnz, L,
                        lane_hb(L), (int)lane_packed(seg_nnz), plan);
     GMR_LAUNCHED();
     return GMR_OK;
@@ -1162,7 +1220,7 @@ extern "C" int gmr_spmm_plan_pack(const int32_t* rowptr, const int32_t* col, con
 
 static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
                        int32_t seg_nnz, int32_t n_blocks, const Src& s, float alpha, float beta, const Dst& d,
-                       hipStream_t st0);
+                       float* partial, int32_t flags, hipStream_t st0);
 static Dst dst_rowmajor(float* y, int64_t ldy, int n_blocks) {
   Dst d;
   for (int b = 0; b < 4; ++b) {
@@ -1174,7 +1232,8 @@ static Dst dst_rowmajor(float* y, int64_t ldy, int n_blocks) {
 
 extern "C" int gmr_spmm_panel_f32(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                                   const int32_t* plan, int32_t seg_nnz, int32_t n_blocks, const float* x_panel,
-                                  int64_t panel_rows, float alpha, float beta, float* y, int64_t ldy, void* stream) {
+                                  int64_t panel_rows, float alpha, float beta, float* y, int64_t ldy, float* partial,
+                                  int32_t flags, void* stream) {
   GMR_ARG(plan && y && x_panel && (nnz == 0 || (col && val)), "null pointer");
   GMR_ARG(lane_l(seg_nnz) || is_chunk(seg_nnz), "column-panel sources need a lane or chunk plan");
   GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "n_blocks must be 1, 2 or 4");
@@ -1188,7 +1247,7 @@ extern "C" int gmr_spmm_panel_f32(const int32_t* col, const float* val, int64_t 
   s.split = panel_rows;
   s.panel_rows = panel_rows;
   return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, dst_rowmajor(y, ldy, n_blocks),
-                     (hipStream_t)stream);
+                     partial, flags, (hipStream_t)stream);
 }
 
 extern "C" int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream) {
@@ -1230,7 +1289,7 @@ static int chunk_launch(const int32_t* col, const float* val, int64_t n_rows, in
 
 static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
                        int32_t seg_nnz, int32_t n_blocks, const Src& s, float alpha, float beta, const Dst& d,
-                       hipStream_t st0) {
+                       float* partial, int32_t flags, hipStream_t st0) {
   if (is_chunk(seg_nnz)) return chunk_launch(col, val, n_rows, nnz, plan, n_blocks, s, alpha, beta, d, st0);
   // lanes per row: a slice is 4 * lpr columns (column panels are 16 wide below d = 256)
   const int lpr = s.panel_rows > 0 ? (n_blocks == 4 ? 8 : 4) : lane_lpr(n_blocks);
@@ -1242,7 +1301,7 @@ static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int
   const dim3 grid((unsigned)(8 * wpx));
 #define GMR_LANE_LAUNCH(LPRV, PK, EBV)                                                                      \
   hipLaunchKernelGGL((spmm_lane_kernel<LPRV, PK, EBV>), grid, dim3(kLaneThreads), 0, st0, col, val, plan, S, wpx, \
-                   s, alpha, beta, d, (int)n_rows, nnz)
+                   s, alpha, beta, d, (int)n_rows, nnz, partial)
   const bool wide = lane_eb() == 16;  // entries gathered per lane group and batch
   if (lpr == 8) {
     if (packed) { if (wide) GMR_LANE_LAUNCH(8, true, 16); else GMR_LANE_LAUNCH(8, true, 8); }
@@ -1253,13 +1312,23 @@ static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int
   }
 #undef GMR_LANE_LAUNCH
   GMR_LAUNCHED();
+  if (flags & GMR_SPMM_HUB_FIXUP) {  // the plan split hub rows: add their segment partials in order
+    if (!partial) {
+      gmr::set_error("gmr_spmm", "plan has split hub rows (GMR_SPMM_HUB_FIXUP): partial buffer needed");
+      return GMR_ERR_ARG;
+    }
+    hipLaunchKernelGGL(lane_fix_kernel, dim3(32), dim3(256), 0, st0, plan, n_rows, nnz, 64 * n_blocks, partial, alpha,
+                       beta, d);
+    GMR_LAUNCHED();
+  }
   return GMR_OK;
 }
 
 extern "C" int gmr_spmm_multi_f32(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                                   const int32_t* plan, int32_t seg_nnz, int32_t n_blocks, const float* const* x_lo,
                                   const int64_t* ld_lo, const float* const* x_hi, const int64_t* ld_hi, int64_t split,
-                                  float alpha, float beta, float* const* y_blocks, const int64_t* ld_y, void* stream) {
+                                  float alpha, float beta, float* const* y_blocks, const int64_t* ld_y,
+                                  float* partial, int32_t flags, void* stream) {
   GMR_ARG(plan && x_lo && ld_lo && y_blocks && ld_y && (nnz == 0 || (col && val)), "null pointer");
   GMR_ARG(lane_l(seg_nnz) || is_chunk(seg_nnz), "per-block outputs need a lane or chunk plan");
   GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "n_blocks must be 1, 2 or 4");
@@ -1280,7 +1349,8 @@ extern "C" int gmr_spmm_multi_f32(const int32_t* col, const float* val, int64_t 
     GMR_ARG((((uintptr_t)s.lo[b] | (uintptr_t)s.hi[b] | (uintptr_t)d.y[b]) & 15) == 0, "blocks must be 16-byte aligned");
     GMR_ARG(s.ld_lo[b] % 4 == 0 && s.ld_hi[b] % 4 == 0 && d.ld[b] % 4 == 0 && d.ld[b] >= 64, "bad block stride");
   }
-  return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, d, (hipStream_t)stream);
+  return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, d, partial, flags,
+                     (hipStream_t)stream);
 }
 
 extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
@@ -1309,13 +1379,13 @@ extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const
   if (is_chunk(seg_nnz)) {
     GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
     return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, dst_rowmajor(y, ldy, n_blocks),
-                       st0);
+                       partial, flags, st0);
   }
   if (seg_nnz & GMR_SPMM_LANE_PLAN) {
     GMR_ARG(lane_l(seg_nnz), "bad lane plan seg_nnz");
     GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
     return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, dst_rowmajor(y, ldy, n_blocks),
-                       st0);
+                       partial, flags, st0);
   }
   if (seg_nnz >= 512) {
     const int64_t mb = blk_max_blocks(n_rows, nnz, seg_nnz);

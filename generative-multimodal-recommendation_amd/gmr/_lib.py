@@ -33,8 +33,8 @@ SIGNATURES = {
     "gmr_event_destroy": (I32, [P]),
     "gmr_stream_fork": (I32, [P, P, P]),
     "gmr_score_f16": (I32, [I64, I64, I64, P, I64, P, I64, P, I64, P]),
-    "gmr_spmm_multi_f32": (I32, [P, P, I64, I64, P, I32, I32, P, P, P, P, I64, F32, F32, P, P, P]),
-    "gmr_spmm_panel_f32": (I32, [P, P, I64, I64, P, I32, I32, P, I64, F32, F32, P, I64, P]),
+    "gmr_spmm_multi_f32": (I32, [P, P, I64, I64, P, I32, I32, P, P, P, P, I64, F32, F32, P, P, P, I32, P]),
+    "gmr_spmm_panel_f32": (I32, [P, P, I64, I64, P, I32, I32, P, I64, F32, F32, P, I64, P, I32, P]),
     "gmr_spmm_csr_f32": (I32, [P, P, P, I64, I64, P, I32, P, I32, P, P, P, P, I64, F32, F32, P, I64, I32, P]),
     "gmr_bipartite_nnz": (I64, [I64, I64, I64, I32]),
     "gmr_bipartite_workspace_ints": (I64, [I64, I64]),

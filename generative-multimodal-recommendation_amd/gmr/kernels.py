@@ -228,6 +228,7 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
 # (see include/gmr.h).  The lane plan with L = 32 measured fastest on the DiffMM graphs
 # (scripts/spmm_bench.py, profiles/r01_spmm_lane_bench.txt).
 SPMM_NO_SPLIT_ROWS = 1
+SPMM_HUB_FIXUP = 2  # lane plan with split hub rows: the launch adds their segment partials (include/gmr.h)
 SPMM_LANE_PLAN = 1 << 16  # | L (32, 64, 128): lane plan (include/gmr.h)
 SPMM_PACKED = 1 << 17  # | SPMM_LANE_PLAN | 32: packed lane plan (col/val of short rows in plan order)
 SPMM_SEG_NNZ = SPMM_LANE_PLAN | 32
@@ -261,8 +262,10 @@ class CSR:
         hdr = (ctypes.c_int32 * 4)()
         _lib.call("gmr_spmm_plan_info", ptr(self.plan), hdr, stream())  # one sync per graph build
         self.plan_header = tuple(hdr)
-        # segment plan without split rows: the combine pass is skipped
+        # segment plan without split rows: the combine pass is skipped; lane plan with split hubs: fixup pass
         self.flags = SPMM_NO_SPLIT_ROWS if (seg_nnz < 512 and hdr[1] == 0) else 0
+        if seg_nnz & SPMM_LANE_PLAN and hdr[2] >> 1:
+            self.flags |= SPMM_HUB_FIXUP
 
     def spmm(self, out, blocks, split=None, alpha=1.0, beta=0.0, partial=None):
         """out = alpha * A @ X + beta * out; X = column blocks [(lo, hi), ...] of 64 columns each.
@@ -306,7 +309,7 @@ def score_f16(a, b, out):
     return out
 
 
-def spmm_multi(a, outs, blocks, split=None, alpha=1.0, beta=0.0):
+def spmm_multi(a, outs, blocks, split=None, alpha=1.0, beta=0.0, partial=None):
     """One lane-plan launch for independent products of `a`: block b (64 columns, a (lo, hi) split
     source as in CSR.spmm) lands in outs[b] (an n_rows x 64 view).  gmr_spmm_multi_f32."""
     nb = len(blocks)
@@ -327,11 +330,12 @@ def spmm_multi(a, outs, blocks, split=None, alpha=1.0, beta=0.0):
     ldy = LArr(*[_ld(o) for o in outs] + [0] * (4 - nb))
     with _Probe("spmm", (a.nnz, a.n_rows, a.n_cols, nb, beta != 0.0)):
         _lib.call("gmr_spmm_multi_f32", ptr(a.col), ptr(a.val), a.n_rows, a.nnz, ptr(a.plan), a.seg_nnz, nb, lo, ldl,
-                  hi, ldh, split, float(alpha), float(beta), ys, ldy, stream())
+                  hi, ldh, split, float(alpha), float(beta), ys, ldy, ptr(a.partial if partial is None else partial),
+                  a.flags, stream())
     return outs
 
 
-def spmm_panel(a, out, x_panel, nb, alpha=1.0, beta=0.0):
+def spmm_panel(a, out, x_panel, nb, alpha=1.0, beta=0.0, partial=None):
     """out = alpha * A @ X + beta * out with X given in column-panel layout (S, n, W), see
     include/gmr.h gmr_spmm_panel_f32 (lane plans only)."""
     W = 32 if nb == 4 else 16
@@ -341,7 +345,8 @@ def spmm_panel(a, out, x_panel, nb, alpha=1.0, beta=0.0):
         raise ValueError("out shape")
     with _Probe("spmm", (a.nnz, a.n_rows, a.n_cols, nb, beta != 0.0)):
         _lib.call("gmr_spmm_panel_f32", ptr(a.col), ptr(a.val), a.n_rows, a.nnz, ptr(a.plan), a.seg_nnz, nb,
-                  ptr(x_panel), a.n_cols, float(alpha), float(beta), ptr(out), _ld(out), stream())
+                  ptr(x_panel), a.n_cols, float(alpha), float(beta), ptr(out), _ld(out),
+                  ptr(a.partial if partial is None else partial), a.flags, stream())
     return out
 
 

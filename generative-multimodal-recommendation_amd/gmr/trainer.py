@@ -387,9 +387,21 @@ class DiffMMTrainer(Trainer):
         return steps
 
     def _train_epoch(self, train_data, epoch_idx, loss_func=None):
+        timed = os.environ.get("GMR_PHASE_TIMES") == "1"  # phase wall times (adds 3 device syncs)
+        t0 = time()
         steps = self.diffusion_phase(epoch_idx)
+        if timed:
+            torch.cuda.synchronize()
+            t1 = time()
         self.model.rebuild_ui_graphs()                      # trainer.py:529-576
+        if timed:
+            torch.cuda.synchronize()
+            t2 = time()
         rec_loss, batches = super()._train_epoch(train_data, epoch_idx)
+        if timed:
+            t3 = time()
+            self.phase_ms = (1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (t3 - t2))
+            self.logger.info("phases [ms]: diffusion %.2f, rebuild %.2f, bpr %.2f" % self.phase_ms)
         dl = self._dloss.cpu().numpy() / max(steps, 1)
         self.logger.info(f"Diffusion Loss: Image={dl[0]:.4f}, Text={dl[1]:.4f}")
         return rec_loss, batches

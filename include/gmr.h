@@ -81,6 +81,9 @@ int gmr_stream_fork(void* from, void* to, void* ev);
  * All are deterministic.  flags: GMR_SPMM_NO_SPLIT_ROWS when the segment plan has no row
  * longer than seg_nnz (gmr_spmm_plan_info header word 1 == 0): the combine pass is skipped. */
 #define GMR_SPMM_NO_SPLIT_ROWS 1
+/* lane plans whose hub rows were split into segments (plan header word 2 >> 1 > 0): the launch
+ * adds the segment partials (partial buffer of gmr_spmm_partial_rows x 256 floats) in order. */
+#define GMR_SPMM_HUB_FIXUP 2
 #define GMR_SPMM_LANE_PLAN (1 << 16)
 #define GMR_SPMM_PACKED (1 << 17)
 #define GMR_SPMM_CHUNK_PLAN (1 << 18)
@@ -90,7 +93,8 @@ int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int3
                         void* stream);
 /* Copies the 4-word plan header to the host (synchronises the stream): segment plan
  * {n_segments, n_split_rows, n_partials, 0}; blocked plan {n_blocks, 0, 0, seg_nnz};
- * lane plan {n_hub_rows, n_short_rows, packed (0/1), L}. */
+ * lane plan {n_hub_descriptors, n_short_rows, packed | n_split_hub_rows << 1, L}; chunk plan
+ * {n_hub_rows, n_tasks, n_empty_rows, n_packed_entries}. */
 int gmr_spmm_plan_pack(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                        int32_t seg_nnz, int32_t* plan, void* stream);
 /* Lane-plan SpMM with X in column-panel layout: S contiguous panels of panel_rows x W floats
@@ -99,14 +103,14 @@ int gmr_spmm_plan_pack(const int32_t* rowptr, const int32_t* col, const float* v
  * gmr_spmm_csr_f32 on the row-major X. */
 int gmr_spmm_panel_f32(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
                        int32_t seg_nnz, int32_t n_blocks, const float* x_panel, int64_t panel_rows, float alpha,
-                       float beta, float* y, int64_t ldy, void* stream);
+                       float beta, float* y, int64_t ldy, float* partial, int32_t flags, void* stream);
 /* Lane-plan SpMM with one output per 64-column block: block b goes to y_blocks[b] (row stride
  * ld_y[b]; host arrays of device pointers / strides).  Fuses independent products of one matrix
  * (DiffMM's H and K2) into one launch; same sums as the separate gmr_spmm_csr_f32 calls. */
 int gmr_spmm_multi_f32(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
                        int32_t seg_nnz, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
                        const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
-                       float* const* y_blocks, const int64_t* ld_y, void* stream);
+                       float* const* y_blocks, const int64_t* ld_y, float* partial, int32_t flags, void* stream);
 int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream);
 int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                      const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--panel", action="store_true", help="also time column-panel sources (lane plans)")
     ap.add_argument("--cap", type=int, default=0, help="also time norm_adj with item degrees capped at this (hub test)")
+    ap.add_argument("--graphs", default="norm_adj,ui_top1,ui_hub", help="graphs to time")
+    ap.add_argument("--nbs", default="1,2,4", help="64-column blocks per product")
     args = ap.parse_args()
     segs = [int(x) for x in args.segs.split(",")]
     cfg = Config("DiffMM", "baby", {"synthetic": "baby"})
@@ -40,12 +42,19 @@ def main():
     uit = torch.as_tensor(tl.uitems_np).to(dev)
     rng = np.random.default_rng(0)
     top1 = torch.as_tensor(rng.integers(0, I, U).astype(np.int32)).to(dev)
+    # a rebuilt graph after p_sample collapsed: 80 % of the users pick the same item (one hub row
+    # holding ~15.6k users, the shape seen in the DiffMM step)
+    t_hub = rng.integers(0, I, U).astype(np.int32)
+    t_hub[rng.random(U) < 0.8] = 0
+    top1_hub = torch.as_tensor(t_hub).to(dev)
     graphs = {}
     for seg in segs:
         graphs[("norm_adj", seg)] = K.bipartite_symnorm(U, I, uptr, uit, self_loops=False, deg_eps=1e-7, seg_nnz=seg)
         graphs[("ui_top1", seg)] = K.bipartite_symnorm(U, I, torch.arange(U + 1, dtype=torch.int32, device=dev), top1,
                                                        self_loops=True, deg_eps=0.0, seg_nnz=seg)
-    names = ["norm_adj", "ui_top1"]
+        graphs[("ui_hub", seg)] = K.bipartite_symnorm(U, I, torch.arange(U + 1, dtype=torch.int32, device=dev),
+                                                      top1_hub, self_loops=True, deg_eps=0.0, seg_nnz=seg)
+    names = [n for n in ("norm_adj", "ui_top1", "ui_hub") if n in args.graphs.split(",")]
     if args.cap:
         # hub test: the same users and items, each item keeping only its first `cap` users
         up, ui = tl.uptr_np, tl.uitems_np
@@ -80,7 +89,7 @@ def main():
     print(f"copy N x 256 fp32: {us:.1f} us, {2 * X.numel() * 4 / us / 1e3:.0f} GB/s")
     print(f"{'graph':10s} {'nnz':>7s} {'nb':>2s} {'seg':>4s} {'us':>8s} {'GB/s':>7s} {'frac':>6s} max|diff|")
     for name in names:
-        for nb in (1, 2, 4):
+        for nb in [int(x) for x in args.nbs.split(",")]:
             ref = None
             for seg in segs:
                 g = graphs[(name, seg)]

@@ -429,8 +429,107 @@ def gen_vbpr(ref, tmp):
     return out
 
 
+def gen_phases(ref, tmp):
+    """D16 / D18: the reference's diffusion-phase loop (common/trainer.py:491-527) and BPR loop
+    (:144-208) run on the tiny DiffMM of diffmm_tiny.npz with recorded draws / batches, for a
+    phase-level parity test through the optimiser steps (tests/test_phases_gpu.py)."""
+    import torch
+    import torch.optim as optim
+    diffmm = ref["diffmm"]
+    g = dict(np.load(os.path.join(OUT, "diffmm_tiny.npz"), allow_pickle=False))
+    U, I = int(g["U"]), int(g["I"])
+    rows, cols = g["train_rows"], g["train_cols"]
+    os.makedirs(os.path.join(tmp, "tiny"), exist_ok=True)
+    np.save(os.path.join(tmp, "tiny", "image_feat.npy"), g["v_feat"])
+    np.save(os.path.join(tmp, "tiny", "text_feat.npy"), g["t_feat"])
+    cfg = Cfg(USER_ID_FIELD="userID", ITEM_ID_FIELD="itemID", NEG_PREFIX="neg__", train_batch_size=40,
+              device=torch.device("cpu"), end2end=False, is_multimodal_model=True, data_path=tmp + "/",
+              dataset="tiny", vision_feature_file="image_feat.npy", text_feature_file="text_feat.npy",
+              embedding_size=64, n_layers=1, reg_weight=1e-6, ssl_reg=1e-2, temperature=0.1, keep_rate=1,
+              dims=[32], d_emb_size=10, norm=False, steps=5, noise_scale=0.1, noise_min=1e-4, noise_max=0.02,
+              sampling_noise=False, sampling_steps=0, rebuild_k=1, e_loss=0.5, ris_lambda=0.1,
+              ris_adj_lambda=0.2, trans_type=0, cl_method=0)
+    torch.manual_seed(999)
+    model = diffmm.DiffMM(cfg, MockLoader(U, I, rows, cols))
+    assert np.array_equal(model.uEmbeds.detach().numpy(), g["p_uEmbeds"])  # same model as diffmm_tiny
+    out = {}
+    for mod in ("image", "text"):
+        for n, p in getattr(model, "denoise_model_" + mod).named_parameters():
+            out[f"init_{mod}_" + n.replace(".", "_")] = p.detach().numpy().copy()
+    # ---- D16: diffusion phase over all users in batches of 40 (permutation recorded)
+    B = 40
+    rng = np.random.default_rng(21)
+    perm = rng.permutation(U)
+    out["dif_perm"] = perm
+    opt_i = optim.Adam(model.denoise_model_image.parameters(), lr=1e-3, weight_decay=0)
+    opt_t = optim.Adam(model.denoise_model_text.parameters(), lr=1e-3, weight_decay=0)
+    iE = model.getItemEmbeds().detach()
+    feats_i = model.getImageFeats().detach()
+    feats_t = model.getTextFeats().detach()
+    model.train()
+    dm = model.diffusion_model
+    losses = []
+    for b, lo in enumerate(range(0, U, B)):
+        users = perm[lo:lo + B]
+        x0 = np.zeros((len(users), I), np.float32)
+        for r, u in enumerate(users):
+            x0[r, cols[rows == u]] = 1.0
+        xt = torch.from_numpy(x0)
+        idx = torch.as_tensor(users).float()
+        opt_i.zero_grad()
+        opt_t.zero_grad()
+        torch.manual_seed(700 + b)
+        di, gi = dm.training_losses(model.denoise_model_image, xt, iE, idx, feats_i)
+        dt, gt = dm.training_losses(model.denoise_model_text, xt, iE, idx, feats_t)
+        li = di.mean() + gi.mean() * 0.5
+        lt = dt.mean() + gt.mean() * 0.5
+        (li + lt).backward()
+        opt_i.step()
+        opt_t.step()
+        losses.append((li.item(), lt.item()))
+        torch.manual_seed(700 + b)   # replay: randint, randn_like, dropout bernoulli for image, then text
+        for mod in ("image", "text"):
+            out[f"dif{b}_{mod}_t"] = torch.randint(0, 5, (len(users),)).long().numpy()
+            out[f"dif{b}_{mod}_noise"] = torch.randn_like(xt).numpy()
+            out[f"dif{b}_{mod}_keep"] = torch.empty_like(xt).bernoulli_(0.5).numpy()
+    out["dif_batches"] = np.int64(len(losses))
+    out["dif_losses"] = np.asarray(losses, np.float64)
+    for mod in ("image", "text"):
+        for n, p in getattr(model, "denoise_model_" + mod).named_parameters():
+            out[f"final_{mod}_" + n.replace(".", "_")] = p.detach().numpy().copy()
+    # ---- D18: BPR loop, three batches through Adam over model.parameters() (trainer.py:125-208)
+    tr = object.__new__(ref["trainer"].DiffMMTrainer)
+    tr.user_num, tr.item_num, tr.device = U, I, torch.device("cpu")
+    ones = np.ones(U)
+    model.image_UI_matrix = model.edgeDropper(tr.buildUIMatrix(np.arange(U), g["ui_img_items"], ones))
+    model.text_UI_matrix = model.edgeDropper(tr.buildUIMatrix(np.arange(U), g["ui_txt_items"], ones))
+    for name in ["uEmbeds", "iEmbeds", "image_trans", "text_trans", "modal_weight"]:
+        out["bpr_init_" + name] = getattr(model, name).detach().numpy().copy()
+    opt = optim.Adam(model.parameters(), lr=1e-3, weight_decay=0.0)
+    bl = []
+    for s_ in range(3):
+        inter = torch.as_tensor(np.stack([rng.integers(0, U, B), rng.integers(0, I, B), rng.integers(0, I, B)]))
+        out[f"bpr{s_}_inter"] = inter.numpy()
+        opt.zero_grad()
+        loss = model.calculate_loss(inter)
+        loss.backward()
+        opt.step()
+        bl.append(loss.item())
+    out["bpr_losses"] = np.asarray(bl, np.float64)
+    for name in ["uEmbeds", "iEmbeds", "image_trans", "text_trans", "modal_weight"]:
+        out["bpr_final_" + name] = getattr(model, name).detach().numpy().copy()
+    return out
+
+
 def main():
     ref = _import_reference()
+    if "--phases" in sys.argv:  # only the phase-level fixture (the others stay as committed)
+        with tempfile.TemporaryDirectory(dir=os.path.join(os.path.dirname(os.path.dirname(OUT)), ".golden_tmp")
+                                         if os.path.isdir(os.path.join(os.path.dirname(os.path.dirname(OUT)),
+                                                                       ".golden_tmp")) else None) as tmp:
+            np.savez_compressed(os.path.join(OUT, "diffmm_phases_tiny.npz"), **gen_phases(ref, tmp))
+        print("wrote", os.path.join(OUT, "diffmm_phases_tiny.npz"))
+        return
     import torch
     meta = {"torch": torch.__version__, "numpy": np.__version__, "reference": REF_SRC,
             "generator": "tests/golden/make_golden.py"}

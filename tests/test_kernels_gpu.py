@@ -456,3 +456,38 @@ def test_spmm_chunk_rows_spanning_groups(K, nb):
     want = 0.8 * (A @ X.astype(np.float64)) + 0.4 * Y0
     np.testing.assert_allclose(outs[0], want, rtol=1e-5, atol=1e-4)
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
+@pytest.mark.parametrize("seg", [LANE32, PACKED32])
+@pytest.mark.parametrize("nb", [1, 2, 4])
+def test_spmm_split_hub_rows(K, nb, seg):
+    """Lane plans cut hub rows longer than 1,024 entries into segments whose partials a fixup pass
+    adds in segment order (the rebuilt UI graph of a collapsed p_sample: one item row holding most
+    users).  Against fp64, bit-identical across repeats and between the launch entry points."""
+    rng = _rng(12)
+    U, I = 6000, 300
+    top = rng.integers(0, I, U)
+    top[rng.random(U) < 0.7] = 5                       # item 5: ~4.2k users
+    top[rng.random(U) < 0.1] = 17                      # item 17: a second, smaller hub
+    rp, col, val = graph_ref.ui_adj_csr(U, I, np.arange(U), top)
+    assert np.diff(rp).max() > 3 * 1024
+    N = U + I
+    g = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=seg)
+    assert g.flags & K.SPMM_HUB_FIXUP and g.plan_header[2] >> 1 >= 1
+    X = rng.standard_normal((N, 64 * nb)).astype(np.float32)
+    Y0 = rng.standard_normal((N, 64 * nb)).astype(np.float32)
+    Xd = _dev(X)
+    blocks = [(Xd[:, 64 * b:64 * (b + 1)],) for b in range(nb)]
+    outs = []
+    for _ in range(2):
+        Yd = _dev(Y0)
+        g.spmm(Yd, blocks, alpha=0.6, beta=0.5)
+        outs.append(Yd.cpu().numpy())
+    A = graph_ref.csr_to_dense(rp, col, val).astype(np.float64)
+    want = 0.6 * (A @ X.astype(np.float64)) + 0.5 * Y0
+    np.testing.assert_allclose(outs[0], want, rtol=1e-5, atol=1e-5)
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+    Ym = [_dev(Y0[:, 64 * b:64 * (b + 1)].copy()) for b in range(nb)]
+    K.spmm_multi(g, Ym, blocks, alpha=0.6, beta=0.5)
+    got = np.concatenate([y.cpu().numpy() for y in Ym], 1)
+    assert np.array_equal(got.view(np.uint32), outs[0].view(np.uint32))

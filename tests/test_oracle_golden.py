@@ -232,3 +232,63 @@ def test_adam_matches_torch():
     gs = [[rng.standard_normal((7, 5)).astype(np.float32)] for _ in range(3)]
     out = model_ref.adam_reference(ps, gs)
     assert out[0].shape == (7, 5)
+
+
+_DEN = {"emb_W": "emb_layer_weight", "emb_b": "emb_layer_bias", "W1": "in_layers_0_weight",
+        "b1": "in_layers_0_bias", "W2": "out_layers_0_weight", "b2": "out_layers_0_bias"}
+
+
+def test_diffusion_phase_oracle(golden):
+    """D16: the oracle's training_losses + torch Adam over the reference's recorded diffusion phase
+    (common/trainer.py:491-527, diffmm_phases_tiny.npz) reproduce its losses and final weights."""
+    g, ph = golden("diffmm_tiny"), golden("diffmm_phases_tiny")
+    U, I = int(g["U"]), int(g["I"])
+    tab = model_ref.diffmm_schedule()
+    p = _params(g)
+    feats = {"image": model_ref.modal_feats(_feats(g)["v"], p["image_trans"]).detach(),
+             "text": model_ref.modal_feats(_feats(g)["t"], p["text_trans"]).detach()}
+    iE = p["iEmbeds"].detach()
+    ws = {m: {k: torch.tensor(ph[f"init_{m}_{v}"], requires_grad=True) for k, v in _DEN.items()}
+          for m in ("image", "text")}
+    opts = {m: torch.optim.Adam(list(ws[m].values()), lr=1e-3, foreach=False) for m in ws}
+    rows, cols = g["train_rows"], g["train_cols"]
+    perm = ph["dif_perm"]
+    for b in range(int(ph["dif_batches"])):
+        users = perm[b * 40:(b + 1) * 40]
+        x0 = np.zeros((len(users), I), np.float32)
+        for r, u in enumerate(users):
+            x0[r, cols[rows == u]] = 1.0
+        total = 0.0
+        for m in ("image", "text"):
+            opts[m].zero_grad()
+            diff, gc = model_ref.diffmm_training_losses(
+                ws[m], tab, torch.as_tensor(x0), ph[f"dif{b}_{m}_t"], torch.as_tensor(ph[f"dif{b}_{m}_noise"]),
+                torch.as_tensor(ph[f"dif{b}_{m}_keep"]), iE, feats[m])
+            loss = diff.mean() + 0.5 * gc.mean()
+            np.testing.assert_allclose(loss.item(), ph["dif_losses"][b, 0 if m == "image" else 1], rtol=1e-5)
+            total = total + loss
+        total.backward()
+        for m in ("image", "text"):
+            opts[m].step()
+    for m in ("image", "text"):
+        for k, v in _DEN.items():
+            np.testing.assert_allclose(ws[m][k].detach().numpy(), ph[f"final_{m}_{v}"], rtol=1e-4, atol=1e-7)
+
+
+def test_bpr_phase_oracle(golden):
+    """D18: the oracle's rec_loss + torch Adam over the reference's three recorded BPR steps
+    (common/trainer.py:144-208) reproduce its losses and final rec parameters."""
+    g, ph = golden("diffmm_tiny"), golden("diffmm_phases_tiny")
+    (adj, iadj, tadj), _ = _graphs(g)
+    p = _params(g)
+    names = ["uEmbeds", "iEmbeds", "image_trans", "text_trans", "modal_weight"]
+    opt = torch.optim.Adam([p[n] for n in names], lr=1e-3, foreach=False)
+    for st in range(3):
+        inter = torch.as_tensor(ph[f"bpr{st}_inter"])
+        opt.zero_grad()
+        loss = model_ref.rec_loss(p, _feats(g), adj, iadj, tadj, inter[0], inter[1], inter[2])
+        loss.backward()
+        opt.step()
+        np.testing.assert_allclose(loss.item(), ph["bpr_losses"][st], rtol=1e-5)
+    for n in names:
+        np.testing.assert_allclose(p[n].detach().numpy(), ph["bpr_final_" + n], rtol=1e-4, atol=1e-7)
