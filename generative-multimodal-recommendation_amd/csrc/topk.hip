@@ -179,18 +179,21 @@ __global__ void __launch_bounds__(256) argmax_rows_kernel(int64_t n_rows, int64_
 
 // One thread per user.  ks = {5, 10, 20, 50} (any ascending list <= K, up to 8).
 // sums layout: [metric][k] with metric 0 recall, 1 ndcg, 2 precision, 3 map; per-block partials.
-__global__ void __launch_bounds__(256) metrics_kernel(int64_t n_users, const int* __restrict__ topk, int64_t ld_topk,
+// sel (optional): the eval-user rows to sum over (a user group of the test-time extras)
+__global__ void __launch_bounds__(256) metrics_kernel(int64_t n_users, const int* __restrict__ sel,
+                                                      const int* __restrict__ topk, int64_t ld_topk,
                                                       int K, const int64_t* __restrict__ pos_ptr,
                                                       const int* __restrict__ pos_items, int n_ks, const int* __restrict__ ks,
                                                       double* __restrict__ part) {
   __shared__ double red[4][8][4];
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t u = (i < n_users && sel) ? (int64_t)sel[i] : i;
   double m[4][8];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 8; ++b) m[a][b] = 0.0;
-  if (u < n_users) {
+  if (i < n_users) {
     const int64_t beg = pos_ptr[u], end = pos_ptr[u + 1];
     const int plen = (int)(end - beg);
     double cum = 0.0, dcg = 0.0, idcg = 0.0, sum_pre = 0.0;
@@ -235,6 +238,21 @@ __global__ void __launch_bounds__(256) metrics_kernel(int64_t n_users, const int
     const int a = threadIdx.x >> 3, b = threadIdx.x & 7;
     part[(int64_t)blockIdx.x * 32 + threadIdx.x] = (red[a][b][0] + red[a][b][1]) + (red[a][b][2] + red[a][b][3]);
   }
+}
+
+// per-item recommendation counts of the top-ks[j] columns (Coverage / Gini / Tail%, topk_evaluator.py:212-270);
+// integer atomics, so the counts are exact whatever the order
+__global__ void item_counts_kernel(int64_t n_users, const int* __restrict__ topk, int64_t ld_topk, int n_ks,
+                                   const int* __restrict__ ks, int64_t n_items, int* __restrict__ counts) {
+  const int kmax = ks[n_ks - 1];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_users * kmax) return;
+  const int64_t u = i / kmax;
+  const int r = (int)(i % kmax);
+  const int item = topk[u * ld_topk + r];
+  if (item < 0 || item >= n_items) return;
+  for (int j = 0; j < n_ks; ++j)
+    if (r < ks[j]) atomicAdd(&counts[(int64_t)j * n_items + item], 1);
 }
 
 __global__ void reduce_parts_kernel(int nparts, int width, const double* __restrict__ part, double* __restrict__ out) {
@@ -288,10 +306,37 @@ extern "C" int gmr_eval_metrics(int64_t n_users, const int32_t* topk, int64_t ld
   GMR_ARG(topk && pos_ptr && pos_items && ks && partials && out_sums && n_users > 0, "bad args");
   GMR_ARG(n_ks >= 1 && n_ks <= 8 && K <= 64, "n_ks must be 1..8");
   const int g = gmr::grid_for(n_users, 256);
-  hipLaunchKernelGGL(metrics_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, n_users, topk, ld_topk, K, pos_ptr,
+  hipLaunchKernelGGL(metrics_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, n_users, nullptr, topk, ld_topk, K,
+                     pos_ptr, pos_items, n_ks, ks, partials);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(reduce_parts_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, g, 32, partials, out_sums);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_eval_metrics_sel(int64_t n_sel, const int32_t* sel, const int32_t* topk, int64_t ld_topk, int32_t K,
+                                    const int64_t* pos_ptr, const int32_t* pos_items, int32_t n_ks, const int32_t* ks,
+                                    double* partials, double* out_sums, void* stream) {
+  GMR_ARG(sel && topk && pos_ptr && pos_items && ks && partials && out_sums && n_sel > 0, "bad args");
+  GMR_ARG(n_ks >= 1 && n_ks <= 8 && K <= 64, "n_ks must be 1..8");
+  const int g = gmr::grid_for(n_sel, 256);
+  hipLaunchKernelGGL(metrics_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, n_sel, sel, topk, ld_topk, K, pos_ptr,
                      pos_items, n_ks, ks, partials);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(reduce_parts_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, g, 32, partials, out_sums);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_topk_item_counts(int64_t n_users, const int32_t* topk, int64_t ld_topk, int32_t n_ks,
+                                    const int32_t* ks, int64_t n_items, int32_t* counts, void* stream) {
+  GMR_ARG(topk && ks && counts && n_users > 0 && n_items > 0 && n_ks >= 1 && n_ks <= 8, "bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)n_ks * (size_t)n_items, st);
+  if (e != hipSuccess) return gmr::hip_status(__func__, e);
+  // ks sorted ascending, the last one <= the top-k width (callers pass the evaluator's sorted topk list)
+  hipLaunchKernelGGL(item_counts_kernel, dim3(gmr::grid_for(n_users * 64, 256)), dim3(256), 0, st, n_users, topk, ld_topk,
+                     n_ks, ks, n_items, counts);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -87,6 +87,8 @@ SIGNATURES = {
     "gmr_topk_rows_f32": (I32, [I64, I64, P, I64, I32, P, I64, P, P]),
     "gmr_eval_metrics_partials": (I64, [I64]),
     "gmr_eval_metrics": (I32, [I64, P, I64, I32, P, P, I32, P, P, P, P]),
+    "gmr_eval_metrics_sel": (I32, [I64, P, P, I64, I32, P, P, I32, P, P, P, P]),
+    "gmr_topk_item_counts": (I32, [I64, P, I64, I32, P, I64, P, P]),
     "gmr_adam_f32": (I32, [I64, P, P, P, P, F32, F32, F32, F32, F32, F32, P]),
     "gmr_colsum_split_floats": (I64, [I64]),
     "gmr_colsum_split_f32": (I32, [I64, I64, P, I64, P, I32, P, I64, P]),

@@ -2,9 +2,13 @@
 
 Recall/NDCG/Precision/MAP@k for the full eval split are computed on the device
 (gmr_eval_metrics: per-user hit test against sorted positives + fp64 sums), then averaged and
-rounded to 4 decimals (topk_evaluator.py:114-120).  The test-only extras (popular/niche items,
-cold/warm users, Coverage/Gini/Tail%, topk_evaluator.py:122-270) and the top-K CSV dump
-(:93-106) are host-side bookkeeping on the K-column index matrix.
+rounded to 4 decimals (topk_evaluator.py:114-120).  The test-only extras (topk_evaluator.py:122-270)
+run on the device too: Pop/Niche are the same sums against each user's popular / niche positives
+over the users holding any (gmr_eval_metrics_sel), Cold/Warm the sums over the user groups, and
+Coverage/Gini/Tail% come from per-item recommendation counts (gmr_topk_item_counts); the host
+only turns those few numbers into the rounded dict.  The group tables (per-user popular and niche
+positives, cold/warm rows) are built once per eval split.  `evaluate` keeps the reference's host
+path (and its top-K CSV dump, :93-106) for callers holding batch lists.
 """
 import os
 from collections import Counter
@@ -108,11 +112,96 @@ class TopKEvaluator:
                 else:  # recall2 needs the global positive count
                     v = None
                 out[f"{m}@{k}"] = round(float(v), 4) if v is not None else None
-        if is_test or any(v is None for v in out.values()):
-            host = self.evaluate([topk_dev], eval_data, is_test=is_test, idx=idx)
+        if is_test:
+            out.update(self.extras_device(topk_dev, eval_data, n))
+            if self.save_recom_result:
+                self._dump(topk_dev[:n].cpu().numpy(), eval_data, idx)
+        if any(v is None for v in out.values()):  # recall2 (global positive count): host path
+            host = self.evaluate([topk_dev[:n]], eval_data, is_test=False, idx=idx)
             for k2, v in host.items():
-                if k2 not in out or out[k2] is None:
+                if out.get(k2) is None:
                     out[k2] = v
+        return out
+
+    # ------------------------------------------------------------------ test-time extras on the device
+    def _groups(self, eval_data, dev):
+        """Per eval split, once: sorted popular / niche positives per user and the user rows of the
+        Pop / Niche / Cold / Warm groups (topk_evaluator.py:122-200)."""
+        key = (id(eval_data), dev)
+        cache = getattr(self, "_grp", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        n = len(eval_data.eval_u_np)
+        lens = np.asarray(eval_data.get_eval_len_list(), np.int64)
+        items = np.concatenate([np.sort(x) for x in eval_data.get_eval_items()]) if n else np.zeros(0, np.int64)
+        rows = np.repeat(np.arange(n), lens)
+        g = {}
+        t = lambda a, dt=np.int32: torch.as_tensor(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+        if self.pop_items is not None:
+            pop = np.isin(items, np.fromiter(self.pop_items, np.int64, len(self.pop_items)))
+            for name, msk in (("Pop", pop), ("Niche", ~pop)):
+                cnt = np.bincount(rows[msk], minlength=n)
+                ptr = np.concatenate([[0], np.cumsum(cnt)])
+                sel = np.nonzero(cnt > 0)[0]
+                if len(sel):
+                    g[name] = (t(sel), t(ptr, np.int64), t(items[msk]), len(sel))
+        if self.warm_users is not None:
+            warm = np.isin(eval_data.eval_u_np, np.fromiter(self.warm_users, np.int64, len(self.warm_users)))
+            d = eval_data.to_device()
+            for name, msk in (("Cold", ~warm), ("Warm", warm)):
+                sel = np.nonzero(msk)[0]
+                if len(sel):
+                    g[name] = (t(sel), d["pos_ptr"], d["pos_items"], len(sel))
+        self._grp = (key, g)
+        return g
+
+    def extras_device(self, topk_dev, eval_data, n):
+        dev = topk_dev.device
+        ks = sorted(self.topk)
+        kt = torch.as_tensor(np.asarray(ks, np.int32)).to(dev)
+        out = {}
+        for name, (sel, ptr_, items_, m) in self._groups(eval_data, dev).items():
+            parts = torch.empty(int(_lib.load().gmr_eval_metrics_partials(m)), dtype=torch.float64, device=dev)
+            sums = torch.empty(32, dtype=torch.float64, device=dev)
+            _lib.call("gmr_eval_metrics_sel", m, K.ptr(sel), K.ptr(topk_dev), K._ld(topk_dev), topk_dev.shape[1],
+                      K.ptr(ptr_), K.ptr(items_), len(ks), K.ptr(kt), K.ptr(parts), K.ptr(sums), K.stream())
+            s = sums.cpu().numpy().reshape(4, 8) / m
+            for mname in self.metrics:
+                if mname in _DEVICE_METRICS:
+                    for k in self.topk:
+                        out[f"{name}_{_NAMES.get(mname, mname)}@{k}"] = round(float(s[_DEVICE_METRICS.index(mname),
+                                                                                       ks.index(k)]), 4)
+        item_num = eval_data.dataset.item_num
+        counts = torch.empty((len(ks), item_num), dtype=torch.int32, device=dev)
+        _lib.call("gmr_topk_item_counts", n, K.ptr(topk_dev), K._ld(topk_dev), len(ks), K.ptr(kt), item_num,
+                  K.ptr(counts), K.stream())
+        cnts = counts.cpu().numpy().astype(np.int64)
+        if self.pop_items is not None and self.pop_mask is None:
+            self.pop_mask = np.zeros(item_num, bool)
+            self.pop_mask[[i for i in self.pop_items if i < item_num]] = True
+        for j, k in enumerate(ks):
+            out.update(self._diversity(cnts[j], k, n, item_num))
+        return out
+
+    def _diversity(self, cnt, k, n_users, item_num):
+        """Coverage / Gini / Gini2 / Coverage2 / Tail% at k from the per-item counts (topk_evaluator.py:222-270)."""
+        out = {f"Coverage@{k}": round(np.count_nonzero(cnt) / item_num, 4)}
+        srt = np.sort(cnt)
+        tot = srt.sum()
+        if tot > 0:
+            nn = item_num
+            out[f"Gini@{k}"] = round(float((2 * np.sum(np.arange(1, nn + 1) * srt)) / (nn * tot) - (nn + 1) / nn), 4)
+        else:
+            out[f"Gini@{k}"] = 0.0
+        nz = cnt[cnt > 0]
+        if len(nz):
+            out[f"Gini2@{k}"] = round(float(cal_gini(nz)), 4)
+            out[f"Coverage2@{k}"] = round(len(nz) / item_num, 4)
+        else:
+            out[f"Gini2@{k}"] = 0.0
+            out[f"Coverage2@{k}"] = 0.0
+        if self.pop_mask is not None:
+            out[f"Tail%@{k}"] = round(float(cnt[~self.pop_mask].sum() / (n_users * k)), 4)
         return out
 
     # ------------------------------------------------------------------ reference-style host path

@@ -309,6 +309,16 @@ int64_t gmr_eval_metrics_partials(int64_t n_users);
 int gmr_eval_metrics(int64_t n_users, const int32_t* topk, int64_t ld_topk, int32_t K, const int64_t* pos_ptr,
                      const int32_t* pos_items, int32_t n_ks, const int32_t* ks, double* partials, double* out_sums,
                      void* stream);
+/* The same sums over the eval-user rows sel[0 .. n_sel) only, each scored against its own row of
+ * (pos_ptr, pos_items): the test-time group metrics (Pop/Niche positives, Cold/Warm users,
+ * topk_evaluator.py:122-200).  partials: gmr_eval_metrics_partials(n_sel) doubles. */
+int gmr_eval_metrics_sel(int64_t n_sel, const int32_t* sel, const int32_t* topk, int64_t ld_topk, int32_t K,
+                         const int64_t* pos_ptr, const int32_t* pos_items, int32_t n_ks, const int32_t* ks,
+                         double* partials, double* out_sums, void* stream);
+/* counts[j * n_items + i] = times item i appears in the first ks[j] columns of topk (ks ascending, <= 64, n_ks <= 8):
+ * Coverage / Gini / Tail% (topk_evaluator.py:212-270). */
+int gmr_topk_item_counts(int64_t n_users, const int32_t* topk, int64_t ld_topk, int32_t n_ks, const int32_t* ks,
+                         int64_t n_items, int32_t* counts, void* stream);
 
 /* ---------------------------------------------------------------- GenRecV1 rec step (models/genrecv1.py:225-427)
  * Tables are rows x 64 fp32.  BatchNorm1d(64) (eps, momentum as nn.BatchNorm1d): train mode uses

@@ -518,7 +518,48 @@ def gen_phases(ref, tmp):
     out["bpr_losses"] = np.asarray(bl, np.float64)
     for name in ["uEmbeds", "iEmbeds", "image_trans", "text_trans", "modal_weight"]:
         out["bpr_final_" + name] = getattr(model, name).detach().numpy().copy()
+    out.update(gen_csv(ref, tmp))
     return out
+
+
+def gen_csv(ref, tmp):
+    """The top-K CSV the reference writes on a test evaluation (utils/topk_evaluator.py:93-106) and the
+    test-time extras it returns next to it (pop / niche, cold / warm, coverage / gini / tail)."""
+    import glob
+    import torch
+    rng = np.random.default_rng(33)
+    n, k, I = 9, 50, 80
+    topk = np.stack([rng.permutation(I)[:k] for _ in range(n)])
+    users = np.array([5, 2, 11, 7, 3, 30, 1, 8, 4])
+    pos = [np.sort(rng.choice(I, size=int(rng.integers(1, 6)), replace=False)) for _ in range(n)]
+    d = os.path.join(tmp, "topk_csv")
+    cfg = Cfg(metrics=["Recall", "NDCG", "Precision", "MAP"], topk=[5, 10, 20, 50], save_recommended_topk=True,
+              recommend_topk=d, dataset="tiny", model="DiffMM", pop_items=set(range(0, I, 3)),
+              warm_users={5, 7, 30, 4})
+
+    class DS:
+        item_num = I
+
+    class ED:
+        dataset = DS()
+
+        def get_eval_items(self):
+            return pos
+
+        def get_eval_len_list(self):
+            return np.asarray([len(p) for p in pos])
+
+        def get_eval_users(self):
+            return torch.as_tensor(users)
+
+    res = ref["topk_evaluator"].TopKEvaluator(cfg).evaluate([torch.as_tensor(topk)], ED(), is_test=True, idx=0)
+    files = glob.glob(os.path.join(d, "*.csv"))
+    assert len(files) == 1
+    with open(files[0]) as f:
+        text = f.read()
+    return {"csv_topk": topk, "csv_users": users, "csv_pos_flat": np.concatenate(pos),
+            "csv_pos_len": np.asarray([len(p) for p in pos]), "csv_text": np.array(text),
+            "csv_name": np.array(os.path.basename(files[0])), "csv_extras_json": np.array(json.dumps(res))}
 
 
 def main():

@@ -154,7 +154,7 @@ def test_spmm_packed_bit_exact_vs_lane(K, nb):
     N = U + I
     lane = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=LANE32)
     packed = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=PACKED32)
-    assert packed.plan_header[2] == 1 and packed.plan_header[0] > 0  # packed, with hub rows
+    assert packed.plan_header[2] & 1 and packed.plan_header[0] > 0  # packed, with hub rows
     X = _dev(rng.standard_normal((N, 64 * nb)).astype(np.float32))
     Y0 = rng.standard_normal((N, 64 * nb)).astype(np.float32)
     outs = []
