@@ -426,9 +426,15 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
     // K ~ 1000 ones, 64^2 (with split-K) the skinny N = 64 / K = 64 products and the TN updates.
     // The 2048 x 512 x 512 transformer products (GenRecV1) run best on 64^2 tiles without split-K,
     // their K = 6710 input projection on 128^2, the K = 256 output projection on 256^2.
+    // Wide products with 256 <= K <= 1024 take 256^2 unless its last wave is much emptier than
+    // 128^2's (a 256^2 tile runs ~8% faster per flop; one 256^2 block or two 128^2 blocks per CU).
     const bool tnm = ta && !tb;
+    auto fill = [](int64_t tiles, int64_t slots) { return (double)tiles / (double)(((tiles + slots - 1) / slots) * slots); };
+    const bool wide256 = M >= 2048 && N >= 4096 && K >= 256 && K <= 1024 &&
+                         fill(((M + 255) / 256) * ((N + 255) / 256), 256) >=
+                             0.92 * fill(((M + 127) / 128) * ((N + 127) / 128), 512);
     if (!tnm && M >= 2048 && N >= 1000 && K >= 4096) tile = 256;
-    else if (!tnm && M >= 2048 && N >= 4096 && K >= 256 && K <= 512) tile = 256;
+    else if (!tnm && wide256) tile = 256;
     else if (!tnm && M * N >= (int64_t)8 << 20 && K >= 512) tile = 128;
     else if (!tnm && M * N >= (int64_t)1 << 20 && K >= 4096) tile = 128;
     else tile = 64;
@@ -442,8 +448,13 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
   p.tn = (N + p.bn - 1) / p.bn;
   int splits = split_k;
   if (splits <= 0) {  // auto: aim for >= 512 workgroups on 256 CUs
+    // skinny 64^2 products (one tile row or column: the N = 64 projections) split down to
+    // ~192-deep K slabs (measured: 384 x 64 x 7050 TN 34 -> 16 us at 32 slabs); the rest keep >= 512
+    const bool skinny = p.bm == 64 && (p.tm == 1 || p.tn == 1);
+    const int64_t min_k = skinny ? 192 : 512;
+    const int max_s = skinny ? 64 : 16;
     splits = 1;
-    while (p.tm * p.tn * splits < 512 && K / (splits * 2) >= 512 && splits < 16) splits *= 2;
+    while (p.tm * p.tn * splits < 512 && K / (splits * 2) >= min_k && splits < max_s) splits *= 2;
   }
   int64_t kps = (K + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;

@@ -23,6 +23,9 @@ SHAPES = [
     ("psample_out19k (NT)", 19445, 7050, 1000, 0, 1, 10),
     ("psample_h (NT)", 8192, 1000, 7050, 0, 1, 20),
     ("psample_out (NT)", 8192, 7050, 1000, 0, 1, 20),
+    # p_sample output layer with the in-place posterior epilogue (as models/diffmm.py p_sample runs it)
+    ("psample_post (NT,epi)", 8192, 7050, 1000, 0, 1, 20),
+    ("psample_post3061 (NT,epi)", 3061, 7050, 1000, 0, 1, 10),
     ("train_h (NT)", 2048, 1000, 7050, 0, 1, 20),
     ("train_out (NT)", 2048, 7050, 1000, 0, 1, 20),
     ("dh (NN)", 2048, 1000, 7050, 0, 0, 20),
@@ -30,6 +33,8 @@ SHAPES = [
     ("dW1 (TN)", 1000, 7050, 2048, 1, 0, 20),
     ("proj_v (NN,N=64)", 7050, 64, 4096, 0, 0, 60),
     ("proj_v_grad (TN,N=64)", 4096, 64, 7050, 1, 0, 60),
+    ("proj_t (NN,N=64)", 7050, 64, 384, 0, 0, 60),
+    ("proj_t_grad (TN,N=64)", 384, 64, 7050, 1, 0, 60),
     ("cl_logits_u (NT,K=64)", 2048, 19445, 64, 0, 1, 60),
     ("cl_dtab_u (TN,N=64)", 19445, 64, 2048, 1, 0, 60),
     ("cl_dp1_u (NN,N=64)", 2048, 64, 19445, 0, 0, 60),
@@ -59,17 +64,21 @@ def run(args):
         A = torch.randn((Kd, r4(M)) if ta else (M, r4(Kd)), device=dev)[:, :(M if ta else Kd)]
         B = torch.randn((N, r4(Kd)) if tb else (Kd, r4(N)), device=dev)[:, :(Kd if tb else N)]
         C = torch.empty((M, r4(N)), device=dev)[:, :N]
+        kw = {}
+        if "epi" in name:
+            bias = torch.randn(N, device=dev)
+            kw = dict(epi=K.EPI_POSTERIOR, bias=bias, aux=C, slope=0.9, beta=0.1)
         best = None
         for tile0 in args.tiles:
           for mf in args.mfma:
            tile = tile0 | (MF_FLAG[mf] if tile0 else 0)
            for split in args.splits:
             for _ in range(3):
-                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=split)
+                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=split, **kw)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(args.reps):
-                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=split)
+                K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=split, **kw)
             e.record()
             torch.cuda.synchronize()
             us = 1e3 * s.elapsed_time(e) / args.reps
