@@ -137,10 +137,12 @@ def summarize_probe(p, model="diffmm", shape=None):
                         "algorithmic_unit": "flop", "kernel": KERNEL_NAMES[tag]}
         else:
             # bytes = 8 nnz + 4 (n_rows+1) + 4 d n_cols (X once) + 4 d n_rows (Y once [+ read if beta])
+            # (a multi-job launch, key ("jobs", job, ...), moves the sum of its jobs' bytes)
             byts = 0.0
-            for nnz, nr, nc, nb, has_beta in (r[2] for r in recs):
-                d = 64 * nb
-                byts += 8.0 * nnz + 4.0 * (nr + 1) + 4.0 * d * nc + 4.0 * d * nr * (2 if has_beta else 1)
+            for key in (r[2] for r in recs):
+                for nnz, nr, nc, nb, has_beta in (key[1:] if key[0] == "jobs" else (key,)):
+                    d = 64 * nb
+                    byts += 8.0 * nnz + 4.0 * (nr + 1) + 4.0 * d * nc + 4.0 * d * nr * (2 if has_beta else 1)
             achieved = byts / (tot_ms * 1e-3) / 1e9
             out[tag] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "launches": len(recs),

@@ -243,11 +243,25 @@ __global__ void scatter_sorted_kernel(int n, int cols, const unsigned long long*
   const unsigned key = (unsigned)(e >> 32);
   if (key == 0xFFFFFFFFu) return;
   if (i > 0 && (unsigned)(plan[i - 1] >> 32) == key) return;
+  // the run is read 8 plan words at a time (independent loads: a popular item's run of dozens of
+  // slots is 1/8 the dependent round trips), then summed in slot order
   float4 s = f4(0, 0, 0, 0);
-  for (int64_t j = i; j < n; ++j) {
-    const unsigned long long ej = plan[j];
-    if ((unsigned)(ej >> 32) != key) break;
-    s = gmr::f4_add(s, ld4(contrib + (int64_t)(unsigned)(ej & 0xFFFFFFFFull) * ldc + c));
+  for (int64_t j0 = i; j0 < n; j0 += 8) {
+    unsigned long long ej[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ej[q] = j0 + q < n ? plan[j0 + q] : ~0ull;
+    float4 x[8];
+    int m = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const bool in = (unsigned)(ej[q] >> 32) == key && m == q;
+      m += in ? 1 : 0;
+      x[q] = in ? ld4(contrib + (int64_t)(unsigned)(ej[q] & 0xFFFFFFFFull) * ldc + c) : f4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < m) s = gmr::f4_add(s, x[q]);
+    if (m < 8) break;
   }
   float* o = dst + (int64_t)key * ldd + c;
   st4(o, gmr::f4_add(ld4(o), s));

@@ -183,6 +183,74 @@ __device__ __forceinline__ float4 frag16(const float* s, int row, int k0) {
   return make_float4(s[(k0 + 0) * LD + row], s[(k0 + 1) * LD + row], s[(k0 + 2) * LD + row], s[(k0 + 3) * LD + row]);
 }
 
+// epilogue: acc element e of lane -> row (e&3) + 8(e>>2) + 4h, col l32 (MF = 32) / row 4h + e (MF = 16)
+template <int BM, int BN, int WGM, int WGN, int MF, typename AccT>
+__device__ __forceinline__ void gemm_epilogue(const AccT (&acc)[BM / WGM / MF][BN / WGN / MF], int64_t M, int64_t N,
+                                              float* __restrict__ C, int64_t ldc, const Epi& epi, int64_t m0,
+                                              int64_t n0, float* __restrict__ ws) {
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / MF, TN = WTN / MF;
+  constexpr int NE = MF == 32 ? 16 : 4;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int wm = w / WGN, wn = w % WGN;
+  const int h = MF == 32 ? lane >> 5 : lane >> 4;
+  const int l32 = MF == 32 ? lane & 31 : lane & 15;
+  if (ws) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn * WTN + j * MF + l32;
+        if (n >= N) continue;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
+          if (m < M) ws[((int64_t)blockIdx.z * M + m) * N + n] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+  const bool rx = epi_reads_x(epi);
+  if (!rx && !epi.bias_row && !epi.rv1 && !epi.rv2) {
+    // no per-element inputs: one bias value per column at most
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn * WTN + j * MF + l32;
+        if (n >= N) continue;
+        const float b = epi.bias ? epi.bias[n] : 0.f;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
+          if (m < M) C[m * ldc + n] = epi_fin(epi, acc[i][j][e], b, 0.f, 0.f, 0.f);
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t n = n0 + wn * WTN + j * MF + l32;
+      if (n >= N) continue;
+      float bv[NE], xv[NE];
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {  // all loads of the 16 elements first (no store in between)
+        const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
+        const bool ok = m < M;
+        bv[e] = (epi.bias && ok) ? epi.bias[(epi.bias_row ? (int64_t)epi.bias_row[m] : 0) * epi.ld_bias + n] : 0.f;
+        xv[e] = (rx && ok) ? *epi_x_ptr(epi, C, ldc, m, n) : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
+        if (m < M) C[m * ldc + n] = epi_fin(epi, acc[i][j][e], bv[e], xv[e], epi_r1(epi, m), epi_r2(epi, m));
+      }
+    }
+}
+
 template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, bool VEC, int MF>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t N, int64_t K,
                                                              const float* __restrict__ A, int64_t lda,
@@ -285,60 +353,304 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t
     cur ^= 1;
   }
 
-  // epilogue: acc element e of lane -> row (e&3) + 8(e>>2) + 4h, col l32
-  if (ws) {
+  gemm_epilogue<BM, BN, WGM, WGN, MF>(acc, M, N, C, ldc, epi, m0, n0, ws);
+}
+
+// ---------------------------------------------------------------------------------------------
+// glds variant (MF = 32, 16-byte aligned operands): global -> LDS by global_load_lds_dwordx4, no
+// register staging and no ds_write pass before the barrier.  One glds wave-instruction writes
+// 1 KiB of LDS lane-linearly (base + 16 * lane), so the LDS images are unpadded:
+//   k-contiguous operand (KC): [R rows][32 k], the eight 16-byte k chunks of row r stored at
+//     chunk c ^ ((r >> 1) & 7) (the XOR goes on the glds SOURCE address and on the read), which
+//     keeps the 16-lane groups of a ds_read_b128 fragment read on distinct banks;
+//   m-contiguous operand (MC): [32 k][R rows], read with conflict-free ds_read_b32.
+// The full 32-deep k tiles go by glds; a partial last tile (K % 32) by zero-filled register loads
+// + ds_write into the same images.  Same MFMA order per output as gemm_kernel: bit-identical.
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ int kc_swz(int r) { return (r >> 1) & 7; }
+
+// One global_load_lds_dwordx4 (lane -> lds + 16 * lane), issued in inline asm: hipcc treats its own
+// glds as a pending LDS write and waits vmcnt(0) before the next ds_read of ANY buffer, which
+// would drain the prefetch of tile t+1 before tile t is computed.  hipcc does not count asm loads:
+// the kernel waits for them itself (glds_wait) before the barrier that publishes the buffer.
+// M0 (the LDS destination base) is saved and restored inside the statement.
+__device__ __forceinline__ void glds16(const float* src, float* lds) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void*)lds);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(dst)
+               : "memory");
+}
+__device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <int R, bool KC, int NW>
+__device__ __forceinline__ void glds_tile(const float* __restrict__ p, int64_t ld, int64_t r0, int64_t nrows,
+                                          int64_t k0, float* img, int w, int lane) {
+  constexpr int NI = R / 8;  // 1 KiB instructions per operand tile (32 x R floats)
+  static_assert(NI % NW == 0, "glds instructions must split evenly over the waves");
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < NI / NW; ++i) {
+    const int j = w + NW * i;
+    const float* src;
+    if (KC) {
+      const int r = 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ kc_swz(r);
+      const int64_t row = min(r0 + r, nrows - 1);  // rows past the edge: any valid row (discarded)
+      src = p + row * ld + k0 + 4 * c;
+    } else {
+      const int f = 256 * j + 4 * lane;
+      const int k = f / R, m = f % R;
+      const int64_t row = min(r0 + m, ((nrows - 1) >> 2) << 2);
+      src = p + (k0 + k) * ld + row;
+    }
+    glds16(src, img + 256 * j);
+  }
+}
+
+// partial last k tile: zero-filled register loads (issued before the compute) ...
+template <int R, bool KC, int NT>
+struct TailStage {
+  static constexpr int N4 = R * BK / 4 / NT;
+  float4 r[N4];
+  __device__ __forceinline__ void load(const float* __restrict__ p, int64_t ld, int64_t r0, int64_t nrows, int64_t k0,
+                                       int64_t kend) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int64_t n = n0 + wn * WTN + j * MF + l32;
-        if (n >= N) continue;
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-          const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
-          if (m < M) ws[((int64_t)blockIdx.z * M + m) * N + n] = acc[i][j][e];
+    for (int i = 0; i < N4; ++i) {
+      const int idx = threadIdx.x + NT * i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (KC) {
+        const int rr = idx >> 3, k = (int)k0 + (idx & 7) * 4;
+        const int64_t row = r0 + rr;
+        if (row < nrows) {
+          const float* q = p + row * ld + k;
+          if (k < kend) v.x = q[0];
+          if (k + 1 < kend) v.y = q[1];
+          if (k + 2 < kend) v.z = q[2];
+          if (k + 3 < kend) v.w = q[3];
+        }
+      } else {
+        const int kk = idx / (R / 4), m4 = (idx % (R / 4)) * 4;
+        const int64_t k = k0 + kk, row = r0 + m4;
+        if (k < kend) {
+          const float* q = p + k * ld + row;
+          if (row < nrows) v.x = q[0];
+          if (row + 1 < nrows) v.y = q[1];
+          if (row + 2 < nrows) v.z = q[2];
+          if (row + 3 < nrows) v.w = q[3];
         }
       }
-    return;
+      r[i] = v;
+    }
   }
+  // ... and ds_write into the glds image layout (after the compute of the current tile)
+  __device__ __forceinline__ void store(float* img) const {
+#pragma unroll
+    for (int i = 0; i < N4; ++i) {
+      const int idx = threadIdx.x + NT * i;
+      if (KC) {
+        const int rr = idx >> 3, c = idx & 7;
+        *reinterpret_cast<float4*>(img + rr * BK + 4 * (c ^ kc_swz(rr))) = r[i];
+      } else {
+        const int kk = idx / (R / 4), m4 = (idx % (R / 4)) * 4;
+        *reinterpret_cast<float4*>(img + kk * R + m4) = r[i];
+      }
+    }
+  }
+};
+
+// Epilogue through LDS (glds kernel): after the k loop the staging buffers are free, so the tile
+// goes to LDS in row blocks of HR rows (fragment element stores: 32 consecutive columns per half
+// wave, conflict-free) and comes back as float4 row chunks: the bias / aux / C traffic and the
+// output stores are 16-byte, coalesced, and no per-element arrays are held in registers (the
+// register epilogue of a 1,024-thread 256^2 tile spills).  Same per-element arithmetic (epi_fin).
+template <int BM, int BN, int WGM, int WGN>
+__device__ __forceinline__ void gemm_epilogue_lds(const floatx16 (&acc)[BM / WGM / 32][BN / WGN / 32], float* smem,
+                                                  int64_t M, int64_t N, float* __restrict__ C, int64_t ldc,
+                                                  const Epi& epi, int64_t m0, int64_t n0, float* __restrict__ ws) {
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int AVAIL = 2 * (BM + BN) * BK;                // floats of the two staging buffers
+  constexpr int HR0 = (AVAIL / BN) / 32 * 32;
+  constexpr int HR = HR0 < BM ? HR0 : BM;                   // rows per pass
+  constexpr int C4 = BN / 4;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int wm = w / WGN, wn = w % WGN;
+  const int h = lane >> 5, l32 = lane & 31;
   const bool rx = epi_reads_x(epi);
-  if (!rx && !epi.bias_row && !epi.rv1 && !epi.rv2) {
-    // no per-element inputs: one bias value per column at most
+  const bool pure = !rx && !epi.bias_row && !epi.rv1 && !epi.rv2;
+  // 16-byte paths: output (slab) rows, bias and x rows all 16-byte aligned
+  const float* xb = (epi.kind == GMR_EPI_NONE || epi.kind == GMR_EPI_BIAS) ? C : epi.aux;
+  const int64_t ldx = (epi.kind == GMR_EPI_NONE || epi.kind == GMR_EPI_BIAS) ? ldc : epi.ld_aux;
+  const bool v_out = ws ? (N % 4 == 0 && ((uintptr_t)ws & 15) == 0) : (ldc % 4 == 0 && ((uintptr_t)C & 15) == 0);
+  const bool v_in = (!epi.bias || (((uintptr_t)epi.bias & 15) == 0 && (!epi.bias_row || epi.ld_bias % 4 == 0))) &&
+                    (!rx || (((uintptr_t)xb & 15) == 0 && ldx % 4 == 0));
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+  for (int r0 = 0; r0 < BM; r0 += HR) {
+    __syncthreads();  // the buffers (first pass: the k loop's last reads; later: the previous pass) are free
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = wm * WTM + i * 32;
+      if (rb < r0 || rb >= r0 + HR) continue;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int64_t n = n0 + wn * WTN + j * MF + l32;
-        if (n >= N) continue;
-        const float b = epi.bias ? epi.bias[n] : 0.f;
+        const int col = wn * WTN + j * 32 + l32;
 #pragma unroll
-        for (int e = 0; e < NE; ++e) {
-          const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
-          if (m < M) C[m * ldc + n] = epi_fin(epi, acc[i][j][e], b, 0.f, 0.f, 0.f);
+        for (int e = 0; e < 16; ++e) smem[(rb - r0 + (e & 3) + 8 * (e >> 2) + 4 * h) * BN + col] = acc[i][j][e];
+      }
+    }
+    __syncthreads();
+    const int rows = BM - r0 < HR ? BM - r0 : HR;
+    for (int idx = threadIdx.x; idx < rows * C4; idx += NT) {
+      const int rr = idx / C4, c = (idx % C4) * 4;
+      const int64_t m = m0 + r0 + rr, n = n0 + c;
+      if (m >= M || n >= N) continue;
+      const float4 v = *reinterpret_cast<const float4*>(smem + rr * BN + c);
+      const float a4[4] = {v.x, v.y, v.z, v.w};
+      const bool full = n + 3 < N;
+      if (ws) {
+        float* o = ws + ((int64_t)blockIdx.z * M + m) * N + n;
+        if (full && v_out) {
+          *reinterpret_cast<float4*>(o) = v;
+        } else {
+          for (int q = 0; q < 4 && n + q < N; ++q) o[q] = a4[q];
+        }
+        continue;
+      }
+      float b4[4] = {0.f, 0.f, 0.f, 0.f}, x4[4] = {0.f, 0.f, 0.f, 0.f};
+      const float* bp = epi.bias ? epi.bias + (epi.bias_row ? (int64_t)epi.bias_row[m] * epi.ld_bias : 0) + n : nullptr;
+      const float* xp = rx ? xb + m * ldx + n : nullptr;
+      if (full && v_in) {
+        if (bp) {
+          const float4 t = *reinterpret_cast<const float4*>(bp);
+          b4[0] = t.x, b4[1] = t.y, b4[2] = t.z, b4[3] = t.w;
+        }
+        if (xp) {
+          const float4 t = *reinterpret_cast<const float4*>(xp);
+          x4[0] = t.x, x4[1] = t.y, x4[2] = t.z, x4[3] = t.w;
+        }
+      } else {
+        for (int q = 0; q < 4 && n + q < N; ++q) {
+          if (bp) b4[q] = bp[q];
+          if (xp) x4[q] = xp[q];
         }
       }
-    return;
+      const float r1 = pure ? 0.f : epi_r1(epi, m), r2 = pure ? 0.f : epi_r2(epi, m);
+      float o4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o4[q] = epi_fin(epi, a4[q], b4[q], x4[q], r1, r2);
+      float* o = C + m * ldc + n;
+      if (full && v_out) {
+        *reinterpret_cast<float4*>(o) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+      } else {
+        for (int q = 0; q < 4 && n + q < N; ++q) o[q] = o4[q];
+      }
+    }
   }
+}
+
+template <bool KC, int R>
+__device__ __forceinline__ float4 gfrag(const float* img, int row, int h, int q) {
+  if (KC) return *reinterpret_cast<const float4*>(img + row * BK + 4 * ((4 * h + q) ^ kc_swz(row)));
+  const int k = 16 * h + 4 * q;
+  return make_float4(img[k * R + row], img[(k + 1) * R + row], img[(k + 2) * R + row], img[(k + 3) * R + row]);
+}
+
+template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm_glds_kernel(int64_t M, int64_t N, int64_t K,
+                                                                  const float* __restrict__ A, int64_t lda,
+                                                                  const float* __restrict__ B, int64_t ldb,
+                                                                  float* __restrict__ C, int64_t ldc, Epi epi,
+                                                                  int tiles_n, int64_t k_per_split,
+                                                                  float* __restrict__ ws) {
+  constexpr int NW = WGM * WGN, NT = 64 * NW;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int AW = BM * BK, STAGE = (BM + BN) * BK;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int nwg = gridDim.x;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int64_t m0 = (int64_t)(tile / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(tile % tiles_n) * BN;
+  const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
+  const int64_t kend = min(K, kbeg + k_per_split);
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w / WGN, wn = w % WGN;
+  const int h = lane >> 5, l32 = lane & 31;
+
+  floatx16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int64_t n = n0 + wn * WTN + j * MF + l32;
-      if (n >= N) continue;
-      float bv[NE], xv[NE];
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < NE; ++e) {  // all loads of the 16 elements first (no store in between)
-        const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
-        const bool ok = m < M;
-        bv[e] = (epi.bias && ok) ? epi.bias[(epi.bias_row ? (int64_t)epi.bias_row[m] : 0) * epi.ld_bias + n] : 0.f;
-        xv[e] = (rx && ok) ? *epi_x_ptr(epi, C, ldc, m, n) : 0.f;
-      }
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const int64_t m = m0 + wm * WTM + i * MF + (MF == 32 ? (e & 3) + 8 * (e >> 2) + 4 * h : 4 * h + e);
-        if (m < M) C[m * ldc + n] = epi_fin(epi, acc[i][j][e], bv[e], xv[e], epi_r1(epi, m), epi_r2(epi, m));
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  TailStage<BM, AKC, NT> ta;
+  TailStage<BN, BKC, NT> tb;
+  if (kbeg < kend) {
+    if (kbeg + BK <= kend) {
+      glds_tile<BM, AKC, NW>(A, lda, m0, M, kbeg, smem, w, lane);
+      glds_tile<BN, BKC, NW>(B, ldb, n0, N, kbeg, smem + AW, w, lane);
+    } else {
+      ta.load(A, lda, m0, M, kbeg, kend);
+      tb.load(B, ldb, n0, N, kbeg, kend);
+      ta.store(smem);
+      tb.store(smem + AW);
+    }
+  }
+  glds_wait();
+  __syncthreads();
+  int cur = 0;
+  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+    const bool more = k0 + BK < kend;
+    const bool tail = more && k0 + 2 * BK > kend;  // the next tile is the partial last one
+    float* nxt = smem + (cur ^ 1) * STAGE;
+    if (more) {
+      if (!tail) {
+        glds_tile<BM, AKC, NW>(A, lda, m0, M, k0 + BK, nxt, w, lane);
+        glds_tile<BN, BKC, NW>(B, ldb, n0, N, k0 + BK, nxt + AW, w, lane);
+      } else {
+        ta.load(A, lda, m0, M, k0 + BK, kend);
+        tb.load(B, ldb, n0, N, k0 + BK, kend);
       }
     }
+    const float* a_s = smem + cur * STAGE;
+    const float* b_s = a_s + AW;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      float4 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = gfrag<AKC, BM>(a_s, wm * WTM + i * 32 + l32, h, qq);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = gfrag<BKC, BN>(b_s, wn * WTN + j * 32 + l32, h, qq);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].x, fb[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].y, fb[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].z, fb[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+    if (tail) {
+      ta.store(nxt);
+      tb.store(nxt + AW);
+    }
+    glds_wait();      // this wave's glds of the next tile have landed ...
+    __syncthreads();  // ... everyone's, and this tile's reads are done
+    cur ^= 1;
+  }
+  gemm_epilogue_lds<BM, BN, WGM, WGN>(acc, smem, M, N, C, ldc, epi, m0, n0, ws);
 }
 
 __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const float* __restrict__ ws,
@@ -362,10 +674,17 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const flo
 }
 
 template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int MF>
-void launch_t(bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
-              const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n, int64_t kps,
-              float* ws) {
+void launch_t(bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A,
+              int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n,
+              int64_t kps, float* ws) {
   const dim3 blk(64 * WGM * WGN);
+  if constexpr (MF == 32) {
+    if (vec && glds) {
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, AKC, BKC>), grid, blk, 0, st, M, N, K, A, lda, B, ldb, C,
+                         ldc, epi, tiles_n, kps, ws);
+      return;
+    }
+  }
   if (vec)
     hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, AKC, BKC, true, MF>), grid, blk, 0, st, M, N, K, A, lda, B, ldb,
                        C, ldc, epi, tiles_n, kps, ws);
@@ -375,35 +694,45 @@ void launch_t(bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t
 }
 
 template <int BM, int BN, int WGM, int WGN, int MF>
-void launch_mf(int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A,
-               int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n,
-               int64_t kps, float* ws) {
+void launch_mf(int ta, int tb, bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K,
+               const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi,
+               int tiles_n, int64_t kps, float* ws) {
   // AKC = A is k-contiguous (not transposed); BKC = B is k-contiguous (transposed)
   if (!ta && tb)
-    launch_t<BM, BN, WGM, WGN, true, true, MF>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+    launch_t<BM, BN, WGM, WGN, true, true, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
+                                               ws);
   else if (!ta && !tb)
-    launch_t<BM, BN, WGM, WGN, true, false, MF>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+    launch_t<BM, BN, WGM, WGN, true, false, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
+                                                ws);
   else if (ta && !tb)
-    launch_t<BM, BN, WGM, WGN, false, false, MF>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+    launch_t<BM, BN, WGM, WGN, false, false, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n,
+                                                 kps, ws);
   else
-    launch_t<BM, BN, WGM, WGN, false, true, MF>(vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+    launch_t<BM, BN, WGM, WGN, false, true, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
+                                                ws);
 }
 
 template <int BM, int BN, int WGM, int WGN>
-void launch_tile(int mf, int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K,
-                 const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi,
-                 int tiles_n, int64_t kps, float* ws) {
+void launch_tile(int mf, bool glds, int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N,
+                 int64_t K, const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                 const Epi& epi, int tiles_n, int64_t kps, float* ws) {
   if (mf == 16)
-    launch_mf<BM, BN, WGM, WGN, 16>(ta, tb, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+    launch_mf<BM, BN, WGM, WGN, 16>(ta, tb, vec, false, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
+                                    ws);
   else
-    launch_mf<BM, BN, WGM, WGN, 32>(ta, tb, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+    launch_mf<BM, BN, WGM, WGN, 32>(ta, tb, vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
+                                    ws);
 }
 
 // Tile, MFMA shape and split-K choice of gmr_gemm_f32 (tile / split_k = 0: automatic).
 // tile | GMR_GEMM_MFMA16 / GMR_GEMM_MFMA32 forces the MFMA shape; otherwise the environment variable
 // GMR_GEMM_MFMA (16 or 32, read once) or the built-in default.
+// Staging: global_load_lds (gemm_glds_kernel) unless tile | GMR_GEMM_REGSTAGE, or the environment
+// variable GMR_GEMM_GLDS = 0 (read once), asks for register staging (gemm_kernel); MFMA16 plans and
+// operands that are not 16-byte aligned always take register staging.
 struct Plan {
   int tile, bm, bn, splits, mf;
+  bool glds;
   int64_t tm, tn, kps;
 };
 
@@ -415,11 +744,22 @@ int default_mfma() {
   return mf;
 }
 
+bool default_glds() {
+  static bool g = [] {
+    const char* e = getenv("GMR_GEMM_GLDS");
+    return !(e && atoi(e) == 0);
+  }();
+  return g;
+}
+
 Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int split_k) {
   int mf = default_mfma();
   if (tile & GMR_GEMM_MFMA16) mf = 16;
   if (tile & GMR_GEMM_MFMA32) mf = 32;
-  tile &= ~(GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32);
+  bool glds = default_glds();
+  if (tile & GMR_GEMM_GLDS) glds = true;
+  if (tile & GMR_GEMM_REGSTAGE) glds = false;
+  tile &= ~(GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32 | GMR_GEMM_GLDS | GMR_GEMM_REGSTAGE);
   if (tile == 0) {
     // measured on MI355X (scripts/gemm_bench.py): 256^2 tiles win the long-K products of the
     // denoiser (M >= 2048, N >= 1000, K >= 4096; one 16-wave block per CU), 128^2 the wide
@@ -433,7 +773,8 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
     const bool wide256 = M >= 2048 && N >= 4096 && K >= 256 && K <= 1024 &&
                          fill(((M + 255) / 256) * ((N + 255) / 256), 256) >=
                              0.92 * fill(((M + 127) / 128) * ((N + 127) / 128), 512);
-    if (!tnm && M >= 2048 && N >= 1000 && K >= 4096) tile = 256;
+    // (with glds staging the NN form of the long-K hidden products, dh = G W1, is faster on 128^2)
+    if (!tnm && M >= 2048 && N >= 1000 && K >= 4096) tile = (tb || !glds) ? 256 : 128;
     else if (!tnm && wide256) tile = 256;
     else if (!tnm && M * N >= (int64_t)8 << 20 && K >= 512) tile = 128;
     else if (!tnm && M * N >= (int64_t)1 << 20 && K >= 4096) tile = 128;
@@ -441,6 +782,7 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
   }
   Plan p;
   p.mf = mf;
+  p.glds = glds && mf == 32;
   p.tile = tile;
   p.bm = tile == 256128 ? 256 : tile == 128256 ? 128 : tile;
   p.bn = tile == 256128 ? 128 : tile == 128256 ? 256 : tile;
@@ -487,7 +829,7 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
           "epilogue needs aux");
   GMR_ARG(epilogue != GMR_EPI_ROWSCALE_AUX || rowvec1, "epilogue needs rowvec1");
   {
-    const int t = tile & ~(GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32);
+    const int t = tile & ~(GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32 | GMR_GEMM_GLDS | GMR_GEMM_REGSTAGE);
     GMR_ARG(t == 0 || t == 64 || t == 128 || t == 256 || t == 256128 || t == 128256,
             "tile must be 0 (auto), 64, 128, 256, 256128 or 128256 (| GMR_GEMM_MFMA16 / GMR_GEMM_MFMA32)");
   }
@@ -519,19 +861,19 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   dim3 grid((unsigned)(tm * tn), 1, (unsigned)splits);
   switch (tile) {
     case 256:
-      launch_tile<256, 256, 4, 4>(pl.mf, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<256, 256, 4, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
       break;
     case 256128:
-      launch_tile<256, 128, 4, 2>(pl.mf, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<256, 128, 4, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
       break;
     case 128256:
-      launch_tile<128, 256, 2, 4>(pl.mf, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<128, 256, 2, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
       break;
     case 128:
-      launch_tile<128, 128, 2, 2>(pl.mf, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<128, 128, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
       break;
     default:
-      launch_tile<64, 64, 2, 2>(pl.mf, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<64, 64, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
   }
   GMR_LAUNCHED();
   if (ws) {

@@ -540,13 +540,13 @@ __global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__
 }
 
 // hub-segment fixup: y[row] = alpha * sum_j partial[slot0 + j] + beta * y[row], j in order
-__global__ void __launch_bounds__(256) lane_fix_kernel(const int* __restrict__ plan, int64_t n_rows, int64_t nnz,
-                                                       int ncols, const float* __restrict__ part, float alpha,
-                                                       float beta, Dst dst) {
+__device__ __forceinline__ void lane_fix_body(const int* __restrict__ plan, int64_t n_rows, int64_t nnz, int ncols,
+                                              const float* __restrict__ part, float alpha, float beta, const Dst& dst,
+                                              int i0, int step) {
   const int n_fix = plan[2] >> 1;
   const int4* fix = reinterpret_cast<const int4*>(plan + lane_fix_off(n_rows, nnz));
   const int c4n = ncols / 4;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_fix * c4n; i += gridDim.x * blockDim.x) {
+  for (int i = i0; i < n_fix * c4n; i += step) {
     const int f = i / c4n, c = (i % c4n) * 4;
     const int4 fx = fix[f];
     float4 s = *reinterpret_cast<const float4*>(part + (int64_t)fx.y * 256 + c);
@@ -556,6 +556,12 @@ __global__ void __launch_bounds__(256) lane_fix_kernel(const int* __restrict__ p
     if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
     *reinterpret_cast<float4*>(yp) = o;
   }
+}
+__global__ void __launch_bounds__(256) lane_fix_kernel(const int* __restrict__ plan, int64_t n_rows, int64_t nnz,
+                                                       int ncols, const float* __restrict__ part, float alpha,
+                                                       float beta, Dst dst) {
+  lane_fix_body(plan, n_rows, nnz, ncols, part, alpha, beta, dst, blockIdx.x * blockDim.x + threadIdx.x,
+                gridDim.x * blockDim.x);
 }
 
 // Packed lane plan (GMR_SPMM_LANE_PLAN | GMR_SPMM_PACKED | 32).  The short rows' col/val are
@@ -586,17 +592,18 @@ __global__ void __launch_bounds__(256) lane_pack_kernel(const int* __restrict__ 
   }
 }
 
+// One lane-plan product for workgroup `bid` of its launch (bid & 7 = the XCD: launches and the
+// job ranges of a multi-job launch are multiples of 8 workgroups).
 template <int LPR, bool PACKED, int EB>
-__global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __restrict__ col,
-                                                                  const float* __restrict__ val,
-                                                                  const int* __restrict__ plan, int S, int wpx, Src src,
-                                                                  float alpha, float beta, Dst dst, int n_rows,
-                                                                  int64_t nnz, float* __restrict__ hub_part) {
+__device__ __forceinline__ void lane_body(const int* __restrict__ col, const float* __restrict__ val,
+                                          const int* __restrict__ plan, int S, int wpx, const Src& src, float alpha,
+                                          float beta, const Dst& dst, int n_rows, int64_t nnz,
+                                          float* __restrict__ hub_part, int bid, int nt) {
   constexpr int NW = kLaneThreads / 64;  // waves per workgroup
   constexpr int NG = 64 / LPR;           // lane groups per wave
   constexpr int EPL = EB / LPR;          // col/val words per lane per batch
   __shared__ float4 s_red[NW][LPR];
-  const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+  const int xcd = bid & 7, k = bid >> 3;
   const int slice = xcd % S, part = xcd / S, P = 8 / S;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int grp = lane / LPR, sub = lane % LPR, gbase = grp * LPR;
@@ -613,6 +620,10 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
   float* yc = dst.y[blk] + (c0 & 63) + sub * 4;
   const int64_t ldy = dst.ld[blk];
 
+  // nt & 2: the streamed-once index words (col/val, packed entries) are read non-temporally, so they
+  // do not evict the X slice from L2; nt & 1: Y is stored non-temporally for the same reason
+  auto ldi = [&](const int* p) -> int { return (nt & 2) ? __builtin_nontemporal_load(p) : *p; };
+  auto ldf = [&](const float* p) -> float { return (nt & 2) ? __builtin_nontemporal_load(p) : *p; };
   // sum over the batches at e0, e0 + step, ... below end (e0, end and step are uniform in the group)
   auto walk = [&](int e0, int end, int step) -> float4 {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -621,8 +632,8 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
       const int i = e0 + q * LPR + sub;
-      cc[q] = i < end ? col[i] : 0;
-      vv[q] = i < end ? val[i] : 0.f;
+      cc[q] = i < end ? ldi(col + i) : 0;
+      vv[q] = i < end ? ldf(val + i) : 0.f;
     }
     for (int e = e0; e < end; e += step) {
       float4 xs[EB];
@@ -639,8 +650,8 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
 #pragma unroll
       for (int q = 0; q < EPL; ++q) {  // the next batch's indices travel while the gathers land
         const int i = en + q * LPR + sub;
-        cc[q] = i < end ? col[i] : 0;
-        vv[q] = i < end ? val[i] : 0.f;
+        cc[q] = i < end ? ldi(col + i) : 0;
+        vv[q] = i < end ? ldf(val + i) : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < EB; ++u) acc = gmr::f4_fma(vs[u], xs[u], acc);
@@ -651,7 +662,13 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
     float* yp = yc + (int64_t)row * ldy;
     float4 o = gmr::f4_scale(alpha, acc);
     if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
-    *reinterpret_cast<float4*>(yp) = o;
+    if (nt & 1) {
+      typedef float v4 __attribute__((ext_vector_type(4)));
+      v4 ov = {o.x, o.y, o.z, o.w};
+      __builtin_nontemporal_store(ov, reinterpret_cast<v4*>(yp));
+    } else {
+      *reinterpret_cast<float4*>(yp) = o;
+    }
   };
 
   const int wg = part * wpx + k, n_wg = P * wpx;
@@ -704,8 +721,8 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
 #pragma unroll
         for (int q = 0; q < EM; ++q) {
           const int i = q * LPR + sub;
-          cc[q] = i < deg ? pcol[e0 + i] : 0;
-          vv[q] = i < deg ? pval[e0 + i] : 0.f;
+          cc[q] = i < deg ? ldi(pcol + e0 + i) : 0;
+          vv[q] = i < deg ? ldf(pval + e0 + i) : 0.f;
         }
       } else {
 #pragma unroll
@@ -772,6 +789,62 @@ __global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __re
     if (d.x >= 0) store(d.x, acc);
     d = dn;
   }
+}
+
+template <int LPR, bool PACKED, int EB>
+__global__ void __launch_bounds__(kLaneThreads) spmm_lane_kernel(const int* __restrict__ col,
+                                                                  const float* __restrict__ val,
+                                                                  const int* __restrict__ plan, int S, int wpx, Src src,
+                                                                  float alpha, float beta, Dst dst, int n_rows,
+                                                                  int64_t nnz, float* __restrict__ hub_part, int nt) {
+  lane_body<LPR, PACKED, EB>(col, val, plan, S, wpx, src, alpha, beta, dst, n_rows, nnz, hub_part, blockIdx.x, nt);
+}
+
+// Multi-job lane launch (gmr_spmm_jobs_f32): independent products, possibly of different
+// matrices, in one grid; job q owns workgroups [off[q], off[q+1]) (multiples of 8, so each keeps
+// its XCD-slice mapping) and runs exactly the single-job body.
+constexpr int kMaxJobs = 4;
+struct LaneJob {
+  const int* col;
+  const float* val;
+  const int* plan;
+  float* part;
+  Src src;
+  Dst dst;
+  int64_t nnz;
+  float alpha, beta;
+  int S, wpx, n_rows, packed, fix, ncols, nt;
+};
+struct LaneJobs {
+  LaneJob j[kMaxJobs];
+  int off[kMaxJobs + 1];
+  int n;
+};
+
+// hub-segment fixups of every job whose plan split hub rows (jobs write disjoint outputs)
+__global__ void __launch_bounds__(256) lane_fix_jobs_kernel(LaneJobs J) {
+  for (int q = 0; q < J.n; ++q) {
+    const LaneJob& jb = J.j[q];
+    if (jb.fix)
+      lane_fix_body(jb.plan, jb.n_rows, jb.nnz, jb.ncols, jb.part, jb.alpha, jb.beta, jb.dst,
+                    blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
+  }
+}
+
+template <int LPR, int EB>
+__global__ void __launch_bounds__(kLaneThreads) spmm_lane_jobs_kernel(LaneJobs J) {
+  const int b = blockIdx.x;
+  int q = 0;
+#pragma unroll
+  for (int t = 1; t < kMaxJobs; ++t) q += (t < J.n && b >= J.off[t]) ? 1 : 0;
+  const LaneJob& jb = J.j[q];
+  const int bid = b - J.off[q];
+  if (jb.packed)
+    lane_body<LPR, true, EB>(jb.col, jb.val, jb.plan, jb.S, jb.wpx, jb.src, jb.alpha, jb.beta, jb.dst, jb.n_rows,
+                             jb.nnz, jb.part, bid, jb.nt);
+  else
+    lane_body<LPR, false, EB>(jb.col, jb.val, jb.plan, jb.S, jb.wpx, jb.src, jb.alpha, jb.beta, jb.dst, jb.n_rows,
+                              jb.nnz, jb.part, bid, jb.nt);
 }
 
 
@@ -1124,6 +1197,18 @@ static int lane_lpr(int n_blocks) {  // GMR_SPMM_LPR = 4 / 8 overrides (tuning);
   return n_blocks == 4 ? 8 : ov ? ov : 4;
 }
 
+// GMR_SPMM_NT: 1 = non-temporal Y stores (default: the output rows stream past L2 instead of
+// evicting the XCD's X slice; -5..-16 % on the baby graphs, profiles/r02i_spmm_nt.txt),
+// 2 = non-temporal index loads as well (no gain measured), 0 = plain stores
+static int lane_nt() {
+  static const int nt = [] {
+    const char* s = getenv("GMR_SPMM_NT");
+    const int v = s ? atoi(s) : 1;
+    return v >= 0 && v <= 3 ? v : 1;
+  }();
+  return nt;
+}
+
 static int lane_eb() {  // GMR_SPMM_EB = 16: 16 gathers in flight per lane group and batch (tuning)
   static const int eb = [] {
     const char* s = getenv("GMR_SPMM_EB");
@@ -1287,21 +1372,27 @@ static int chunk_launch(const int32_t* col, const float* val, int64_t n_rows, in
   return GMR_OK;
 }
 
+// column slices S and workgroups per XCD of a lane-plan product
+static void lane_grid(int64_t n_rows, int32_t n_blocks, int lpr, bool packed, int& S, int& wpx) {
+  S = 16 * n_blocks / lpr;  // column slices: 4 (d = 64), 8 (d = 128, 256)
+  const int64_t waves = (n_rows + 64 / lpr - 1) / (64 / lpr) / (8 / S) + 1;  // one pass over the rows
+  const int cap = packed ? lane_wpx_cap_packed() : lane_wpx_cap();
+  wpx = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, cap));
+}
+
 static int lane_launch(const int32_t* col, const float* val, int64_t n_rows, int64_t nnz, const int32_t* plan,
                        int32_t seg_nnz, int32_t n_blocks, const Src& s, float alpha, float beta, const Dst& d,
                        float* partial, int32_t flags, hipStream_t st0) {
   if (is_chunk(seg_nnz)) return chunk_launch(col, val, n_rows, nnz, plan, n_blocks, s, alpha, beta, d, st0);
   // lanes per row: a slice is 4 * lpr columns (column panels are 16 wide below d = 256)
   const int lpr = s.panel_rows > 0 ? (n_blocks == 4 ? 8 : 4) : lane_lpr(n_blocks);
-  const int S = 16 * n_blocks / lpr;      // column slices: 4 (d = 64), 8 (d = 128, 256)
-  const int64_t waves = (n_rows + 64 / lpr - 1) / (64 / lpr) / (8 / S) + 1;  // one pass over the rows
   const bool packed = lane_packed(seg_nnz);
-  const int cap = packed ? lane_wpx_cap_packed() : lane_wpx_cap();
-  const int wpx = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, cap));
+  int S, wpx;
+  lane_grid(n_rows, n_blocks, lpr, packed, S, wpx);
   const dim3 grid((unsigned)(8 * wpx));
 #define GMR_LANE_LAUNCH(LPRV, PK, EBV)                                                                      \
   hipLaunchKernelGGL((spmm_lane_kernel<LPRV, PK, EBV>), grid, dim3(kLaneThreads), 0, st0, col, val, plan, S, wpx, \
-                   s, alpha, beta, d, (int)n_rows, nnz, partial)
+                   s, alpha, beta, d, (int)n_rows, nnz, partial, lane_nt())
   const bool wide = lane_eb() == 16;  // entries gathered per lane group and batch
   if (lpr == 8) {
     if (packed) { if (wide) GMR_LANE_LAUNCH(8, true, 16); else GMR_LANE_LAUNCH(8, true, 8); }
@@ -1351,6 +1442,75 @@ extern "C" int gmr_spmm_multi_f32(const int32_t* col, const float* val, int64_t 
   }
   return lane_launch(col, val, n_rows, nnz, plan, seg_nnz, n_blocks, s, alpha, beta, d, partial, flags,
                      (hipStream_t)stream);
+}
+
+extern "C" int gmr_spmm_jobs_f32(int32_t n_jobs, const gmr_spmm_job* jobs, void* stream) {
+  GMR_ARG(jobs && n_jobs >= 1 && n_jobs <= kMaxJobs, "1 to 4 jobs");
+  LaneJobs J;
+  int lpr = 0, off = 0;
+  bool any_fix = false;
+  for (int q = 0; q < n_jobs; ++q) {
+    const gmr_spmm_job& g = jobs[q];
+    GMR_ARG(g.plan && (g.nnz == 0 || (g.col && g.val)), "job: null pointer");
+    GMR_ARG(lane_l(g.seg_nnz), "job: jobs take lane plans (GMR_SPMM_LANE_PLAN [| GMR_SPMM_PACKED] | L)");
+    GMR_ARG(g.n_blocks == 1 || g.n_blocks == 2 || g.n_blocks == 4, "job: n_blocks must be 1, 2 or 4");
+    GMR_ARG(g.n_rows > 0 && g.n_rows < (1ll << 31) && g.nnz >= 0 && ((uintptr_t)g.plan & 15) == 0, "job: bad shape");
+    const int l = lane_lpr(g.n_blocks);
+    GMR_ARG(lpr == 0 || l == lpr, "jobs of one launch need one lane width (n_blocks 1 and 2 together, 4 alone)");
+    lpr = l;
+    LaneJob& j = J.j[q];
+    j.col = g.col;
+    j.val = g.val;
+    j.plan = g.plan;
+    j.part = g.partial;
+    j.nnz = g.nnz;
+    j.alpha = g.alpha;
+    j.beta = g.beta;
+    j.n_rows = (int)g.n_rows;
+    j.packed = lane_packed(g.seg_nnz) ? 1 : 0;
+    j.fix = (g.flags & GMR_SPMM_HUB_FIXUP) ? 1 : 0;
+    j.ncols = 64 * g.n_blocks;
+    j.nt = lane_nt();
+    GMR_ARG(!j.fix || g.partial, "job: plan has split hub rows (GMR_SPMM_HUB_FIXUP): partial buffer needed");
+    any_fix = any_fix || j.fix;
+    j.src.split = g.split;
+    j.src.panel_rows = 0;
+    for (int b = 0; b < 4; ++b) {
+      const int bb = b < g.n_blocks ? b : 0;
+      j.src.lo[b] = g.x_lo[bb];
+      j.src.ld_lo[b] = g.ld_lo[bb];
+      const bool two = g.split < g.n_rows && g.x_hi[bb];
+      j.src.hi[b] = two ? g.x_hi[bb] : g.x_lo[bb];
+      j.src.ld_hi[b] = two ? g.ld_hi[bb] : g.ld_lo[bb];
+      j.dst.y[b] = g.y[bb];
+      j.dst.ld[b] = g.ld_y[bb];
+      GMR_ARG(j.src.lo[b] && j.src.hi[b] && j.dst.y[b], "job: null block");
+      GMR_ARG((((uintptr_t)j.src.lo[b] | (uintptr_t)j.src.hi[b] | (uintptr_t)j.dst.y[b]) & 15) == 0,
+              "job: blocks must be 16-byte aligned");
+      GMR_ARG(j.src.ld_lo[b] % 4 == 0 && j.src.ld_hi[b] % 4 == 0 && j.dst.ld[b] % 4 == 0 && j.dst.ld[b] >= 64,
+              "job: bad block stride");
+    }
+    lane_grid(g.n_rows, g.n_blocks, lpr, j.packed, j.S, j.wpx);
+    J.off[q] = off;
+    off += 8 * j.wpx;
+  }
+  for (int q = n_jobs; q <= kMaxJobs; ++q) J.off[q] = off;
+  J.n = n_jobs;
+  hipStream_t st = (hipStream_t)stream;
+  const bool wide = lane_eb() == 16;
+  if (lpr == 8) {
+    if (wide) hipLaunchKernelGGL((spmm_lane_jobs_kernel<8, 16>), dim3(off), dim3(kLaneThreads), 0, st, J);
+    else hipLaunchKernelGGL((spmm_lane_jobs_kernel<8, 8>), dim3(off), dim3(kLaneThreads), 0, st, J);
+  } else {
+    if (wide) hipLaunchKernelGGL((spmm_lane_jobs_kernel<4, 16>), dim3(off), dim3(kLaneThreads), 0, st, J);
+    else hipLaunchKernelGGL((spmm_lane_jobs_kernel<4, 8>), dim3(off), dim3(kLaneThreads), 0, st, J);
+  }
+  GMR_LAUNCHED();
+  if (any_fix) {
+    hipLaunchKernelGGL(lane_fix_jobs_kernel, dim3(32), dim3(256), 0, st, J);
+    GMR_LAUNCHED();
+  }
+  return GMR_OK;
 }
 
 extern "C" int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,

@@ -17,6 +17,16 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 CP = ctypes.c_char_p
 
+
+
+class SpmmJob(ctypes.Structure):
+    """gmr_spmm_job (include/gmr.h)."""
+    _fields_ = [("col", P), ("val", P), ("plan", P), ("partial", P), ("n_rows", I64), ("nnz", I64),
+                ("seg_nnz", I32), ("n_blocks", I32), ("flags", I32), ("reserved", I32),
+                ("x_lo", P * 4), ("ld_lo", I64 * 4), ("x_hi", P * 4), ("ld_hi", I64 * 4), ("split", I64),
+                ("alpha", F32), ("beta", F32), ("y", P * 4), ("ld_y", I64 * 4)]
+
+
 # name: (restype, argtypes) — must match include/gmr.h
 SIGNATURES = {
     "gmr_last_error_string": (CP, []),
@@ -34,6 +44,7 @@ SIGNATURES = {
     "gmr_stream_fork": (I32, [P, P, P]),
     "gmr_score_f16": (I32, [I64, I64, I64, P, I64, P, I64, P, I64, P]),
     "gmr_spmm_multi_f32": (I32, [P, P, I64, I64, P, I32, I32, P, P, P, P, I64, F32, F32, P, P, P, I32, P]),
+    "gmr_spmm_jobs_f32": (I32, [I32, P, P]),
     "gmr_spmm_panel_f32": (I32, [P, P, I64, I64, P, I32, I32, P, I64, F32, F32, P, I64, P, I32, P]),
     "gmr_spmm_csr_f32": (I32, [P, P, P, I64, I64, P, I32, P, I32, P, P, P, P, I64, F32, F32, P, I64, I32, P]),
     "gmr_bipartite_nnz": (I64, [I64, I64, I64, I32]),

@@ -11,6 +11,8 @@ The BPR/contrastive step (calculate_loss, diffmm.py:203-258) runs as one fused f
 a hand-derived backward: 12 CSR SpMM launches (the reference issues 22), fp32 MFMA GEMMs for
 the projections, the fused MFMA InfoNCE (no B x n logits), and deterministic sorted scatter-adds.
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -22,6 +24,13 @@ from .abstract_recommender import GeneralRecommender
 from .denoise import Denoiser
 from .kernels import ptr, stream
 from .slab import Slab
+
+# independent SpMM products that go out as multi-job launches (gmr_spmm_jobs_f32), a bit mask:
+#   FUSE_FWD   Qi / Qt / G of forward_MM            FUSE_BWD_CL  Tcl / T1 (joins the cl side stream)
+#   FUSE_BWD3  OutI / OutT / T2 (main stream)       FUSE_UI_T    OutI / OutT (cl side stream, T2 on main)
+# GMR_SPMM_FUSE overrides (0 = one launch per product, on side streams as before), for A/B runs
+FUSE_FWD, FUSE_BWD_CL, FUSE_BWD3, FUSE_UI_T = 1, 2, 4, 8
+SPMM_FUSE = int(os.environ.get("GMR_SPMM_FUSE", str(FUSE_FWD | FUSE_UI_T)))
 
 
 def diffmm_tables(noise_scale, noise_min, noise_max, steps):
@@ -191,13 +200,19 @@ class DiffMM(GeneralRecommender):
         st = self._streams
         self._project(w)
         # Qi = iadj @ [E0 | [uE; nimg]]: ris-adj term + contrastive view (diffmm.py:135-136, 175-176)
-        with st.on(0):
-            iadj.spmm(Qi, [(E0, iE), (E0, NF[:, :64])], split=U)
-        with st.on(1):
-            tadj.spmm(Qt, [(E0, iE), (E0, NF[:, 64:])], split=U)
+        # Qt = tadj @ [E0 | [uE; ntxt]]
         # G = adj @ [[uE; nimg] | [uE; ntxt]]                       (diffmm.py:138-139, 148-149)
-        adj.spmm(G, [(E0, NF[:, :64]), (E0, NF[:, 64:])], split=U)
-        st.join(0, 1)
+        if SPMM_FUSE & FUSE_FWD:  # one launch over the three matrices
+            K.spmm_jobs([(iadj, Qi, [(E0, iE), (E0, NF[:, :64])], U, None),
+                         (tadj, Qt, [(E0, iE), (E0, NF[:, 64:])], U, None),
+                         (adj, G, [(E0, NF[:, :64]), (E0, NF[:, 64:])], U, None)])
+        else:
+            with st.on(0):
+                iadj.spmm(Qi, [(E0, iE), (E0, NF[:, :64])], split=U)
+            with st.on(1):
+                tadj.spmm(Qt, [(E0, iE), (E0, NF[:, 64:])], split=U)
+            adj.spmm(G, [(E0, NF[:, :64]), (E0, NF[:, 64:])], split=U)
+            st.join(0, 1)
         # H = adj @ [[G_img[:U]; iE] | [G_txt[:U]; iE]]             (diffmm.py:141-143, 151-153)
         if with_cl:
             # ... and K2 = adj @ [C_img | C_txt] (diffmm.py:171-195) in the same launch: both only
@@ -285,29 +300,60 @@ class DiffMM(GeneralRecommender):
                       ptr(dCLN), 128, stream())
             K.normalize_rows_bwd(w["CLN"][:, :64], w["nrmCL"][0], dCLN[:, :64], dK[:, :64])
             K.normalize_rows_bwd(w["CLN"][:, 64:], w["nrmCL"][1], dCLN[:, 64:], dK[:, 64:])
-            adj.spmm(w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], partial=w["part_cl"])
+            if not SPMM_FUSE & FUSE_BWD_CL:
+                adj.spmm(w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], partial=w["part_cl"])
         K.zero_(dEmb)
         _lib.call("gmr_scatter_sorted_f32", plan_bpr.numel(), 64, ptr(plan_bpr), ptr(w["contrib_bpr"]), 64,
                   ptr(dEmb), 64, stream())
         s.zero_grad()
-        adj.spmm(w["T1"], [(dEmb,)])                                            # adj^T dEmb (adj symmetric)
+        if SPMM_FUSE & FUSE_BWD_CL:  # Tcl = adj^T dK and T1 = adj^T dEmb (adj symmetric) in one launch
+            st.join(0)
+            K.spmm_jobs([(adj, w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], None, w["part_cl"]),
+                         (adj, w["T1"], [(dEmb,)], None, None)])
+        else:
+            adj.spmm(w["T1"], [(dEmb,)])                                        # adj^T dEmb (adj symmetric)
         _lib.call("gmr_dmm_final_bwd", N, ptr(dEmb), ptr(w["T1"]), ptr(w["M"]), ptr(w["nrmM"]), self.ris_lambda,
                   ptr(w["G"]), ptr(s.view("modal_weight")), ptr(w["dE"]), ptr(w["partials"]), stream())
         _lib.call("gmr_dmm_mw_grad", w["partials"].numel() // 2, ptr(w["partials"]), ptr(s.view("modal_weight")),
                   ptr(s.gview("modal_weight")), 0, stream())
+        if SPMM_FUSE & FUSE_BWD3:
+            # the UI-graph transposes of the contrastive/ris branch and the first GCN hop adj^T dE
+            # are independent: one launch; then the second hop
+            _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
+                      ptr(w["Rt"]), stream())
+            K.spmm_jobs([(self._transpose_of(iadj), w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)], None, None),
+                         (self._transpose_of(tadj), w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)], None, None),
+                         (adj, w["T2"], [(w["dE"][:, :64],), (w["dE"][:, 64:],)], None, None)])
+            _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
+            adj.spmm(w["T3"], [(w["DG"][:, :64],), (w["DG"][:, 64:],)])
+            return self._rec_tail(w, loss, reg_share)
         # the contrastive branch (side stream 0, now also after dE) and the two-hop GCN branch (main)
         # only meet in assemble
         with st.on(0):
             _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
                       ptr(w["Rt"]), stream())
-            with st.on(1):
-                self._transpose_of(tadj).spmm(w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)])
-            self._transpose_of(iadj).spmm(w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)])
-            st.join(1)
+            if SPMM_FUSE & FUSE_UI_T:  # both UI-graph transposes in one launch
+                K.spmm_jobs([(self._transpose_of(iadj), w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)], None,
+                              None),
+                             (self._transpose_of(tadj), w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)], None,
+                              None)])
+            else:
+                with st.on(1):
+                    self._transpose_of(tadj).spmm(w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)])
+                self._transpose_of(iadj).spmm(w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)])
+                st.join(1)
         adj.spmm(w["T2"], [(w["dE"][:, :64],), (w["dE"][:, 64:],)])
         _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
         adj.spmm(w["T3"], [(w["DG"][:, :64],), (w["DG"][:, 64:],)])
         st.join(0)
+        return self._rec_tail(w, loss, reg_share)
+
+    def _rec_tail(self, w, loss, reg_share):
+        """assemble dE0 / dNF, then the modality projections' backward (end of rec_step)."""
+        N, U = self.N, self.n_users
+        s = self.rec_slab
+        st = self._streams
+        E0 = s.view("E0")
         _lib.call("gmr_dmm_assemble", N, U, ptr(w["T2"]), ptr(w["T3"]), ptr(w["OutI"]), ptr(w["OutT"]), ptr(E0),
                   2.0 * self.reg_weight * reg_share, ptr(s.gview("E0")), ptr(w["dNF"]), stream())
         # modality projections: normalize + leaky-relu backward, then W grads (text beside image)

@@ -232,10 +232,11 @@ SPMM_HUB_FIXUP = 2  # lane plan with split hub rows: the launch adds their segme
 SPMM_LANE_PLAN = 1 << 16  # | L (32, 64, 128): lane plan (include/gmr.h)
 SPMM_PACKED = 1 << 17  # | SPMM_LANE_PLAN | 32: packed lane plan (col/val of short rows in plan order)
 SPMM_SEG_NNZ = SPMM_LANE_PLAN | 32
-# the fixed norm_adj (built once, 8 of the 12 products of a DiffMM step) runs the packed lane plan:
-# bit-identical sums, 4-7 % faster there at d = 128/256 and slower on the small rebuilt UI graphs
-# (scripts/spmm_bench.py, profiles/r01g_spmm_packed_bench.txt)
-SPMM_NORM_ADJ = SPMM_PACKED | SPMM_LANE_PLAN | 32
+# the fixed norm_adj (built once, 7 of the 11 products of a DiffMM step) runs the plain lane plan:
+# since hub rows are cut into 1,024-entry segments the packed plan (bit-identical sums, 4-7 %
+# faster in round 1, profiles/r01g_spmm_packed_bench.txt) is 5-8 % slower at d = 64 / 128 and
+# 3 % faster only at d = 256 (profiles/r02i_spmm_nt.txt); it stays a tested alternative
+SPMM_NORM_ADJ = SPMM_LANE_PLAN | 32
 SPMM_CHUNK = 1 << 18  # chunk plan: whole-row tasks of <= 128 entries, one gather round per wave (include/gmr.h)
 
 
@@ -333,6 +334,45 @@ def spmm_multi(a, outs, blocks, split=None, alpha=1.0, beta=0.0, partial=None):
                   hi, ldh, split, float(alpha), float(beta), ys, ldy, ptr(a.partial if partial is None else partial),
                   a.flags, stream())
     return outs
+
+
+def spmm_jobs(jobs, alpha=1.0, beta=0.0):
+    """One launch for up to 4 independent lane-plan products (gmr_spmm_jobs_f32).
+
+    jobs: [(a, outs, blocks, split, partial), ...] with a CSR, outs a list of n_rows x 64 output
+    views (one per block) or one n_rows x 64*nb tensor, blocks / split as in CSR.spmm, and partial
+    the hub-row scratch (None: a.partial).  Each job's sums equal its CSR.spmm call's."""
+    n = len(jobs)
+    if not 1 <= n <= 4:
+        raise ValueError("1 to 4 jobs")
+    arr = (_lib.SpmmJob * n)()
+    for q, (a, outs, blocks, split, partial) in enumerate(jobs):
+        nb = len(blocks)
+        if nb not in (1, 2, 4):
+            raise ValueError("1, 2 or 4 blocks of 64 columns")
+        if isinstance(outs, torch.Tensor):
+            if outs.shape != (a.n_rows, 64 * nb):
+                raise ValueError(f"out shape {tuple(outs.shape)} != ({a.n_rows}, {64 * nb})")
+            outs = [outs[:, 64 * b:64 * (b + 1)] for b in range(nb)]
+        if len(outs) != nb or any(o.shape != (a.n_rows, 64) for o in outs):
+            raise ValueError("one n_rows x 64 output per block")
+        for b in blocks:
+            if b[0].shape[1] != 64 or (split is not None and b[1].shape[1] != 64):
+                raise ValueError("each block is 64 columns wide")
+        j = arr[q]
+        j.col, j.val, j.plan = ptr(a.col), ptr(a.val), ptr(a.plan)
+        j.partial = ptr(a.partial if partial is None else partial)
+        j.n_rows, j.nnz, j.seg_nnz, j.n_blocks, j.flags = a.n_rows, a.nnz, a.seg_nnz, nb, a.flags
+        for b in range(nb):
+            j.x_lo[b], j.ld_lo[b] = blocks[b][0].data_ptr(), _ld(blocks[b][0])
+            if split is not None:
+                j.x_hi[b], j.ld_hi[b] = blocks[b][1].data_ptr(), _ld(blocks[b][1])
+            j.y[b], j.ld_y[b] = outs[b].data_ptr(), _ld(outs[b])
+        j.split = a.n_cols if split is None else split
+        j.alpha, j.beta = float(alpha), float(beta)
+    key = tuple((a.nnz, a.n_rows, a.n_cols, len(bl), beta != 0.0) for a, _, bl, _, _ in jobs)
+    with _Probe("spmm", ("jobs",) + key):
+        _lib.call("gmr_spmm_jobs_f32", n, ctypes.cast(arr, ctypes.c_void_p), stream())
 
 
 def spmm_panel(a, out, x_panel, nb, alpha=1.0, beta=0.0, partial=None):

@@ -38,6 +38,8 @@ extern "C" {
 #define GMR_EPI_DTANH 5        /* C = alpha*acc * (1 - aux[m,n]^2)      tanh backward      */
 #define GMR_EPI_ROWSCALE_AUX 6 /* C = alpha*acc + bias + rv1[m]*aux[m,n]                  */
 #define GMR_EPI_BIAS_RELU 7    /* C = relu(alpha*acc + bias)        TransformerDecoderLayer FF */
+#define GMR_GEMM_GLDS (1 << 22)      /* tile flag: stage operands by global_load_lds (the default) */
+#define GMR_GEMM_REGSTAGE (1 << 23)  /* tile flag: stage operands through registers + ds_write */
 #define GMR_GEMM_MFMA16 (1 << 24)
 #define GMR_GEMM_MFMA32 (1 << 25)
 #define GMR_EPI_DRELU 8        /* C = aux[m,n] > 0 ? alpha*acc : 0  ReLU (+ dropout) backward  */
@@ -111,6 +113,30 @@ int gmr_spmm_multi_f32(const int32_t* col, const float* val, int64_t n_rows, int
                        int32_t seg_nnz, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
                        const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
                        float* const* y_blocks, const int64_t* ld_y, float* partial, int32_t flags, void* stream);
+/* One launch for up to 4 independent lane-plan products, of one or several matrices (DiffMM's
+ * Qi = iadj.[E0|nimg], Qt = tadj.[E0|ntxt] and G = adj.[nimg|ntxt] of forward_MM, models/diffmm.py:
+ * 135-149; the backward's adj^T products of the contrastive and BPR gradients, and the UI-graph
+ * transposes beside adj^T dE).  Job q is gmr_spmm_multi_f32's argument list; every job keeps its
+ * own plan, sources, outputs, alpha/beta, partial buffer and flags, and its sums are exactly the
+ * single-job call's.  All jobs of a launch need n_blocks in {1, 2} or all 4.  Hub-row fixups of
+ * the jobs that need one (GMR_SPMM_HUB_FIXUP) follow in one second launch. */
+typedef struct gmr_spmm_job {
+  const int32_t* col;
+  const float* val;
+  const int32_t* plan;
+  float* partial;
+  int64_t n_rows, nnz;
+  int32_t seg_nnz, n_blocks, flags, reserved;
+  const float* x_lo[4];
+  int64_t ld_lo[4];
+  const float* x_hi[4];
+  int64_t ld_hi[4];
+  int64_t split;
+  float alpha, beta;
+  float* y[4];
+  int64_t ld_y[4];
+} gmr_spmm_job;
+int gmr_spmm_jobs_f32(int32_t n_jobs, const gmr_spmm_job* jobs, void* stream);
 int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream);
 int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                      const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,
@@ -145,7 +171,9 @@ int gmr_topk_to_user_csr(int64_t n_users, int32_t k, const int32_t* topk, int64_
  * op(B) = B (K x N, ldb) or B^T (B stored N x K).  bias[(bias_row ? bias_row[m] : 0)*ld_bias + n].
  * Replaces nn.Linear / torch.mm / matmul: diffmm.py:117,124,277,352-358,472-473; vbpr.py:70,105.
  * tile: 0 auto, 64, 128, 256, 256128 (256 x 128) or 128256, optionally | GMR_GEMM_MFMA16 (v_mfma_f32_16x16x4_f32)
- * or | GMR_GEMM_MFMA32 (v_mfma_f32_32x32x2_f32) to force the matrix instruction; split_k: 0 auto, else >= 1.
+ * or | GMR_GEMM_MFMA32 (v_mfma_f32_32x32x2_f32) to force the matrix instruction, | GMR_GEMM_REGSTAGE /
+ * GMR_GEMM_GLDS to force register or global_load_lds operand staging (same sums, bit for bit);
+ * split_k: 0 auto, else >= 1.
  * gmr_gemm_workspace_floats returns the exact scratch the same call needs (splits*M*N floats of
  * split-K partials, 0 when it does not split). */
 int64_t gmr_gemm_workspace_floats(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, int32_t tile,

@@ -76,6 +76,33 @@ def test_rec_step_loss_and_grads(model, golden):
     # (contrast terms are inside rec_loss; checked through the total and the gradients)
 
 
+def test_rec_step_fused_spmm_launches_bit_identical(model, golden):
+    """The multi-job SpMM launches of rec_step (gmr_spmm_jobs_f32: Qi/Qt/G, Tcl/T1, OutI/OutT/T2,
+    OutI/OutT) give exactly the per-product launches' loss and gradients (GMR_SPMM_FUSE=0 path)."""
+    import gmr.diffmm as D
+    g = golden("diffmm_tiny")
+    t = lambda k: torch.as_tensor(g[k].astype(np.int32)).to(DEV)  # noqa: E731
+    out = {}
+    saved = D.SPMM_FUSE
+    try:
+        for fuse in (True, False):
+            # all fusions (the OutI/OutT/T2 variant subsumes the side-stream OutI/OutT one) vs none
+            D.SPMM_FUSE = (D.FUSE_FWD | D.FUSE_BWD_CL | D.FUSE_BWD3) if fuse else 0
+            loss = model.rec_step(t("bpr_users"), t("bpr_pos"), t("bpr_neg"))
+            out[fuse] = (loss.clone(), model.rec_slab.grad.clone())
+    finally:
+        D.SPMM_FUSE = saved
+    assert torch.equal(out[True][0].view(torch.int32), out[False][0].view(torch.int32))
+    assert torch.equal(out[True][1].view(torch.int32), out[False][1].view(torch.int32))
+    try:
+        D.SPMM_FUSE = D.FUSE_FWD | D.FUSE_UI_T
+        loss = model.rec_step(t("bpr_users"), t("bpr_pos"), t("bpr_neg"))
+    finally:
+        D.SPMM_FUSE = saved
+    assert torch.equal(loss.view(torch.int32), out[False][0].view(torch.int32))
+    assert torch.equal(model.rec_slab.grad.view(torch.int32), out[False][1].view(torch.int32))
+
+
 def test_calculate_loss_autograd(model, golden):
     """Reference-style drop-in: loss.backward() leaves the gradients in .grad."""
     g = golden("diffmm_tiny")

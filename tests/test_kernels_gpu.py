@@ -491,3 +491,80 @@ def test_spmm_split_hub_rows(K, nb, seg):
     K.spmm_multi(g, Ym, blocks, alpha=0.6, beta=0.5)
     got = np.concatenate([y.cpu().numpy() for y in Ym], 1)
     assert np.array_equal(got.view(np.uint32), outs[0].view(np.uint32))
+
+
+def test_spmm_jobs_bit_exact(K):
+    """gmr_spmm_jobs_f32: products of three matrices (a packed norm_adj-like plan, a UI graph whose
+    hub rows are split into fixup segments, a small lane plan) in one launch, with split sources,
+    1- and 2-block jobs and alpha/beta, equal the separate CSR.spmm calls bit for bit; two 4-block
+    jobs likewise; mixing 4-block with narrower jobs is refused."""
+    rng = _rng(21)
+    U, I = 6000, 300
+    deg = rng.integers(0, 30, size=U)
+    rows = np.repeat(np.arange(U), deg)
+    p = 1.0 / np.arange(1, I + 1) ** 1.1
+    cols = rng.choice(I, size=rows.size, p=p / p.sum())
+    g1 = K.CSR(*(_dev(a) for a in graph_ref.norm_adj_csr(U, I, rows, cols)), seg_nnz=PACKED32)
+    top = rng.integers(0, I, U)
+    top[rng.random(U) < 0.7] = 5
+    g2 = K.CSR(*(_dev(a) for a in graph_ref.ui_adj_csr(U, I, np.arange(U), top)), seg_nnz=LANE32)
+    assert g2.flags & K.SPMM_HUB_FIXUP
+    Us, Is = 500, 90
+    d3 = rng.integers(0, 6, size=Us)
+    g3 = K.CSR(*(_dev(a) for a in graph_ref.norm_adj_csr(Us, Is, np.repeat(np.arange(Us), d3),
+                                                          rng.integers(0, Is, size=d3.sum()))), seg_nnz=LANE32)
+    N, N3 = U + I, Us + Is
+    X = _dev(rng.standard_normal((N, 256)).astype(np.float32))
+    E = _dev(rng.standard_normal((I, 64)).astype(np.float32))
+    X3 = _dev(rng.standard_normal((N3, 64)).astype(np.float32))
+    Y0 = rng.standard_normal((N, 256)).astype(np.float32)
+    Y3 = rng.standard_normal((N3, 64)).astype(np.float32)
+    jobs_in = [(g1, 2, [(X[:, :64], E), (X[:, 64:128], E)], U),
+               (g2, 2, [(X[:, 128:192],), (X[:, 192:],)], None),
+               (g3, 1, [(X3,)], None)]
+    want = []
+    for g, nb, blocks, split in jobs_in:
+        y = _dev((Y3 if g is g3 else Y0)[:, :64 * nb].copy())
+        g.spmm(y, blocks, split=split, alpha=0.7, beta=0.3)
+        want.append(y.cpu().numpy())
+    outs = [_dev((Y3 if g is g3 else Y0)[:, :64 * nb].copy()) for g, nb, _, _ in jobs_in]
+    K.spmm_jobs([(g, o, blocks, split, None) for (g, nb, blocks, split), o in zip(jobs_in, outs)], alpha=0.7, beta=0.3)
+    for w, o in zip(want, outs):
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), w.view(np.uint32))
+    # two 4-block jobs
+    w4 = []
+    for g in (g1, g2):
+        y = torch.empty((N, 256), device=DEV)
+        g.spmm(y, [(X[:, 64 * b:64 * (b + 1)],) for b in range(4)])
+        w4.append(y)
+    o4 = [torch.empty((N, 256), device=DEV) for _ in range(2)]
+    K.spmm_jobs([(g, o, [(X[:, 64 * b:64 * (b + 1)],) for b in range(4)], None, None) for g, o in zip((g1, g2), o4)])
+    for w, o in zip(w4, o4):
+        assert torch.equal(w.view(torch.int32), o.view(torch.int32))
+    with pytest.raises(Exception, match="lane width"):
+        K.spmm_jobs([(g1, o4[0], [(X[:, 64 * b:64 * (b + 1)],) for b in range(4)], None, None),
+                     (g3, _dev(Y3.copy()), [(X3,)], None, None)])
+
+
+@pytest.mark.parametrize("tile", [64, 128, 256, 256128, 128256])
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
+def test_gemm_glds_bit_exact_vs_register_staging(K, tile, ta, tb):
+    """global_load_lds operand staging (GMR_GEMM_GLDS, swizzled k-contiguous LDS images) gives the
+    register-staged kernel's sums bit for bit: ragged M/N edges, a partial last k tile, split-K
+    slabs and the posterior epilogue; against torch fp32 as well."""
+    GLDS, REG = 1 << 22, 1 << 23
+    rng = _rng(31)
+    for M, N, Kd, split in ((300, 200, 1000, 1), (517, 260, 70, 1), (64, 1000, 2048, 4), (1000, 64, 7050, 8)):
+        A = _dev(rng.standard_normal((Kd, M) if ta else (M, Kd)).astype(np.float32))
+        B = _dev(rng.standard_normal((N, Kd) if tb else (Kd, N)).astype(np.float32))
+        bias = _dev(rng.standard_normal(N).astype(np.float32))
+        outs = []
+        for flag in (GLDS, REG):
+            C = _dev(np.full((M, N), 0.5, dtype=np.float32))
+            K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), epi=K.EPI_POSTERIOR, bias=bias, aux=C, slope=0.9,
+                   beta=0.1, tile=tile | flag, split_k=split)
+            outs.append(C)
+        assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)), (M, N, Kd, split)
+        ref = (A.t() if ta else A) @ (B.t() if tb else B)
+        want = 0.9 * (ref + bias) + 0.1 * 0.5
+        torch.testing.assert_close(outs[0], want, rtol=2e-4, atol=2e-3)
