@@ -49,9 +49,10 @@ STEP_DESC = {"diffmm": "one DiffMMTrainer epoch (diffusion train + graph rebuild
                         "importance-sampled t)"}
 HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFS = 157.3
-KERNEL_NAMES = {"gemm": "gemm_kernel (fp32 MFMA v_mfma_f32_32x32x2_f32, XCD-aware tiles)",
+KERNEL_NAMES = {"gemm": "gemm_glds_kernel (fp32 MFMA v_mfma_f32_32x32x2_f32, global_load_lds staging, XCD-aware tiles)",
                 "infonce": "cl_rows_kernel + cl_table_kernel (fused InfoNCE, fp32 MFMA)",
-                "spmm": "spmm_lane_kernel (CSR, XCD column slices, lane group per row; norm_adj packed plan)"}
+                "spmm": "spmm_lane_kernel / spmm_lane_jobs_kernel (CSR lane plan, XCD column slices, lane group per "
+                        "row, multi-job launches)"}
 
 
 def log(*a):

@@ -783,13 +783,24 @@ __device__ __forceinline__ clx16 cl_dot(const float* blk, const float4 (&fr)[2][
     }
   return s;
 }
-// y^T (64 x 32) += blk^T (64 x 32) X, X (32 x 32) in the accumulator registers (row (e&3)+8(e>>2)+4h)
-__device__ __forceinline__ void cl_acc(const float* blk, const clx16& X, clx16& y0, clx16& y1, int l32, int h) {
+// the lane's A operands of cl_acc, read from LDS ahead of the exp phase (issued together, so the
+// MFMA chain of cl_acc does not wait on one LDS round trip per step)
+__device__ __forceinline__ void cl_acc_load(const float* blk, float (&a0)[16], float (&a1)[16], int l32, int h) {
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int r = (e & 3) + 8 * (e >> 2) + 4 * h;
-    y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(blk[r * kClLd + l32], X[e], y0, 0, 0, 0);
-    y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(blk[r * kClLd + 32 + l32], X[e], y1, 0, 0, 0);
+    a0[e] = blk[r * kClLd + l32];
+    a1[e] = blk[r * kClLd + 32 + l32];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the reads here: hipcc otherwise sinks each next to its MFMA
+}
+// y^T (64 x 32) += blk^T (64 x 32) X, X (32 x 32) in the accumulator registers (row (e&3)+8(e>>2)+4h)
+__device__ __forceinline__ void cl_acc(const float (&a0)[16], const float (&a1)[16], const clx16& X, clx16& y0,
+                                       clx16& y1) {
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], X[e], y0, 0, 0, 0);
+    y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], X[e], y1, 0, 0, 0);
   }
 }
 // the lane's 64-float column of y^T: registers 4g .. 4g+3 hold d = 8g + 4h + 0..3 (+32 in y1)
@@ -818,7 +829,7 @@ __device__ __forceinline__ float cl_exp(float inv_t, float x) {
 }
 
 template <bool FAST>
-__global__ void __launch_bounds__(256) cl_rows_kernel(int B, int n, const float* __restrict__ P, int64_t ldp,
+__global__ void __launch_bounds__(256, 2) cl_rows_kernel(int B, int n, const float* __restrict__ P, int64_t ldp,
                                                       const float* __restrict__ T, int64_t ldt, float inv_t, int chunk,
                                                       float* __restrict__ part_u, float* __restrict__ part_z) {
   __shared__ __attribute__((aligned(16))) float s_blk[2][32 * kClLd];
@@ -841,13 +852,15 @@ __global__ void __launch_bounds__(256) cl_rows_kernel(int B, int n, const float*
     if (more) cl_load(st, T, ldt, j + 32, j1);
     const float* blk = s_blk[cur];
     clx16 s = cl_dot(blk, fr, l32, h);
+    float a0[16], a1[16];
+    cl_acc_load(blk, a0, a1, l32, h);
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int r = (e & 3) + 8 * (e >> 2) + 4 * h;
       s[e] = j + r < j1 ? cl_exp<FAST>(inv_t, s[e]) : 0.f;
       z += s[e];
     }
-    cl_acc(blk, s, y0, y1, l32, h);
+    cl_acc(a0, a1, s, y0, y1);
     if (more) cl_store(st, s_blk[cur ^ 1]);
     __syncthreads();
     cur ^= 1;
@@ -901,7 +914,7 @@ __global__ void __launch_bounds__(256) cl_finalize_kernel(int B, int nc, const f
 }
 
 template <bool FAST>
-__global__ void __launch_bounds__(256) cl_table_kernel(int B, int n, const float* __restrict__ P, int64_t ldp,
+__global__ void __launch_bounds__(256, 2) cl_table_kernel(int B, int n, const float* __restrict__ P, int64_t ldp,
                                                        const float* __restrict__ r, const float* __restrict__ T,
                                                        int64_t ldt, float inv_t, int chunk, float* __restrict__ part_t) {
   __shared__ __attribute__((aligned(16))) float s_blk[2][32 * kClLd];
@@ -930,9 +943,11 @@ __global__ void __launch_bounds__(256) cl_table_kernel(int B, int n, const float
     }
     const float* blk = s_blk[cur];
     clx16 s = cl_dot(blk, fr, l32, h);  // S' (rows i of the block x the wave's 32 table rows)
+    float a0[16], a1[16];
+    cl_acc_load(blk, a0, a1, l32, h);
 #pragma unroll
     for (int e = 0; e < 16; ++e) s[e] = s_r[cur][(e & 3) + 8 * (e >> 2) + 4 * h] * cl_exp<FAST>(inv_t, s[e]);
-    cl_acc(blk, s, y0, y1, l32, h);  // dT^T += P_blk^T (r E)
+    cl_acc(a0, a1, s, y0, y1);  // dT^T += P_blk^T (r E)
     if (more) {
       cl_store(st, s_blk[cur ^ 1]);
       if (threadIdx.x < 32) s_r[cur ^ 1][threadIdx.x] = sr;

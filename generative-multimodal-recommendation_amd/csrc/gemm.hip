@@ -752,6 +752,18 @@ bool default_glds() {
   return g;
 }
 
+// automatic split-K: aim for >= 512 workgroups on 256 CUs; skinny 64^2 products (one tile row or
+// column: the N = 64 projections) split down to ~192-deep K slabs (measured: 384 x 64 x 7050 TN
+// 34 -> 16 us at 32 slabs); the rest keep slabs >= 512 deep
+int auto_splits(int64_t tm, int64_t tn, int bm, int64_t K) {
+  const bool skinny = bm == 64 && (tm == 1 || tn == 1);
+  const int64_t min_k = skinny ? 192 : 512;
+  const int max_s = skinny ? 64 : 16;
+  int s = 1;
+  while (tm * tn * s < 512 && K / (s * 2) >= min_k && s < max_s) s *= 2;
+  return s;
+}
+
 Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int split_k) {
   int mf = default_mfma();
   if (tile & GMR_GEMM_MFMA16) mf = 16;
@@ -773,8 +785,20 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
     const bool wide256 = M >= 2048 && N >= 4096 && K >= 256 && K <= 1024 &&
                          fill(((M + 255) / 256) * ((N + 255) / 256), 256) >=
                              0.92 * fill(((M + 127) / 128) * ((N + 127) / 128), 512);
-    // (with glds staging the NN form of the long-K hidden products, dh = G W1, is faster on 128^2)
-    if (!tnm && M >= 2048 && N >= 1000 && K >= 4096) tile = (tb || !glds) ? 256 : 128;
+    // Long-K products: 256^2 vs 128^2 by the fill of the last wave of workgroups (one 256^2 or
+    // two 128^2 blocks per CU), the split-K slabs each needs (-5 % per doubling) and the 256^2
+    // tile's ~3 % per-flop edge: 19445 x 1000 x 7050 (the whole-user p_sample) runs 2.29 ms on
+    // 128^2 vs 2.67 on 256^2 with two slabs (profiles/r02l_gemm_g1.txt).  With glds staging the
+    // NN form (dh = G W1) is faster on 128^2.
+    auto score = [&](int t) {
+      const int64_t tm = (M + t - 1) / t, tn = (N + t - 1) / t;
+      const int s = auto_splits(tm, tn, t, K);
+      double pen = 1.0;
+      for (int q = s; q > 1; q >>= 1) pen *= 0.95;
+      return fill(tm * tn * s, t == 256 ? 256 : 512) * pen * (t == 256 ? 1.03 : 1.0);
+    };
+    if (!tnm && M >= 2048 && N >= 1000 && K >= 4096)
+      tile = (tb || !glds) && score(256) >= score(128) ? 256 : 128;
     else if (!tnm && wide256) tile = 256;
     else if (!tnm && M * N >= (int64_t)8 << 20 && K >= 512) tile = 128;
     else if (!tnm && M * N >= (int64_t)1 << 20 && K >= 4096) tile = 128;
@@ -789,15 +813,7 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
   p.tm = (M + p.bm - 1) / p.bm;
   p.tn = (N + p.bn - 1) / p.bn;
   int splits = split_k;
-  if (splits <= 0) {  // auto: aim for >= 512 workgroups on 256 CUs
-    // skinny 64^2 products (one tile row or column: the N = 64 projections) split down to
-    // ~192-deep K slabs (measured: 384 x 64 x 7050 TN 34 -> 16 us at 32 slabs); the rest keep >= 512
-    const bool skinny = p.bm == 64 && (p.tm == 1 || p.tn == 1);
-    const int64_t min_k = skinny ? 192 : 512;
-    const int max_s = skinny ? 64 : 16;
-    splits = 1;
-    while (p.tm * p.tn * splits < 512 && K / (splits * 2) >= min_k && splits < max_s) splits *= 2;
-  }
+  if (splits <= 0) splits = auto_splits(p.tm, p.tn, p.bm, K);
   int64_t kps = (K + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
   p.splits = (int)((K + kps - 1) / kps);

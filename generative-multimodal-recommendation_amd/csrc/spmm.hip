@@ -482,7 +482,11 @@ __device__ __forceinline__ int lane_bucket(int deg, int L, int HB) {
   return deg > L ? 30 - (31 - __clz(deg)) : HB + (L - deg);
 }
 
-__host__ __device__ inline int hub_segs(int deg) { return (deg + kHubSeg - 1) / kHubSeg; }
+// rows up to kHubSplit entries stay whole (one workgroup, ≤ 16 passes): norm_adj's Zipf hubs
+// (≤ 4.4k at baby) then need no fixup launch; longer rows (a collapsed rebuilt UI graph's item
+// row of most users) are cut into kHubSeg-entry segments
+constexpr int kHubSplit = 8192;
+__host__ __device__ inline int hub_segs(int deg) { return deg > kHubSplit ? (deg + kHubSeg - 1) / kHubSeg : 1; }
 
 __global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__ rowptr, int n_rows, int64_t nnz, int L,
                                                          int HB, int packed, int* __restrict__ plan) {

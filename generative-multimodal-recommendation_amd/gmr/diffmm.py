@@ -31,6 +31,10 @@ from .slab import Slab
 # GMR_SPMM_FUSE overrides (0 = one launch per product, on side streams as before), for A/B runs
 FUSE_FWD, FUSE_BWD_CL, FUSE_BWD3, FUSE_UI_T = 1, 2, 4, 8
 SPMM_FUSE = int(os.environ.get("GMR_SPMM_FUSE", str(FUSE_FWD | FUSE_UI_T)))
+# users per p_sample launch chain of the graph rebuild: the whole baby user set in one chain
+# (−1.5 ms per rebuild vs 8,192-user chunks: fewer, fuller GEMM waves; 1.3 GB of buffers per
+# denoiser, profiles/r02m_knobs_ab.txt); GMR_REBUILD_CHUNK overrides, for tuning
+REBUILD_CHUNK = int(os.environ.get("GMR_REBUILD_CHUNK", "32768"))
 
 
 def diffmm_tables(noise_scale, noise_min, noise_max, steps):
@@ -383,7 +387,8 @@ class DiffMM(GeneralRecommender):
     def graph_key(self):
         """Identity of every device buffer a captured rec_step bakes in besides its inputs."""
         gs = (self.norm_adj, self.image_UI_matrix, self.text_UI_matrix)
-        return tuple((g.rowptr.data_ptr(), g.plan.data_ptr(), g.flags) for g in gs if g is not None)
+        gs = gs + tuple(self._transpose_of(g) for g in gs[1:] if g is not None)
+        return tuple((g.rowptr.data_ptr(), g.plan.data_ptr(), g.col.data_ptr(), g.flags) for g in gs if g is not None)
 
     def _plans(self, users, pos, neg):
         B = users.numel()
@@ -557,7 +562,7 @@ class DiffMM(GeneralRecommender):
     def p_sample_topk(self, den, users_lo, users_hi, out_topk, k, x_out=None, w1t_fresh=False, slot=0):
         """p_sample(x0, steps=0, no noise) for users [lo, hi) + per-row top-k (trainer.py:545-546)."""
         B = users_hi - users_lo
-        w = self._dwork(min(B, 8192), slot)
+        w = self._dwork(B, slot)
         I, T = self.n_items, self.steps
         assert B <= w["B"]
         x, h = w["x"][:B], w["h"][:B]
@@ -581,11 +586,12 @@ class DiffMM(GeneralRecommender):
         return xi
 
     @torch.no_grad()
-    def rebuild_ui_graphs(self, chunk=8192):
+    def rebuild_ui_graphs(self, chunk=None):
         """Graph construction phase of DiffMMTrainer._train_epoch (trainer.py:529-576) on the device.
         Data parallel: each rank p_samples a contiguous user shard; top-k rows are all-gathered."""
         U, I, k = self.n_users, self.n_items, self.rebuild_k
         dev = self.device
+        chunk = chunk or REBUILD_CHUNK
         lo_r, hi_r, size = dist.padded_shard(U)
         W = dist.world()
         topks = [torch.zeros((W * size, k), dtype=torch.int32, device=dev) for _ in range(2)]

@@ -60,13 +60,11 @@ class Trainer:
         self.evaluator = TopKEvaluator(config)
         self.mg = mg
         self._loss_acc = torch.zeros(2, dtype=torch.float32, device=self.device)
-        # HIP-graph replay of the fixed-size BPR steps (GMR_GRAPHS=1) was measured not to pay on the
-        # baby shape (157.9 vs 155.5 ms/epoch: the graph is re-captured every epoch because the
-        # rebuilt UI adjacencies are new allocations).  Since the rec step forks side streams and
-        # allocates lazily sized workspaces, its capture crashes the process: refused here.
-        if os.environ.get("GMR_GRAPHS", "0") == "1":
-            raise NotImplementedError("GMR_GRAPHS=1: HIP-graph capture of the side-stream rec step is not supported")
-        self._use_graphs = False
+        # GMR_GRAPHS=1: full-size BPR steps of models that expose graph_key() (DiffMM) replay a HIP
+        # graph of the whole rec step, side streams included (torch.cuda.CUDAGraph; captured on the
+        # first step and again when the model's device graphs change, i.e. after each rebuild).
+        # Off by default: the step is GPU-bound, so replay saves only launch gaps.
+        self._use_graphs = os.environ.get("GMR_GRAPHS", "0") == "1" and hasattr(model, "graph_key")
         self._graph = None
 
     def _build_optimizer(self):

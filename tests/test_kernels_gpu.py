@@ -461,16 +461,18 @@ def test_spmm_chunk_rows_spanning_groups(K, nb):
 @pytest.mark.parametrize("seg", [LANE32, PACKED32])
 @pytest.mark.parametrize("nb", [1, 2, 4])
 def test_spmm_split_hub_rows(K, nb, seg):
-    """Lane plans cut hub rows longer than 1,024 entries into segments whose partials a fixup pass
-    adds in segment order (the rebuilt UI graph of a collapsed p_sample: one item row holding most
-    users).  Against fp64, bit-identical across repeats and between the launch entry points."""
+    """Lane plans cut hub rows longer than 8,192 entries into 1,024-entry segments whose partials a
+    fixup pass adds in segment order (the rebuilt UI graph of a collapsed p_sample: one item row
+    holding most users); shorter hubs stay whole.  Against fp64, bit-identical across repeats and
+    between the launch entry points."""
     rng = _rng(12)
-    U, I = 6000, 300
+    U, I = 20000, 300
     top = rng.integers(0, I, U)
-    top[rng.random(U) < 0.7] = 5                       # item 5: ~4.2k users
-    top[rng.random(U) < 0.1] = 17                      # item 17: a second, smaller hub
+    r = rng.random(U)
+    top[r < 0.6] = 5                                   # item 5: ~12k users (split)
+    top[(r >= 0.6) & (r < 0.8)] = 17                   # item 17: ~4k users (a whole-row hub)
     rp, col, val = graph_ref.ui_adj_csr(U, I, np.arange(U), top)
-    assert np.diff(rp).max() > 3 * 1024
+    assert np.diff(rp).max() > 8192 and np.sort(np.diff(rp))[-2] > 2048
     N = U + I
     g = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=seg)
     assert g.flags & K.SPMM_HUB_FIXUP and g.plan_header[2] >> 1 >= 1
@@ -499,7 +501,7 @@ def test_spmm_jobs_bit_exact(K):
     1- and 2-block jobs and alpha/beta, equal the separate CSR.spmm calls bit for bit; two 4-block
     jobs likewise; mixing 4-block with narrower jobs is refused."""
     rng = _rng(21)
-    U, I = 6000, 300
+    U, I = 14000, 300
     deg = rng.integers(0, 30, size=U)
     rows = np.repeat(np.arange(U), deg)
     p = 1.0 / np.arange(1, I + 1) ** 1.1
