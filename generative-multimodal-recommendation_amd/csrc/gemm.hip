@@ -387,7 +387,7 @@ __device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" 
 
 template <int R, bool KC, int NW>
 __device__ __forceinline__ void glds_tile(const float* __restrict__ p, int64_t ld, int64_t r0, int64_t nrows,
-                                          int64_t k0, float* img, int w, int lane) {
+                                          int64_t k0, int64_t kend, float* img, int w, int lane) {
   constexpr int NI = R / 8;  // 1 KiB instructions per operand tile (32 x R floats)
   static_assert(NI % NW == 0, "glds instructions must split evenly over the waves");
 #pragma unroll
@@ -398,67 +398,33 @@ __device__ __forceinline__ void glds_tile(const float* __restrict__ p, int64_t l
       const int r = 8 * j + (lane >> 3);
       const int c = (lane & 7) ^ kc_swz(r);
       const int64_t row = min(r0 + r, nrows - 1);  // rows past the edge: any valid row (discarded)
-      src = p + row * ld + k0 + 4 * c;
+      int64_t k = k0 + 4 * c;
+      if (k >= kend) k = k0;  // chunks past K: any valid chunk, zeroed in LDS (glds_zero_tail)
+      src = p + row * ld + k;
     } else {
       const int f = 256 * j + 4 * lane;
       const int k = f / R, m = f % R;
       const int64_t row = min(r0 + m, ((nrows - 1) >> 2) << 2);
-      src = p + (k0 + k) * ld + row;
+      src = p + min(k0 + k, kend - 1) * ld + row;
     }
     glds16(src, img + 256 * j);
   }
 }
 
-// partial last k tile: zero-filled register loads (issued before the compute) ...
+// a partial last k tile (kend - k0 < 32) landed with junk past K: zero it in the LDS image (the
+// chunk that straddles K was read whole: ld % 4 == 0 keeps that read inside the row)
 template <int R, bool KC, int NT>
-struct TailStage {
-  static constexpr int N4 = R * BK / 4 / NT;
-  float4 r[N4];
-  __device__ __forceinline__ void load(const float* __restrict__ p, int64_t ld, int64_t r0, int64_t nrows, int64_t k0,
-                                       int64_t kend) {
-#pragma unroll
-    for (int i = 0; i < N4; ++i) {
-      const int idx = threadIdx.x + NT * i;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (KC) {
-        const int rr = idx >> 3, k = (int)k0 + (idx & 7) * 4;
-        const int64_t row = r0 + rr;
-        if (row < nrows) {
-          const float* q = p + row * ld + k;
-          if (k < kend) v.x = q[0];
-          if (k + 1 < kend) v.y = q[1];
-          if (k + 2 < kend) v.z = q[2];
-          if (k + 3 < kend) v.w = q[3];
-        }
-      } else {
-        const int kk = idx / (R / 4), m4 = (idx % (R / 4)) * 4;
-        const int64_t k = k0 + kk, row = r0 + m4;
-        if (k < kend) {
-          const float* q = p + k * ld + row;
-          if (row < nrows) v.x = q[0];
-          if (row + 1 < nrows) v.y = q[1];
-          if (row + 2 < nrows) v.z = q[2];
-          if (row + 3 < nrows) v.w = q[3];
-        }
-      }
-      r[i] = v;
+__device__ __forceinline__ void glds_zero_tail(float* img, int kvalid) {
+  for (int idx = threadIdx.x; idx < R * BK; idx += NT) {
+    if (KC) {
+      const int r = idx / BK, kk = idx % BK;  // logical (row, k); stored at chunk (kk / 4) ^ swz(r)
+      if (kk >= kvalid) img[r * BK + 4 * ((kk >> 2) ^ kc_swz(r)) + (kk & 3)] = 0.f;
+    } else {
+      const int kk = idx / R;
+      if (kk >= kvalid) img[idx] = 0.f;
     }
   }
-  // ... and ds_write into the glds image layout (after the compute of the current tile)
-  __device__ __forceinline__ void store(float* img) const {
-#pragma unroll
-    for (int i = 0; i < N4; ++i) {
-      const int idx = threadIdx.x + NT * i;
-      if (KC) {
-        const int rr = idx >> 3, c = idx & 7;
-        *reinterpret_cast<float4*>(img + rr * BK + 4 * (c ^ kc_swz(rr))) = r[i];
-      } else {
-        const int kk = idx / (R / 4), m4 = (idx % (R / 4)) * 4;
-        *reinterpret_cast<float4*>(img + kk * R + m4) = r[i];
-      }
-    }
-  }
-};
+}
 
 // Epilogue through LDS (glds kernel): after the k loop the staging buffers are free, so the tile
 // goes to LDS in row blocks of HR rows (fragment element stores: 32 consecutive columns per half
@@ -559,7 +525,15 @@ __device__ __forceinline__ float4 gfrag(const float* img, int row, int h, int q)
   return make_float4(img[k * R + row], img[(k + 1) * R + row], img[(k + 2) * R + row], img[(k + 3) * R + row]);
 }
 
-template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC>
+// ST-stage ring of LDS images: tile t + ST - 1 is issued while tile t is computed; each wave
+// waits for its own glds with a counted vmcnt (the asm glds are invisible to hipcc's counters),
+// then one barrier publishes the tile.  ST = 2 (ST = 3 optional for the 64^2 tiles).
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int ST>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm_glds_kernel(int64_t M, int64_t N, int64_t K,
                                                                   const float* __restrict__ A, int64_t lda,
                                                                   const float* __restrict__ B, int64_t ldb,
@@ -570,7 +544,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_glds_kernel(int64_t M, in
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   constexpr int AW = BM * BK, STAGE = (BM + BN) * BK;
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  constexpr int GPW = (BM + BN) / 8 / NW;  // glds instructions per wave per k tile
+  static_assert(ST >= 2 && ST <= 4, "2 to 4 stages");
+  __shared__ __attribute__((aligned(16))) float smem[ST * STAGE];
 
   const int nwg = gridDim.x;
   const int b = blockIdx.x;
@@ -580,6 +556,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_glds_kernel(int64_t M, in
   const int64_t n0 = (int64_t)(tile % tiles_n) * BN;
   const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
   const int64_t kend = min(K, kbeg + k_per_split);
+  const int nk = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;  // k tiles; only the last may be partial
+  const int kv_last = (int)(kend - kbeg - (int64_t)(nk - 1) * BK);     // its valid k
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -594,36 +572,34 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_glds_kernel(int64_t M, in
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  TailStage<BM, AKC, NT> ta;
-  TailStage<BN, BKC, NT> tb;
-  if (kbeg < kend) {
-    if (kbeg + BK <= kend) {
-      glds_tile<BM, AKC, NW>(A, lda, m0, M, kbeg, smem, w, lane);
-      glds_tile<BN, BKC, NW>(B, ldb, n0, N, kbeg, smem + AW, w, lane);
-    } else {
-      ta.load(A, lda, m0, M, kbeg, kend);
-      tb.load(B, ldb, n0, N, kbeg, kend);
-      ta.store(smem);
-      tb.store(smem + AW);
+  auto issue = [&](int t) {  // glds of k tile t into ring slot t % ST
+    float* img = smem + (t % ST) * STAGE;
+    const int64_t k0 = kbeg + (int64_t)t * BK;
+    glds_tile<BM, AKC, NW>(A, lda, m0, M, k0, kend, img, w, lane);
+    glds_tile<BN, BKC, NW>(B, ldb, n0, N, k0, kend, img + AW, w, lane);
+  };
+  auto publish = [&](int t) {  // after this wave's glds of tile t landed: share it (zero the tail)
+    __syncthreads();
+    if (t == nk - 1 && kv_last < BK) {
+      float* img = smem + (t % ST) * STAGE;
+      glds_zero_tail<BM, AKC, NT>(img, kv_last);
+      glds_zero_tail<BN, BKC, NT>(img + AW, kv_last);
+      __syncthreads();
     }
+  };
+
+#pragma unroll
+  for (int t = 0; t < ST - 1; ++t)
+    if (t < nk) issue(t);
+  if (nk > 0) {
+    if (nk >= ST - 1) vm_wait<(ST - 2) * GPW>();  // tile 0 landed, tiles 1 .. ST-2 may be in flight
+    else vm_wait<0>();
+    publish(0);
   }
-  glds_wait();
-  __syncthreads();
-  int cur = 0;
-  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
-    const bool more = k0 + BK < kend;
-    const bool tail = more && k0 + 2 * BK > kend;  // the next tile is the partial last one
-    float* nxt = smem + (cur ^ 1) * STAGE;
-    if (more) {
-      if (!tail) {
-        glds_tile<BM, AKC, NW>(A, lda, m0, M, k0 + BK, nxt, w, lane);
-        glds_tile<BN, BKC, NW>(B, ldb, n0, N, k0 + BK, nxt + AW, w, lane);
-      } else {
-        ta.load(A, lda, m0, M, k0 + BK, kend);
-        tb.load(B, ldb, n0, N, k0 + BK, kend);
-      }
-    }
-    const float* a_s = smem + cur * STAGE;
+  for (int t = 0; t < nk; ++t) {
+    const bool refill = t + ST - 1 < nk;
+    if (refill) issue(t + ST - 1);  // the slot of tile t - 1, released by the last barrier
+    const float* a_s = smem + (t % ST) * STAGE;
     const float* b_s = a_s + AW;
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
@@ -642,14 +618,16 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_glds_kernel(int64_t M, in
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
         }
     }
-    if (tail) {
-      ta.store(nxt);
-      tb.store(nxt + AW);
+    if (t + 1 < nk) {
+      // tile t + 1 must have landed; tiles t + 2 .. t + ST - 1 (if issued) may stay in flight
+      if (refill) vm_wait<(ST - 2) * GPW>();
+      else vm_wait<0>();
+      publish(t + 1);
+    } else {
+      __syncthreads();  // every wave is done with the ring before the epilogue reuses it
     }
-    glds_wait();      // this wave's glds of the next tile have landed ...
-    __syncthreads();  // ... everyone's, and this tile's reads are done
-    cur ^= 1;
   }
+  if (nk == 0) __syncthreads();
   gemm_epilogue_lds<BM, BN, WGM, WGN>(acc, smem, M, N, C, ldc, epi, m0, n0, ws);
 }
 
@@ -673,6 +651,16 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const flo
   C[m * ldc + n] = epi_apply(epi, s, m, n, C, ldc);
 }
 
+// ring depth of the 64^2 glds tiles (GMR_GEMM_STAGES64 = 3 for a 3-slot ring; default 2: the
+// 3-slot ring measured no faster on the N = 64 projections, profiles/r02r_gemm.txt)
+int stages64() {
+  static const int s = [] {
+    const char* e = getenv("GMR_GEMM_STAGES64");
+    return (e && atoi(e) == 3) ? 3 : 2;
+  }();
+  return s;
+}
+
 template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int MF>
 void launch_t(bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A,
               int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n,
@@ -680,8 +668,15 @@ void launch_t(bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t
   const dim3 blk(64 * WGM * WGN);
   if constexpr (MF == 32) {
     if (vec && glds) {
-      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, AKC, BKC>), grid, blk, 0, st, M, N, K, A, lda, B, ldb, C,
-                         ldc, epi, tiles_n, kps, ws);
+      if constexpr (BM == 64 && BN == 64) {
+        if (stages64() == 3) {
+          hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, AKC, BKC, 3>), grid, blk, 0, st, M, N, K, A, lda, B,
+                             ldb, C, ldc, epi, tiles_n, kps, ws);
+          return;
+        }
+      }
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, AKC, BKC, 2>), grid, blk, 0, st, M, N, K, A, lda, B, ldb,
+                         C, ldc, epi, tiles_n, kps, ws);
       return;
     }
   }
@@ -754,13 +749,24 @@ bool default_glds() {
 
 // automatic split-K: aim for >= 512 workgroups on 256 CUs; skinny 64^2 products (one tile row or
 // column: the N = 64 projections) split down to ~192-deep K slabs (measured: 384 x 64 x 7050 TN
-// 34 -> 16 us at 32 slabs); the rest keep slabs >= 512 deep
+// 34 -> 16 us at 32 slabs); the rest keep slabs >= 512 deep, and 128^2 long-K products keep
+// splitting while they would run fewer than 8 waves of workgroups or leave the last wave < 90 %
+// full (19445 x 1000 x 7050: 2.42 ms unsplit, 2.30 ms at 4 slabs, profiles/r02q_split.txt)
 int auto_splits(int64_t tm, int64_t tn, int bm, int64_t K) {
   const bool skinny = bm == 64 && (tm == 1 || tn == 1);
   const int64_t min_k = skinny ? 192 : 512;
   const int max_s = skinny ? 64 : 16;
   int s = 1;
   while (tm * tn * s < 512 && K / (s * 2) >= min_k && s < max_s) s *= 2;
+  if (bm == 128) {
+    const int64_t slots = 512;  // two 128^2 workgroups per CU
+    auto waves = [&](int q) { return (double)(tm * tn * q) / (double)slots; };
+    auto fill = [&](int q) {
+      const int64_t w = tm * tn * q;
+      return (double)w / (double)(((w + slots - 1) / slots) * slots);
+    };
+    while ((waves(s) < 8.0 || fill(s) < 0.9) && K / (s * 2) >= min_k && s < max_s) s *= 2;
+  }
   return s;
 }
 
