@@ -128,6 +128,10 @@ def summarize_probe(p, model="diffmm", shape=None):
         if tag in ("gemm", "infonce"):
             if tag == "gemm":
                 work = sum(2.0 * r[2][0] * r[2][1] * r[2][2] for r in recs)
+                # operands read once + C written once (+ read for the in-place / aux epilogues)
+                x_epi = (4, 5, 6, 8)  # POSTERIOR, DTANH, ROWSCALE_AUX, DRELU (include/gmr.h)
+                alg_bytes = sum(4.0 * (M_ * K_ + K_ * N_ + M_ * N_ * (2 if ep in x_epi else 1))
+                                for M_, N_, K_, _, _, ep in (r[2] for r in recs))
             else:  # rows pass S = P T^T and U = E T, table pass the same again: 4 B n 64 MACs
                 work = sum(8.0 * r[2][0] * r[2][1] * 64 for r in recs)
             achieved = work / (tot_ms * 1e-3) / 1e12
@@ -136,6 +140,8 @@ def summarize_probe(p, model="diffmm", shape=None):
                         "launches": len(recs), "avg_us": round(1e3 * tot_ms / len(recs), 2),
                         "total_ms": round(tot_ms, 3), "algorithmic_per_launch": work / len(recs),
                         "algorithmic_unit": "flop", "kernel": KERNEL_NAMES[tag]}
+            if tag == "gemm":
+                out[tag]["algorithmic_bytes_per_launch"] = round(alg_bytes / len(recs))
         else:
             # bytes = 8 nnz + 4 (n_rows+1) + 4 d n_cols (X once) + 4 d n_rows (Y once [+ read if beta])
             # (a multi-job launch, key ("jobs", job, ...), moves the sum of its jobs' bytes)
@@ -155,6 +161,10 @@ def summarize_probe(p, model="diffmm", shape=None):
         if c:
             o["traffic"] = round(c["traffic_per_launch"])
             o["traffic_unit"] = "bytes/launch (memory side: 2 x FETCH_SIZE + WRITE_SIZE)"
+            alg_b = o.get("algorithmic_bytes_per_launch") or (o["algorithmic_per_launch"]
+                                                            if o["algorithmic_unit"] == "bytes" else None)
+            if alg_b:
+                o["traffic_vs_algorithmic_bytes"] = round(c["traffic_per_launch"] / alg_b, 3)
             if c.get("mfma_util") is not None:
                 o["mfma_util"] = round(c["mfma_util"], 4)
             o["pmc_source"] = pmc_src
