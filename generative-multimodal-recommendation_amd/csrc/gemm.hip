@@ -426,6 +426,57 @@ __device__ __forceinline__ void glds_zero_tail(float* img, int kvalid) {
   }
 }
 
+// Final epilogue of one float4 chunk (row m, columns n .. n + 3): bias / x reads and the C store
+// are 16-byte where aligned, element-wise at the right edge.
+struct EpiCtx {
+  const float* xb;
+  int64_t ldx;
+  bool rx, pure, v_in, v_out;
+};
+__device__ __forceinline__ EpiCtx epi_ctx(const Epi& epi, const float* C, int64_t ldc) {
+  EpiCtx c;
+  c.rx = epi_reads_x(epi);
+  c.pure = !c.rx && !epi.bias_row && !epi.rv1 && !epi.rv2;
+  c.xb = (epi.kind == GMR_EPI_NONE || epi.kind == GMR_EPI_BIAS) ? C : epi.aux;
+  c.ldx = (epi.kind == GMR_EPI_NONE || epi.kind == GMR_EPI_BIAS) ? ldc : epi.ld_aux;
+  c.v_out = ldc % 4 == 0 && ((uintptr_t)C & 15) == 0;
+  c.v_in = (!epi.bias || (((uintptr_t)epi.bias & 15) == 0 && (!epi.bias_row || epi.ld_bias % 4 == 0))) &&
+           (!c.rx || (((uintptr_t)c.xb & 15) == 0 && c.ldx % 4 == 0));
+  return c;
+}
+__device__ __forceinline__ void epi_store4(const Epi& epi, float* __restrict__ C, int64_t ldc, int64_t N, int64_t m,
+                                           int64_t n, const float (&a4)[4], const EpiCtx& ctx) {
+  const bool full = n + 3 < N;
+  float b4[4] = {0.f, 0.f, 0.f, 0.f}, x4[4] = {0.f, 0.f, 0.f, 0.f};
+  const float* bp = epi.bias ? epi.bias + (epi.bias_row ? (int64_t)epi.bias_row[m] * epi.ld_bias : 0) + n : nullptr;
+  const float* xp = ctx.rx ? ctx.xb + m * ctx.ldx + n : nullptr;
+  if (full && ctx.v_in) {
+    if (bp) {
+      const float4 t = *reinterpret_cast<const float4*>(bp);
+      b4[0] = t.x, b4[1] = t.y, b4[2] = t.z, b4[3] = t.w;
+    }
+    if (xp) {
+      const float4 t = *reinterpret_cast<const float4*>(xp);
+      x4[0] = t.x, x4[1] = t.y, x4[2] = t.z, x4[3] = t.w;
+    }
+  } else {
+    for (int q = 0; q < 4 && n + q < N; ++q) {
+      if (bp) b4[q] = bp[q];
+      if (xp) x4[q] = xp[q];
+    }
+  }
+  const float r1 = ctx.pure ? 0.f : epi_r1(epi, m), r2 = ctx.pure ? 0.f : epi_r2(epi, m);
+  float o4[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o4[q] = epi_fin(epi, a4[q], b4[q], x4[q], r1, r2);
+  float* o = C + m * ldc + n;
+  if (full && ctx.v_out) {
+    *reinterpret_cast<float4*>(o) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+  } else {
+    for (int q = 0; q < 4 && n + q < N; ++q) o[q] = o4[q];
+  }
+}
+
 // Epilogue through LDS (glds kernel): after the k loop the staging buffers are free, so the tile
 // goes to LDS in row blocks of HR rows (fragment element stores: 32 consecutive columns per half
 // wave, conflict-free) and comes back as float4 row chunks: the bias / aux / C traffic and the
@@ -446,14 +497,8 @@ __device__ __forceinline__ void gemm_epilogue_lds(const floatx16 (&acc)[BM / WGM
   const int w = threadIdx.x >> 6;
   const int wm = w / WGN, wn = w % WGN;
   const int h = lane >> 5, l32 = lane & 31;
-  const bool rx = epi_reads_x(epi);
-  const bool pure = !rx && !epi.bias_row && !epi.rv1 && !epi.rv2;
-  // 16-byte paths: output (slab) rows, bias and x rows all 16-byte aligned
-  const float* xb = (epi.kind == GMR_EPI_NONE || epi.kind == GMR_EPI_BIAS) ? C : epi.aux;
-  const int64_t ldx = (epi.kind == GMR_EPI_NONE || epi.kind == GMR_EPI_BIAS) ? ldc : epi.ld_aux;
-  const bool v_out = ws ? (N % 4 == 0 && ((uintptr_t)ws & 15) == 0) : (ldc % 4 == 0 && ((uintptr_t)C & 15) == 0);
-  const bool v_in = (!epi.bias || (((uintptr_t)epi.bias & 15) == 0 && (!epi.bias_row || epi.ld_bias % 4 == 0))) &&
-                    (!rx || (((uintptr_t)xb & 15) == 0 && ldx % 4 == 0));
+  const EpiCtx ctx = epi_ctx(epi, C, ldc);
+  const bool v_out = ws ? (N % 4 == 0 && ((uintptr_t)ws & 15) == 0) : ctx.v_out;
 #pragma unroll
   for (int r0 = 0; r0 < BM; r0 += HR) {
     __syncthreads();  // the buffers (first pass: the k loop's last reads; later: the previous pass) are free
@@ -486,34 +531,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const floatx16 (&acc)[BM / WGM
         }
         continue;
       }
-      float b4[4] = {0.f, 0.f, 0.f, 0.f}, x4[4] = {0.f, 0.f, 0.f, 0.f};
-      const float* bp = epi.bias ? epi.bias + (epi.bias_row ? (int64_t)epi.bias_row[m] * epi.ld_bias : 0) + n : nullptr;
-      const float* xp = rx ? xb + m * ldx + n : nullptr;
-      if (full && v_in) {
-        if (bp) {
-          const float4 t = *reinterpret_cast<const float4*>(bp);
-          b4[0] = t.x, b4[1] = t.y, b4[2] = t.z, b4[3] = t.w;
-        }
-        if (xp) {
-          const float4 t = *reinterpret_cast<const float4*>(xp);
-          x4[0] = t.x, x4[1] = t.y, x4[2] = t.z, x4[3] = t.w;
-        }
-      } else {
-        for (int q = 0; q < 4 && n + q < N; ++q) {
-          if (bp) b4[q] = bp[q];
-          if (xp) x4[q] = xp[q];
-        }
-      }
-      const float r1 = pure ? 0.f : epi_r1(epi, m), r2 = pure ? 0.f : epi_r2(epi, m);
-      float o4[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) o4[q] = epi_fin(epi, a4[q], b4[q], x4[q], r1, r2);
-      float* o = C + m * ldc + n;
-      if (full && v_out) {
-        *reinterpret_cast<float4*>(o) = make_float4(o4[0], o4[1], o4[2], o4[3]);
-      } else {
-        for (int q = 0; q < 4 && n + q < N; ++q) o[q] = o4[q];
-      }
+      epi_store4(epi, C, ldc, N, m, n, a4, ctx);
     }
   }
 }
@@ -523,6 +541,55 @@ __device__ __forceinline__ float4 gfrag(const float* img, int row, int h, int q)
   if (KC) return *reinterpret_cast<const float4*>(img + row * BK + 4 * ((4 * h + q) ^ kc_swz(row)));
   const int k = 16 * h + 4 * q;
   return make_float4(img[k * R + row], img[(k + 1) * R + row], img[(k + 2) * R + row], img[(k + 3) * R + row]);
+}
+
+// In-launch split-K reduction (glds kernel): each k slice stores its slab, publishes it (agent-
+// scope release) and counts itself in the tile's counter; the slice that arrives last (acquire)
+// sums the slabs in slab order z = 0, 1, ... (the reduce kernel's order: same bits), applies the
+// epilogue and resets the counter to 0 for the next call.  Correct for any placement of a tile's
+// slices over XCDs; no second launch, and the slabs are re-read while still in L2 / MALL.
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void splitk_fixup(float* smem, int* cnt, int64_t M, int64_t N, float* __restrict__ C,
+                                             int64_t ldc, const Epi& epi, int64_t m0, int64_t n0,
+                                             const float* __restrict__ ws) {
+  const int splits = (int)gridDim.z;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are done
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);  // (the one LDS array: no second __shared__ object)
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == splits - 1;
+    if (last) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  const EpiCtx ctx = epi_ctx(epi, C, ldc);
+  const bool v_ws = N % 4 == 0 && ((uintptr_t)ws & 15) == 0;
+  const int64_t slab = M * N;
+  constexpr int C4 = BN / 4;
+  for (int idx = threadIdx.x; idx < BM * C4; idx += NT) {
+    const int64_t m = m0 + idx / C4, n = n0 + (idx % C4) * 4;
+    if (m >= M || n >= N) continue;
+    const float* p = ws + m * N + n;
+    float a4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (v_ws && n + 3 < N) {
+      for (int z = 0; z < splits; ++z) {
+        const float4 t = *reinterpret_cast<const float4*>(p + (int64_t)z * slab);
+        a4[0] += t.x, a4[1] += t.y, a4[2] += t.z, a4[3] += t.w;
+      }
+    } else {
+      for (int z = 0; z < splits; ++z)
+        for (int q = 0; q < 4 && n + q < N; ++q) a4[q] += p[(int64_t)z * slab + q];
+    }
+    epi_store4(epi, C, ldc, N, m, n, a4, ctx);
+  }
 }
 
 // ST-stage ring of LDS images: tile t + ST - 1 is issued while tile t is computed; each wave
@@ -539,7 +606,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_glds_kernel(int64_t M, in
                                                                   const float* __restrict__ B, int64_t ldb,
                                                                   float* __restrict__ C, int64_t ldc, Epi epi,
                                                                   int tiles_n, int64_t k_per_split,
-                                                                  float* __restrict__ ws) {
+                                                                  float* __restrict__ ws, int* __restrict__ counters) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -629,6 +696,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_glds_kernel(int64_t M, in
   }
   if (nk == 0) __syncthreads();
   gemm_epilogue_lds<BM, BN, WGM, WGN>(acc, smem, M, N, C, ldc, epi, m0, n0, ws);
+  if (ws && counters) splitk_fixup<BM, BN, NT>(smem, counters + tile, M, N, C, ldc, epi, m0, n0, ws);
 }
 
 __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const float* __restrict__ ws,
@@ -651,6 +719,14 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const flo
   C[m * ldc + n] = epi_apply(epi, s, m, n, C, ldc);
 }
 
+bool inkernel_fixup() {
+  static const bool f = [] {
+    const char* e = getenv("GMR_GEMM_FIXUP");
+    return e && atoi(e) == 1;
+  }();
+  return f;
+}
+
 // ring depth of the 64^2 glds tiles (GMR_GEMM_STAGES64 = 3 for a 3-slot ring; default 2: the
 // 3-slot ring measured no faster on the N = 64 projections, profiles/r02r_gemm.txt)
 int stages64() {
@@ -664,19 +740,19 @@ int stages64() {
 template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int MF>
 void launch_t(bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A,
               int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n,
-              int64_t kps, float* ws) {
+              int64_t kps, float* ws, int* counters) {
   const dim3 blk(64 * WGM * WGN);
   if constexpr (MF == 32) {
     if (vec && glds) {
       if constexpr (BM == 64 && BN == 64) {
         if (stages64() == 3) {
           hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, AKC, BKC, 3>), grid, blk, 0, st, M, N, K, A, lda, B,
-                             ldb, C, ldc, epi, tiles_n, kps, ws);
+                             ldb, C, ldc, epi, tiles_n, kps, ws, counters);
           return;
         }
       }
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, AKC, BKC, 2>), grid, blk, 0, st, M, N, K, A, lda, B, ldb,
-                         C, ldc, epi, tiles_n, kps, ws);
+                         C, ldc, epi, tiles_n, kps, ws, counters);
       return;
     }
   }
@@ -691,32 +767,32 @@ void launch_t(bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t
 template <int BM, int BN, int WGM, int WGN, int MF>
 void launch_mf(int ta, int tb, bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K,
                const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi,
-               int tiles_n, int64_t kps, float* ws) {
+               int tiles_n, int64_t kps, float* ws, int* counters) {
   // AKC = A is k-contiguous (not transposed); BKC = B is k-contiguous (transposed)
   if (!ta && tb)
     launch_t<BM, BN, WGM, WGN, true, true, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
-                                               ws);
+                                               ws, counters);
   else if (!ta && !tb)
     launch_t<BM, BN, WGM, WGN, true, false, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
-                                                ws);
+                                                ws, counters);
   else if (ta && !tb)
     launch_t<BM, BN, WGM, WGN, false, false, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n,
-                                                 kps, ws);
+                                                 kps, ws, counters);
   else
     launch_t<BM, BN, WGM, WGN, false, true, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
-                                                ws);
+                                                ws, counters);
 }
 
 template <int BM, int BN, int WGM, int WGN>
 void launch_tile(int mf, bool glds, int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N,
                  int64_t K, const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
-                 const Epi& epi, int tiles_n, int64_t kps, float* ws) {
+                 const Epi& epi, int tiles_n, int64_t kps, float* ws, int* counters) {
   if (mf == 16)
     launch_mf<BM, BN, WGM, WGN, 16>(ta, tb, vec, false, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
-                                    ws);
+                                    ws, counters);
   else
     launch_mf<BM, BN, WGM, WGN, 32>(ta, tb, vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
-                                    ws);
+                                    ws, counters);
 }
 
 // Tile, MFMA shape and split-K choice of gmr_gemm_f32 (tile / split_k = 0: automatic).
@@ -831,10 +907,11 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
 
 extern "C" int64_t gmr_gemm_workspace_floats(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                                              int32_t tile, int32_t split_k) {
-  // exact scratch of gmr_gemm_f32 with the same arguments: splits * M * N partial sums, 0 without split-K
+  // exact scratch of gmr_gemm_f32 with the same arguments: the tile-counter words + splits * M * N
+  // partial sums, 0 without split-K
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const Plan p = make_plan(trans_a, trans_b, M, N, K, tile, split_k);
-  return p.splits > 1 ? (int64_t)p.splits * M * N : 0;
+  return p.splits > 1 ? GMR_GEMM_COUNTER_WORDS + (int64_t)p.splits * M * N : 0;
 }
 
 extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, float alpha,
@@ -874,31 +951,38 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   const int splits = pl.splits;
   GMR_ARG(tm * tn < (1ll << 31), "too many tiles");
   float* ws = nullptr;
+  int* counters = nullptr;
   if (splits > 1) {
-    GMR_ARG(workspace && workspace_floats >= (int64_t)splits * M * N,
-            "split-K needs workspace of splits*M*N floats (gmr_gemm_workspace_floats)");
-    ws = workspace;
+    GMR_ARG(workspace && workspace_floats >= GMR_GEMM_COUNTER_WORDS + (int64_t)splits * M * N,
+            "split-K needs workspace of gmr_gemm_workspace_floats(...) floats");
+    ws = workspace + GMR_GEMM_COUNTER_WORDS;
+    // GMR_GEMM_FIXUP=1: the glds kernel reduces in-launch through per-tile counters (words
+    // [0, tiles) of the workspace, zero on entry and on exit).  Off by default: each slice's
+    // agent-scope release writes back its XCD's L2, and that cost more than the reduce launch it
+    // saves (projections 15 -> 48 us, 19445 x 1000 x 7050 2.30 -> 2.59 ms; profiles/r02u_fixup.txt)
+    if (pl.glds && vec && tm * tn <= GMR_GEMM_COUNTER_WORDS && inkernel_fixup())
+      counters = reinterpret_cast<int*>(workspace);
   }
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)(tm * tn), 1, (unsigned)splits);
   switch (tile) {
     case 256:
-      launch_tile<256, 256, 4, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<256, 256, 4, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws, counters);
       break;
     case 256128:
-      launch_tile<256, 128, 4, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<256, 128, 4, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws, counters);
       break;
     case 128256:
-      launch_tile<128, 256, 2, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<128, 256, 2, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws, counters);
       break;
     case 128:
-      launch_tile<128, 128, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<128, 128, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws, counters);
       break;
     default:
-      launch_tile<64, 64, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws);
+      launch_tile<64, 64, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws, counters);
   }
   GMR_LAUNCHED();
-  if (ws) {
+  if (ws && !counters) {
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gmr::grid_for(M * N, 256)), dim3(256), 0, st, M, N, splits, ws, C,
                        ldc, e);
     GMR_LAUNCHED();

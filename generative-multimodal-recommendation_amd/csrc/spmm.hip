@@ -466,7 +466,7 @@ __global__ void __launch_bounds__(kBlkThreads) spmm_blk_kernel(const int* __rest
 // (lane_fix list {row, first slot, n_segments, 0}), so the sum order stays fixed.
 constexpr int kLaneThreads = 256;
 constexpr int kPackTab = 34;  // packed lane plan: bucket-table entries per column (see below)
-constexpr int kLaneMaxBuckets = 160;
+constexpr int kLaneMaxBuckets = 320;
 constexpr int kHubSeg = 1024;  // entries per hub segment
 
 __host__ __device__ inline int64_t lane_desc_cap(int64_t n_rows, int64_t nnz) { return n_rows + nnz / kHubSeg + 1; }
@@ -488,17 +488,25 @@ __device__ __forceinline__ int lane_bucket(int deg, int L, int HB) {
 constexpr int kHubSplit = 8192;
 __host__ __device__ inline int hub_segs(int deg) { return deg > kHubSplit ? (deg + kHubSeg - 1) / kHubSeg : 1; }
 
+// Row classes (csplit > 0, non-packed plans): the short rows >= csplit (the item rows of a
+// bipartite graph) are listed before the rows < csplit (users), each class by descending degree,
+// so each phase of the launch gathers from ONE side's X rows (users' or items' slice): a smaller
+// live footprint per XCD L2 than the interleaved degree order.
+__device__ __forceinline__ int lane_bucket_c(int r, int deg, int L, int HB, int csplit) {
+  return deg > L ? lane_bucket(deg, L, HB) : lane_bucket(deg, L, HB) + (csplit > 0 && r < csplit ? L + 1 : 0);
+}
+
 __global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__ rowptr, int n_rows, int64_t nnz, int L,
-                                                         int HB, int packed, int* __restrict__ plan) {
+                                                         int HB, int packed, int csplit, int* __restrict__ plan) {
   __shared__ int s_cnt[kLaneMaxBuckets], s_off[kLaneMaxBuckets];
   __shared__ int s_slot, s_nfix;
-  const int t = threadIdx.x, nbk = HB + L + 1;
+  const int t = threadIdx.x, nbk = HB + (csplit > 0 ? 2 : 1) * (L + 1);
   for (int i = t; i < nbk; i += 1024) s_cnt[i] = 0;
   if (t == 0) s_slot = s_nfix = 0;
   __syncthreads();
   for (int r = t; r < n_rows; r += 1024) {
     const int deg = rowptr[r + 1] - rowptr[r];
-    atomicAdd(&s_cnt[lane_bucket(deg, L, HB)], deg > L ? hub_segs(deg) : 1);  // one descriptor per hub segment
+    atomicAdd(&s_cnt[lane_bucket_c(r, deg, L, HB, csplit)], deg > L ? hub_segs(deg) : 1);  // one per hub segment
   }
   __syncthreads();
   if (t == 0) {
@@ -529,7 +537,7 @@ __global__ void __launch_bounds__(1024) lane_plan_kernel(const int* __restrict__
   for (int r = t; r < n_rows; r += 1024) {
     const int beg = rowptr[r], end = rowptr[r + 1], deg = end - beg;
     const int ns = deg > L ? hub_segs(deg) : 1;
-    const int d0 = atomicAdd(&s_off[lane_bucket(deg, L, HB)], ns);
+    const int d0 = atomicAdd(&s_off[lane_bucket_c(r, deg, L, HB, csplit)], ns);
     if (ns == 1) {
       desc[d0] = make_int4(r, beg, end, -1);
     } else {  // segments j of the row write partial[slot0 + j]; the fixup adds them in j order
@@ -1252,9 +1260,19 @@ extern "C" int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t se
   return 2 * ((nnz + seg_nnz - 1) / seg_nnz) + 2;
 }
 
+extern "C" int gmr_spmm_plan_build_split(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t seg_nnz,
+                                         int64_t class_split, int32_t* plan, void* stream);
 extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t seg_nnz,
                                    int32_t* plan, void* stream) {
+  return gmr_spmm_plan_build_split(rowptr, n_rows, nnz, seg_nnz, 0, plan, stream);
+}
+
+extern "C" int gmr_spmm_plan_build_split(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t seg_nnz,
+                                         int64_t class_split, int32_t* plan, void* stream) {
   GMR_ARG(rowptr && plan, "null pointer");
+  GMR_ARG(class_split >= 0 && class_split <= n_rows, "class_split must be in [0, n_rows]");
+  GMR_ARG(class_split == 0 || ((seg_nnz & GMR_SPMM_LANE_PLAN) && !lane_packed(seg_nnz)),
+          "row classes need a non-packed lane plan");
   GMR_ARG(n_rows > 0 && n_rows < (1ll << 31) && nnz >= 0 && nnz < (1ll << 31), "bad size");
   if (is_chunk(seg_nnz)) {
     GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
@@ -1267,7 +1285,7 @@ extern "C" int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_
     GMR_ARG(L, "lane plans take seg_nnz = GMR_SPMM_LANE_PLAN | 32, 64 or 128 (packed: 32)");
     GMR_ARG(((uintptr_t)plan & 15) == 0, "plan must be 16-byte aligned");
     hipLaunchKernelGGL(lane_plan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, (int)n_rows, nnz, L,
-                       lane_hb(L), (int)lane_packed(seg_nnz), plan);
+                       lane_hb(L), (int)lane_packed(seg_nnz), (int)class_split, plan);
     GMR_LAUNCHED();
     return GMR_OK;
   }

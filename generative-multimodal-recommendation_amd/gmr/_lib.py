@@ -37,6 +37,7 @@ SIGNATURES = {
     "gmr_sqnorm_nparts": (I64, [I64]),
     "gmr_spmm_partial_rows": (I64, [I64, I64, I32]),
     "gmr_spmm_plan_build": (I32, [P, I64, I64, I32, P, P]),
+    "gmr_spmm_plan_build_split": (I32, [P, I64, I64, I32, I64, P, P]),
     "gmr_spmm_plan_pack": (I32, [P, P, P, I64, I64, I32, P, P]),
     "gmr_spmm_plan_info": (I32, [P, P, P]),
     "gmr_event_create": (I32, [P]),

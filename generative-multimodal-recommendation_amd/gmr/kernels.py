@@ -187,7 +187,9 @@ def workspace(nfloats, device, tag="gemm"):
            else torch.cuda.current_stream().cuda_stream)
     w = _ws.get(key)
     if w is None or w.numel() < nfloats:
-        w = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
+        # zeroed: a GEMM split-K workspace starts with tile counters that must be zero
+        # (GMR_GEMM_COUNTER_WORDS, include/gmr.h); every call leaves them zero
+        w = torch.zeros(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
         _ws[key] = w
     return w
 
@@ -227,6 +229,10 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
 # SPMM_LANE_PLAN | L = lane plan (XCD column slices, lane group per row)
 # (see include/gmr.h).  The lane plan with L = 32 measured fastest on the DiffMM graphs
 # (scripts/spmm_bench.py, profiles/r01_spmm_lane_bench.txt).
+# GMR_SPMM_CLASSES=1: lane plans of bipartite graphs schedule the item rows before the user rows
+# (gmr_spmm_plan_build_split).  Off by default: −2…3 % per product alone, but the BPR phase ran
+# 1.4 ms slower with it (profiles/r02v_spmm_classes_ab.txt)
+SPMM_CLASSES = os.environ.get("GMR_SPMM_CLASSES", "0") == "1"
 SPMM_NO_SPLIT_ROWS = 1
 SPMM_HUB_FIXUP = 2  # lane plan with split hub rows: the launch adds their segment partials (include/gmr.h)
 SPMM_LANE_PLAN = 1 << 16  # | L (32, 64, 128): lane plan (include/gmr.h)
@@ -243,7 +249,7 @@ SPMM_CHUNK = 1 << 18  # chunk plan: whole-row tasks of <= 128 entries, one gathe
 class CSR:
     """Device CSR (int32 rowptr/col, fp32 val) of an n x n matrix with its SpMM work plan."""
 
-    def __init__(self, rowptr, col, val, n_cols=None, seg_nnz=None, symmetric=True):
+    def __init__(self, rowptr, col, val, n_cols=None, seg_nnz=None, symmetric=True, class_split=0):
         seg_nnz = SPMM_SEG_NNZ if seg_nnz is None else seg_nnz
         self.rowptr, self.col, self.val = rowptr, col, val
         self.n_rows = rowptr.numel() - 1
@@ -256,7 +262,10 @@ class CSR:
         self.plan = torch.empty(words, dtype=torch.int32, device=dev)
         prow = _lib.load().gmr_spmm_partial_rows(self.n_rows, self.nnz, seg_nnz)
         self.partial = torch.zeros((prow, 256), dtype=torch.float32, device=dev)
-        _lib.call("gmr_spmm_plan_build", ptr(rowptr), self.n_rows, self.nnz, seg_nnz, ptr(self.plan), stream())
+        cs = class_split if (SPMM_CLASSES and seg_nnz & SPMM_LANE_PLAN and not seg_nnz & SPMM_PACKED) else 0
+        self.class_split = class_split
+        _lib.call("gmr_spmm_plan_build_split", ptr(rowptr), self.n_rows, self.nnz, seg_nnz, cs, ptr(self.plan),
+                  stream())
         if seg_nnz & SPMM_PACKED or seg_nnz == SPMM_CHUNK:  # col/val are final here (built before wrapping)
             _lib.call("gmr_spmm_plan_pack", ptr(rowptr), ptr(col), ptr(val), self.n_rows, self.nnz, seg_nnz,
                       ptr(self.plan), stream())
@@ -391,7 +400,8 @@ def spmm_panel(a, out, x_panel, nb, alpha=1.0, beta=0.0, partial=None):
 
 
 def bipartite_symnorm(n_users, n_items, user_ptr, user_items, self_loops, deg_eps, seg_nnz=None):
-    """Build the normalised (U+I)^2 bipartite adjacency on the device (graph.hip)."""
+    """Build the normalised (U+I)^2 bipartite adjacency on the device (graph.hip); its lane plan
+    lists the item rows before the user rows (row classes, gmr_spmm_plan_build_split)."""
     lib = _lib.load()
     dev = user_ptr.device
     n_ui = user_items.numel()
@@ -403,7 +413,7 @@ def bipartite_symnorm(n_users, n_items, user_ptr, user_items, self_loops, deg_ep
     ws = torch.empty(lib.gmr_bipartite_workspace_ints(n_users, n_items), dtype=torch.int32, device=dev)
     _lib.call("gmr_bipartite_symnorm_build", n_users, n_items, ptr(user_ptr), ptr(user_items), n_ui,
               int(self_loops), float(deg_eps), ptr(ws), ptr(rowptr), ptr(col), ptr(val), stream())
-    return CSR(rowptr, col[:nnz], val[:nnz], seg_nnz=seg_nnz)
+    return CSR(rowptr, col[:nnz], val[:nnz], seg_nnz=seg_nnz, class_split=n_users)
 
 
 def topk_to_user_csr(topk, user_ptr, user_items):
@@ -504,7 +514,8 @@ def csr_transpose(a):
     ws = torch.empty(2 * nc, dtype=torch.int32, device=dev)
     _lib.call("gmr_csr_transpose", a.n_rows, nc, a.nnz, ptr(a.rowptr), ptr(a.col), ptr(a.val), ptr(ws), ptr(trp),
               ptr(tcol), ptr(tval), ptr(scol), ptr(sval), stream())
-    return CSR(trp, tcol[:a.nnz], tval[:a.nnz], n_cols=a.n_rows, symmetric=False)
+    return CSR(trp, tcol[:a.nnz], tval[:a.nnz], n_cols=a.n_rows, symmetric=False,
+               class_split=a.class_split if a.n_rows == a.n_cols else 0)
 
 
 def csr_drop_edges(a, keep_rate, seed=0, step=0, keep=None, transposed=False):
@@ -522,7 +533,7 @@ def csr_drop_edges(a, keep_rate, seed=0, step=0, keep=None, transposed=False):
     oval = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
     _lib.call("gmr_csr_drop_write", a.n_rows, ptr(a.rowptr), ptr(a.col), ptr(a.val), int(transposed), ptr(keep),
               float(keep_rate), int(seed), int(step), ptr(orp), ptr(ocol), ptr(oval), stream())
-    return CSR(orp, ocol[:nnz], oval[:nnz], n_cols=a.n_cols, symmetric=False)
+    return CSR(orp, ocol[:nnz], oval[:nnz], n_cols=a.n_cols, symmetric=False, class_split=a.class_split)
 
 
 def knn_graph(feat, k):

@@ -38,6 +38,9 @@ extern "C" {
 #define GMR_EPI_DTANH 5        /* C = alpha*acc * (1 - aux[m,n]^2)      tanh backward      */
 #define GMR_EPI_ROWSCALE_AUX 6 /* C = alpha*acc + bias + rv1[m]*aux[m,n]                  */
 #define GMR_EPI_BIAS_RELU 7    /* C = relu(alpha*acc + bias)        TransformerDecoderLayer FF */
+/* split-K workspaces start with this many int32 tile counters: zero them once when the buffer is
+ * allocated (every gmr_gemm_f32 call leaves them zero); the partial slabs follow */
+#define GMR_GEMM_COUNTER_WORDS 16384
 #define GMR_GEMM_GLDS (1 << 22)      /* tile flag: stage operands by global_load_lds (the default) */
 #define GMR_GEMM_REGSTAGE (1 << 23)  /* tile flag: stage operands through registers + ds_write */
 #define GMR_GEMM_MFMA16 (1 << 24)
@@ -91,6 +94,12 @@ int gmr_stream_fork(void* from, void* to, void* ev);
 #define GMR_SPMM_CHUNK_PLAN (1 << 18)
 int64_t gmr_spmm_plan_words(int64_t n_rows, int64_t nnz, int32_t seg_nnz);
 int64_t gmr_spmm_partial_rows(int64_t n_rows, int64_t nnz, int32_t seg_nnz);
+/* gmr_spmm_plan_build with row classes (non-packed lane plans): the short rows >= class_split are
+ * scheduled before the rows < class_split, each class by descending degree (the item rows, then
+ * the user rows of a bipartite graph: each phase gathers one side's X rows); 0 = one class.
+ * Same sums as the one-class plan. */
+int gmr_spmm_plan_build_split(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t seg_nnz,
+                              int64_t class_split, int32_t* plan, void* stream);
 int gmr_spmm_plan_build(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t seg_nnz, int32_t* plan,
                         void* stream);
 /* Copies the 4-word plan header to the host (synchronises the stream): segment plan
@@ -174,8 +183,10 @@ int gmr_topk_to_user_csr(int64_t n_users, int32_t k, const int32_t* topk, int64_
  * or | GMR_GEMM_MFMA32 (v_mfma_f32_32x32x2_f32) to force the matrix instruction, | GMR_GEMM_REGSTAGE /
  * GMR_GEMM_GLDS to force register or global_load_lds operand staging (same sums, bit for bit);
  * split_k: 0 auto, else >= 1.
- * gmr_gemm_workspace_floats returns the exact scratch the same call needs (splits*M*N floats of
- * split-K partials, 0 when it does not split). */
+ * gmr_gemm_workspace_floats returns the exact scratch the same call needs (GMR_GEMM_COUNTER_WORDS
+ * tile counters + splits*M*N floats of split-K partials, 0 when it does not split); the counter
+ * words must be zero before the first call (they are left zero).  With glds staging the slices of
+ * a tile are summed in-launch by the last one to finish (same slab order as the reduce pass). */
 int64_t gmr_gemm_workspace_floats(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, int32_t tile,
                                   int32_t split_k);
 int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,

@@ -570,3 +570,33 @@ def test_gemm_glds_bit_exact_vs_register_staging(K, tile, ta, tb):
         ref = (A.t() if ta else A) @ (B.t() if tb else B)
         want = 0.9 * (ref + bias) + 0.1 * 0.5
         torch.testing.assert_close(outs[0], want, rtol=2e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("nb", [1, 2, 4])
+def test_spmm_row_classes_bit_exact(K, nb):
+    """Lane plans with row classes (item rows scheduled before user rows,
+    gmr_spmm_plan_build_split) give the one-class plan's sums bit for bit, with split sources and
+    a hub row above the segment-split threshold."""
+    rng = _rng(23)
+    U, I = 12000, 400
+    deg = rng.integers(0, 25, size=U)
+    rows = np.repeat(np.arange(U), deg)
+    p = 1.0 / np.arange(1, I + 1) ** 1.2
+    cols = rng.choice(I, size=rows.size, p=p / p.sum())
+    rp, col, val = graph_ref.norm_adj_csr(U, I, rows, cols)
+    N = U + I
+    saved = K.SPMM_CLASSES
+    K.SPMM_CLASSES = True
+    try:
+        g0 = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=LANE32, class_split=0)
+        g1 = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=LANE32, class_split=U)
+    finally:
+        K.SPMM_CLASSES = saved
+    X = _dev(rng.standard_normal((N, 64 * nb)).astype(np.float32))
+    E = _dev(rng.standard_normal((I, 64 * nb)).astype(np.float32))
+    outs = []
+    for g in (g0, g1):
+        y = torch.empty((N, 64 * nb), device=DEV)
+        g.spmm(y, [(X[:, 64 * b:64 * (b + 1)], E[:, 64 * b:64 * (b + 1)]) for b in range(nb)], split=U)
+        outs.append(y)
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
