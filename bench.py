@@ -351,6 +351,7 @@ def main():
     ap.add_argument("--no-legs", action="store_true", help="headline only (no DiffRec / GenRecV1 legs)")
     ap.add_argument("--eval-passes", type=int, default=3)
     ap.add_argument("--no-probe", action="store_true", help="no serial roofline epoch (A/B timing only)")
+    ap.add_argument("--no-dp-local", action="store_true", help="N > 1: skip the GMR_DP_MODE=local measurement")
     ap.add_argument("--scoring-dtype", default=None, choices=["fp32", "fp16"],
                     help="GenRecV1 full-catalog scoring precision (config 5's fp16 MFMA scoring GEMM)")
     args = ap.parse_args()
@@ -383,6 +384,26 @@ def main():
         return float(t.item())
 
     head = run_workload(args, dist_on, barrier, max_over_ranks, world == 1 and not args.no_cpu_baseline)
+    # N > 1: the headline keeps the reference's global batch (each 2,048-row batch split over the
+    # GPUs); the opt-in GMR_DP_MODE=local schedule (each GPU takes whole batches: world x 2,048 rows
+    # per optimiser step, 1 / world of the steps) is measured beside it under its own key
+    dp_local = None
+    if dist_on and not args.no_dp_local and os.environ.get("GMR_DP_MODE", "global") != "local":
+        os.environ["GMR_DP_MODE"] = "local"
+        try:
+            a3 = argparse.Namespace(**vars(args))
+            a3.no_probe = True
+            r = run_workload(a3, dist_on, barrier, max_over_ranks, False)
+            dp_local = {"value": r["train_users_per_s"], "unit": "users/s", "ms_per_step": r["ms_per_step"],
+                        "global_batch": world * r["global_batch"], "eval_users_per_s": r["eval_users_per_s"],
+                        "eval_recall@20": r["eval_recall@20"],
+                        "note": "GMR_DP_MODE=local: each GPU takes whole train_batch_size batches (world x "
+                                "train_batch_size rows per optimiser step, 1/world of the reference's steps per "
+                                "epoch); a different schedule from the reference's, not the headline value"}
+        except Exception as e:  # noqa: BLE001
+            dp_local = {"error": repr(e)}
+        finally:
+            os.environ.pop("GMR_DP_MODE", None)
     leg_out = {}
     if legs:
         for key, m, shape, sd in (("diffrec", "diffrec", "baby", None), ("genrecv1_fp16", "genrecv1", "tiktok", "fp16")):
@@ -420,6 +441,8 @@ def main():
             line["cpu_baseline"] = head["cpu_baseline"]
         if leg_out:
             line["legs"] = leg_out
+        if dp_local:
+            line["dp_local_batch"] = dp_local
         print(json.dumps(line), flush=True)
     if dist_on:
         torch.distributed.destroy_process_group()

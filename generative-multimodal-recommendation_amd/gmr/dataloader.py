@@ -70,7 +70,7 @@ class TrainDataLoader:
 
     def to_device(self):
         from . import dist
-        W = dist.world()
+        W = 1 if dist.local_batches() else dist.world()  # sub-batches per batch (whole batches: 1)
         if self._dev is not None and self._dev["world"] != W:
             self._dev = None
         if self._dev is None:
@@ -125,18 +125,32 @@ class TrainDataLoader:
         return int(self.to_device()["n_fallback"].item())
 
     def batches(self, d, rank=None):
-        """Per batch b of the epoch draw: (b, global rows, users, pos, neg, plan_bpr, plan_cl) of this
-        rank's sub-batch (the whole batch at world size 1).  `global rows` is the size of batch b,
-        which the data-parallel step normalises by; a rank's sub-batch may be empty."""
+        """Per global optimiser step g of the epoch draw: (g, rank_rows, users, pos, neg, plan_bpr,
+        plan_cl) of this rank's rows — its sub-batch of batch g (the whole batch at world size 1), or
+        under GMR_DP_MODE=local its own whole batch g * world + rank.  rank_rows lists the rows of
+        every rank in the step (dist.dp_scales normalises by their sum); a rank's part may be empty."""
         from . import dist
         W = d["world"]
         r = dist.rank() if rank is None else rank
         nb, B = d["n_batches"], self.batch_size
         s, offs = d["sample"], d["offsets_np"]
+        if W == 1 and dist.local_batches():
+            Wd = dist.world()
+            for g in range(-(-nb // Wd)):
+                sizes = [max(0, min(self.n_inter, (g * Wd + q + 1) * B) - min(self.n_inter, (g * Wd + q) * B))
+                         for q in range(Wd)]
+                b = g * Wd + r
+                if b < nb:
+                    lo, hi = int(offs[b]), int(offs[b + 1])
+                    yield g, sizes, s[0, lo:hi], s[1, lo:hi], s[2, lo:hi], d["plan_bpr"][b], d["plan_cl"][b]
+                else:
+                    e = s[:, :0]
+                    yield g, sizes, e[0], e[1], e[2], d["plan_bpr"][0], d["plan_cl"][0]
+            return
         for b in range(nb):
             lo, hi = int(offs[b * W + r]), int(offs[b * W + r + 1])
             rows = min((b + 1) * B, self.n_inter) - b * B
-            yield (b, rows, s[0, lo:hi], s[1, lo:hi], s[2, lo:hi], d["plan_bpr"][b * W + r],
+            yield (b, dist.shard_sizes(rows, W), s[0, lo:hi], s[1, lo:hi], s[2, lo:hi], d["plan_bpr"][b * W + r],
                    d["plan_cl"][b * W + r])
 
     # --- reference-style iteration -------------------------------------------------------

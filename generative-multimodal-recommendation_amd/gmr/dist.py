@@ -13,14 +13,54 @@ F2); this module holds the sharding rules used by the trainers:
 The global batch is the reference's train_batch_size at every world size, so the number of
 optimiser steps per epoch, and the trajectory up to fp32 reassociation of the sums, are the
 single-process ones (the per-GPU batch shrinks as B / world: strong scaling).
+
+Opt-in GMR_DP_MODE=local ("partition users across the GPUs", BASELINE north star): every rank
+takes whole train_batch_size batches (rank r takes batch g * world + r of global step g), so one
+global step is world batches = the single-process step with a world x train_batch_size batch; the
+epoch takes 1 / world of the optimiser steps.  This changes the reference's schedule and is
+reported under its own label by bench.py, never as the default.
 Everything here also runs on CPU tensors with the gloo backend (tests/test_dist_cpu.py).
 """
+import os
+
 import torch
 import torch.distributed as tdist
 
 
 def is_dist():
     return tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1
+
+
+def dp_mode():
+    """'global' (default: the reference's batch split over the ranks) or 'local' (GMR_DP_MODE=local)."""
+    return "local" if os.environ.get("GMR_DP_MODE", "global") == "local" else "global"
+
+
+def local_batches():
+    """True when ranks take whole batches (GMR_DP_MODE=local with more than one rank)."""
+    return dp_mode() == "local" and world() > 1
+
+
+def step_slices(n, B, w=None, r=None):
+    """The global optimiser steps over n rows in batches of B, for rank r of w: yields
+    (g, lo, hi, blo, bhi, rank_rows, row0) — this rank's rows [lo, hi), the batch they belong to
+    [blo, bhi) (the whole global batch in 'global' mode, the rank's own batch in 'local' mode), the
+    rows every rank holds in step g, and this rank's offset inside the step's concatenated rows
+    (the key of its per-row random draws)."""
+    w = world() if w is None else w
+    r = rank() if r is None else r
+    nb = -(-n // B)
+    if dp_mode() == "local" and w > 1:
+        for g in range(-(-nb // w)):
+            sizes = [max(0, min(n, (g * w + q + 1) * B) - min(n, (g * w + q) * B)) for q in range(w)]
+            blo = min(n, (g * w + r) * B)
+            bhi = blo + sizes[r]
+            yield g, blo, bhi, blo, bhi, sizes, sum(sizes[:r])
+        return
+    for g in range(nb):
+        blo, bhi = g * B, min(n, (g + 1) * B)
+        a, b = shard(bhi - blo, w, r)
+        yield g, blo + a, blo + b, blo, bhi, shard_sizes(bhi - blo, w), a
 
 
 def world():

@@ -85,13 +85,13 @@ class Trainer:
         hook = getattr(self.model, "dp_step_end", None)  # per-global-step model state sync (DiffRec)
         # one optimiser step per train_batch_size batch, as the reference (trainer.py:144-208);
         # under data parallelism every batch is split over the ranks
-        for b, rows, u, p, ng, pb, pc in train_data.batches(d):
-            norm, share = dist.dp_scales(dist.shard_sizes(rows, W))
+        for b, rank_rows, u, p, ng, pb, pc in train_data.batches(d):
+            norm, share = dist.dp_scales(rank_rows)
             if u.numel() > 0:
-                if self._use_graphs and rows == train_data.batch_size:
+                if self._use_graphs and W == 1 and u.numel() == train_data.batch_size:
                     self._graphed_step(u, p, ng, pb, pc, norm, share, acc)
                 else:
-                    loss = self._rec_step(u, p, ng, pb, pc, norm, share, dist.shard(rows)[0])
+                    loss = self._rec_step(u, p, ng, pb, pc, norm, share, sum(rank_rows[:dist.rank()]))
                     _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
             else:
                 for s_ in slabs:
@@ -351,11 +351,10 @@ class DiffMMTrainer(Trainer):
         opts = (self.denoise_opt_image, self.denoise_opt_text)
         st = m._streams
         steps = 0
-        for g, lo in enumerate(range(0, U, B)):
-            hi = min(U, lo + B)
-            a, b = dist.shard(hi - lo, W, r)
-            users = self._perm[lo + a:lo + b]
+        for g, lo, hi, _, _, rank_rows, row0 in dist.step_slices(U, B, W, r):
+            users = self._perm[lo:hi]
             nb = users.numel()
+            norm = sum(rank_rows)
             base = (self._epoch_ctr * 100000 + g) * 2
             # the two denoisers are independent until their Adam steps: the text one runs on a side
             # stream (own work buffers, slot 1) beside the image one; under DP the image gradient
@@ -363,10 +362,9 @@ class DiffMMTrainer(Trainer):
             def one(j):
                 den, feats = dens[j]
                 if nb > 0:
-                    diff, gc = m.diffusion_step(den, users, feats, iE, base + j, norm_rows=hi - lo, slot=j, row0=a)
-                    _lib.call("gmr_sum_f64", nb, ptr(diff), 1.0 / (hi - lo), ptr(self._dloss[j:j + 1]), 1, stream())
-                    _lib.call("gmr_sum_f64", nb, ptr(gc), m.e_loss / (hi - lo), ptr(self._dloss[j:j + 1]), 1,
-                              stream())
+                    diff, gc = m.diffusion_step(den, users, feats, iE, base + j, norm_rows=norm, slot=j, row0=row0)
+                    _lib.call("gmr_sum_f64", nb, ptr(diff), 1.0 / norm, ptr(self._dloss[j:j + 1]), 1, stream())
+                    _lib.call("gmr_sum_f64", nb, ptr(gc), m.e_loss / norm, ptr(self._dloss[j:j + 1]), 1, stream())
                 else:
                     den.slab.zero_grad()
 
@@ -460,14 +458,12 @@ class GenRecV1Trainer(Trainer):
         _lib.call("gmr_permutation", U, m.seed, 2000 + self._epoch_ctr, ptr(self._perm), stream())
         K.zero_(self._dloss)
         steps = 0
-        for g, lo in enumerate(range(0, U, B)):
-            hi = min(U, lo + B)
-            a, b = dist.shard(hi - lo, W, r)
-            users = self._perm[lo + a:lo + b]
+        for g, lo, hi, blo, bhi, rank_rows, _ in dist.step_slices(U, B, W, r):
+            users = self._perm[lo:hi]
             step = ((self._epoch_ctr * 100000 + g) * W + r) * 4
             if users.numel() > 0:
-                lv = diff.training_step(den, users, iE, feats_i, m.seed, step, norm_rows=hi - lo,
-                                        sched_users=self._perm[lo:hi])
+                lv = diff.training_step(den, users, iE, feats_i, m.seed, step, norm_rows=sum(rank_rows),
+                                        sched_users=self._perm[blo:bhi])
                 _lib.call("gmr_axpy_dev_f32", 4, ptr(self._one), ptr(lv), ptr(self._dloss), stream())
             else:
                 den.slab.zero_grad()

@@ -130,3 +130,26 @@ def test_dp_gradient_equals_full_batch_gloo():
     size = -(-U // world)
     got = np.concatenate([full[r * size:r * size + hi - lo, 0] for r, (lo, hi) in enumerate(lo_hi)])
     assert np.array_equal(got, np.arange(U))
+
+
+@pytest.mark.parametrize("mode", ["global", "local"])
+@pytest.mark.parametrize("n,B,w", [(1000, 96, 3), (7, 4, 2), (4096, 2048, 8), (95, 96, 4)])
+def test_step_slices_cover_every_row_once(monkeypatch, mode, n, B, w):
+    """dist.step_slices: over all ranks every row lies in exactly one slice; rank_rows agrees with
+    the slices; row0 is the rank's offset in the step's concatenated rows; 'global' keeps
+    ceil(n / B) steps of one batch, 'local' ceil(n / B / w) steps of w whole batches."""
+    from gmr import dist
+    monkeypatch.setenv("GMR_DP_MODE", mode)
+    seen = np.zeros(n, np.int64)
+    steps = None
+    for r in range(w):
+        sl = list(dist.step_slices(n, B, w, r))
+        steps = len(sl) if steps is None else steps
+        assert len(sl) == steps
+        for g, lo, hi, blo, bhi, rank_rows, row0 in sl:
+            assert hi - lo == rank_rows[r] and row0 == sum(rank_rows[:r])
+            assert blo <= lo <= hi <= bhi
+            seen[lo:hi] += 1
+    assert (seen == 1).all()
+    nb = -(-n // B)
+    assert steps == (nb if mode == "global" else -(-nb // w))

@@ -138,3 +138,68 @@ def test_dp2_step_equals_single_process():
     for k in ("den_img", "den_txt", "rec_params"):
         np.testing.assert_allclose(dp[k], single[k], rtol=1e-3, atol=2e-5, err_msg=k)
     np.testing.assert_allclose(dp["bpr_epoch_loss"], single["bpr_epoch_loss"], rtol=1e-5)
+
+
+def _case_local(batch):
+    """Trainer diffusion phase + BPR epoch with train_batch_size = batch (UI graphs fixed)."""
+    from test_diffmm_gpu import build_model, tiny_config
+
+    from gmr.dataloader import TrainDataLoader
+    from gmr.dataset import RecDataset
+    from gmr.trainer import DiffMMTrainer, Trainer
+    g = _golden()
+    U, I = int(g["U"]), int(g["I"])
+    cfg = tiny_config(train_batch_size=batch)
+    ds = RecDataset.from_arrays(cfg, g["train_rows"], g["train_cols"], np.zeros(len(g["train_rows"])), U, I,
+                                g["v_feat"], g["t_feat"])
+    tl = TrainDataLoader(cfg, ds, batch_size=batch)
+    torch.manual_seed(999)
+    m = build_model(g)
+    tr = DiffMMTrainer(cfg, m)
+    out = {"dif_steps": np.array([tr.diffusion_phase(0)]), "dif_epoch_loss": tr._dloss.cpu().numpy(),
+           "den_img": m.denoise_model_image.slab.data.cpu().numpy().copy()}
+    rec_loss, _ = Trainer._train_epoch(tr, tl, 0)
+    out["bpr_epoch_loss"] = np.array([rec_loss])
+    out["rec_params"] = m.rec_slab.data.cpu().numpy().copy()
+    return out
+
+
+def _worker_local(rank, world, port, q, batch):
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "generative-multimodal-recommendation_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, pth)
+    os.environ["GMR_DP_MODE"] = "local"
+    import torch.distributed as tdist
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        res = _case_local(batch)
+        if rank == 0:
+            q.put(res)
+        tdist.barrier()
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_dp2_local_batches_equal_double_batch_single_process():
+    """GMR_DP_MODE=local (opt-in, north-star 'partition users'): two ranks taking whole 40-row
+    batches are one process with 80-row batches — same optimiser steps, draws and parameters
+    within the fp32 / Adam tolerances of the global-batch test."""
+    import torch.multiprocessing as mp
+    single = _case_local(80)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_local, args=(r, 2, port, q, 40)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    dp = q.get(timeout=200)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert dp["dif_steps"][0] == single["dif_steps"][0]
+    np.testing.assert_allclose(dp["dif_epoch_loss"], single["dif_epoch_loss"], rtol=1e-5)
+    np.testing.assert_allclose(dp["bpr_epoch_loss"], single["bpr_epoch_loss"], rtol=1e-5)
+    for k in ("den_img", "rec_params"):
+        np.testing.assert_allclose(dp[k], single[k], rtol=1e-3, atol=2e-5, err_msg=k)

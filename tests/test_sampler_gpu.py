@@ -105,7 +105,8 @@ def test_sub_batch_plans_hold_sorted_keys():
     tl = _loader(users, items, U, I, batch=96)
     d = tl.epoch()
     s = d["sample"].cpu().numpy().astype(np.int64)
-    for b, rows, u, p, n, pb, pc in tl.batches(d):
+    for b, rank_rows, u, p, n, pb, pc in tl.batches(d):
+        rows = sum(rank_rows)
         lo = b * 96
         assert rows == min(96, tl.n_inter - lo) and u.numel() == rows
         keys = np.concatenate([s[0, lo:lo + rows], s[1, lo:lo + rows] + U, s[2, lo:lo + rows] + U])
