@@ -118,34 +118,41 @@ __global__ void densify_ones_kernel(int B, const int* __restrict__ users, const 
 }
 
 // EB[t][h] = sum_j emb[t][j] * W1[h][off + j] + b1[h],  emb[t] = emb_W @ temb(t) + emb_b
-__global__ void time_bias_kernel(int T, int E, const float* __restrict__ embW, const float* __restrict__ embB,
-                                 const float* __restrict__ W1, int64_t ldw, int64_t off, const float* __restrict__ b1,
-                                 int H, float* __restrict__ EB, float* __restrict__ temb_out, float* __restrict__ emb_out) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)T * H) return;
-  const int t = (int)(gid / H), h = (int)(gid % H);
-  float te[64], em[64];
+// One block per timestep t: the E-dim sinusoidal embedding and emb_layer(temb) go to LDS once
+// (thread j / i), then EB[t][h] = W1[h, off:off+E] . emb[t] + b1[h] over the block's threads.
+// (one thread per (t, h) recomputing the E x E emb_layer product was 0.43 ms at DiffRec's
+// T = 100, E = 64, H = 300.)
+__global__ void __launch_bounds__(256) time_bias_kernel(int T, int E, const float* __restrict__ embW,
+                                                        const float* __restrict__ embB, const float* __restrict__ W1,
+                                                        int64_t ldw, int64_t off, const float* __restrict__ b1, int H,
+                                                        float* __restrict__ EB, float* __restrict__ temb_out,
+                                                        float* __restrict__ emb_out) {
+  __shared__ float te[64], em[64];
+  const int t = blockIdx.x, tid = threadIdx.x;
   const int half = E / 2;
-  for (int j = 0; j < half; ++j) {
-    float fr = expf(-9.210340371976184f * (float)j / (float)half);  // ln(10000)
-    float a = (float)t * fr;
-    te[j] = cosf(a);
-    te[half + j] = sinf(a);
-  }
-  if (E & 1) te[E - 1] = 0.f;
-  for (int i = 0; i < E; ++i) {
-    float s = 0.f;
-    for (int j = 0; j < E; ++j) s = fmaf(embW[i * E + j], te[j], s);
-    em[i] = s + embB[i];
-  }
-  float acc = 0.f;
-  for (int j = 0; j < E; ++j) acc = fmaf(em[j], W1[(int64_t)h * ldw + off + j], acc);
-  EB[(int64_t)t * H + h] = acc + b1[h];
-  if (h == 0) {
-    for (int j = 0; j < E; ++j) {
-      if (temb_out) temb_out[t * E + j] = te[j];
-      if (emb_out) emb_out[t * E + j] = em[j];
+  if (tid < E) {
+    float v = 0.f;
+    if (tid < 2 * half) {
+      const int j = tid < half ? tid : tid - half;
+      const float a = (float)t * expf(-9.210340371976184f * (float)j / (float)half);  // ln(10000)
+      v = tid < half ? cosf(a) : sinf(a);
     }
+    te[tid] = v;
+    if (temb_out) temb_out[t * E + tid] = v;
+  }
+  __syncthreads();
+  if (tid < E) {
+    float s = 0.f;
+    for (int j = 0; j < E; ++j) s = fmaf(embW[tid * E + j], te[j], s);
+    em[tid] = s + embB[tid];
+    if (emb_out) emb_out[t * E + tid] = s + embB[tid];
+  }
+  __syncthreads();
+  for (int h = tid; h < H; h += blockDim.x) {
+    const float* w = W1 + (int64_t)h * ldw + off;
+    float acc = 0.f;
+    for (int j = 0; j < E; ++j) acc = fmaf(em[j], w[j], acc);
+    EB[(int64_t)t * H + h] = acc + b1[h];
   }
 }
 
@@ -294,36 +301,48 @@ __global__ void __launch_bounds__(256) colsum_grouped_kernel(int64_t rows, int64
 // time-embedding backward from S[t][h] = sum_{b: t_b = t} dpre[b][h]:
 //   dW1[h][off + j] (+)= sum_t S[t][h] emb[t][j] ; db1[h] (+)= sum_t S[t][h]
 //   demb[t][j] = sum_h S[t][h] W1[h][off + j] ; d emb_W[i][j] = sum_t demb[t][i] temb[t][j] ; d emb_b[i] = sum_t demb[t][i]
-__global__ void time_bwd_h_kernel(int T, int E, int H, const float* __restrict__ S, const float* __restrict__ emb,
-                                  float* __restrict__ dW1, int64_t ldw, int64_t off, float* __restrict__ db1,
-                                  int accumulate) {
-  const int h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= H) return;
-  float sb = 0.f;
-  for (int t = 0; t < T; ++t) sb += S[(int64_t)t * H + h];
-  db1[h] = accumulate ? db1[h] + sb : sb;
-  for (int j = 0; j < E; ++j) {
-    float a = 0.f;
-    for (int t = 0; t < T; ++t) a = fmaf(S[(int64_t)t * H + h], emb[t * E + j], a);
-    float* o = dW1 + (int64_t)h * ldw + off + j;
-    *o = accumulate ? *o + a : a;
+// One thread per (h, j) output of dW1 (the j = 0 thread also sums db1[h]); every sum runs over t
+// in order, as before.
+__global__ void __launch_bounds__(256) time_bwd_h_kernel(int T, int E, int H, const float* __restrict__ S,
+                                                         const float* __restrict__ emb, float* __restrict__ dW1,
+                                                         int64_t ldw, int64_t off, float* __restrict__ db1,
+                                                         int accumulate) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= (int64_t)H * E) return;
+  const int h = (int)(o / E), j = (int)(o % E);
+  float a = 0.f;
+  for (int t = 0; t < T; ++t) a = fmaf(S[(int64_t)t * H + h], emb[t * E + j], a);
+  float* d = dW1 + (int64_t)h * ldw + off + j;
+  *d = accumulate ? *d + a : a;
+  if (j == 0) {
+    float sb = 0.f;
+    for (int t = 0; t < T; ++t) sb += S[(int64_t)t * H + h];
+    db1[h] = accumulate ? db1[h] + sb : sb;
   }
 }
 
-// demb[t][i] = sum_h S[t][h] W1[h][off+i] by 16 waves (one output per wave at a time, lanes over h),
-// then d emb_W[i][j] = sum_t demb[t][i] temb[t][j], d emb_b[i] = sum_t demb[t][i]
+// demb[t][i] = sum_h S[t][h] W1[h][off+i] (one thread per (t, i): a wave holds 64 consecutive i of
+// one t, so the W1 reads are coalesced and S[t][h] is a broadcast), then
+// d emb_W[i][j] = sum_t demb[t][i] temb[t][j], d emb_b[i] = sum_t demb[t][i]
 __global__ void __launch_bounds__(1024) time_bwd_e_kernel(int T, int E, int H, const float* __restrict__ S,
                                                           const float* __restrict__ W1, int64_t ldw, int64_t off,
                                                           const float* __restrict__ temb, float* __restrict__ dembW,
                                                           float* __restrict__ dembB, int accumulate) {
   extern __shared__ __attribute__((aligned(16))) float demb[];  // T * E
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int o = w; o < T * E; o += 16) {
+  for (int o = threadIdx.x; o < T * E; o += 1024) {
     const int t = o / E, i = o % E;
-    float a = 0.f;
-    for (int h = lane; h < H; h += 64) a = fmaf(S[(int64_t)t * H + h], W1[(int64_t)h * ldw + off + i], a);
-    a = gmr::wave_sum(a);
-    if (lane == 0) demb[o] = a;
+    const float* srow = S + (int64_t)t * H;
+    const float* wcol = W1 + off + i;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four chains, summed in a fixed order
+    int h = 0;
+    for (; h + 4 <= H; h += 4) {
+      a0 = fmaf(srow[h], wcol[(int64_t)h * ldw], a0);
+      a1 = fmaf(srow[h + 1], wcol[(int64_t)(h + 1) * ldw], a1);
+      a2 = fmaf(srow[h + 2], wcol[(int64_t)(h + 2) * ldw], a2);
+      a3 = fmaf(srow[h + 3], wcol[(int64_t)(h + 3) * ldw], a3);
+    }
+    for (; h < H; ++h) a0 = fmaf(srow[h], wcol[(int64_t)h * ldw], a0);
+    demb[o] = (a0 + a1) + (a2 + a3);
   }
   __syncthreads();
   for (int o = threadIdx.x; o < E * E; o += 1024) {
@@ -391,39 +410,44 @@ __global__ void __launch_bounds__(1024) sample_t_importance_kernel(int B, int T,
 
 // Lt_history / Lt_count update of training_losses (models/diffrec.py:279-286), with the
 // reference's per-sample sequential semantics: the rows of the batch are applied in order
-// (rows with t < 0 are padding and skipped).  Thread i owns timestep i; the batch is scanned
-// backwards through LDS so each thread keeps the latest Hn losses of its timestep.
+// (rows with t < 0 are padding and skipped), so timestep i ends up with the latest Hn losses of
+// its rows.  The batch's t go to LDS; wave w handles timesteps w, w + 16, ...: it scans the batch
+// from the end 64 rows at a time with a ballot and takes the latest matches (at most Hn) from the
+// mask, latest first, into its LDS list; then its lanes write the history.
 __global__ void __launch_bounds__(1024) lt_update_kernel(int B, int T, int Hn, const int* __restrict__ t,
                                                          const double* __restrict__ loss, double* __restrict__ hist,
                                                          int* __restrict__ count) {
-  __shared__ int st[1024];
-  const int i = threadIdx.x;
-  int seen = 0;          // matches found so far (scanning from the end), capped at Hn
-  int keep[16];          // batch rows of the latest min(seen, Hn) matches, latest first
-  for (int end = B; end > 0; end -= 1024) {
-    const int beg = max(0, end - 1024);
-    __syncthreads();
-    if (beg + i < end) st[i] = t[beg + i];
-    __syncthreads();
-    if (i < T && seen < Hn) {  // once Hn matches are known the older rows no longer matter
-      for (int b = end - 1; b >= beg && seen < Hn; --b) {
-        if (st[b - beg] == i) keep[seen++] = b;
+  extern __shared__ int st[];  // B timesteps
+  __shared__ int keep[16][16];
+  for (int b = threadIdx.x; b < B; b += 1024) st[b] = t[b];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = w; i < T; i += 16) {
+    int seen = 0;  // uniform over the wave
+    for (int end = B; end > 0 && seen < Hn; end -= 64) {
+      const int b = end - 64 + lane;
+      const unsigned long long m = __ballot(b >= 0 && st[b] == i);
+      unsigned long long rest = m;
+      while (rest && seen < Hn) {  // latest match first: highest set bit
+        const int bit = 63 - __clzll(rest);
+        if (lane == 0) keep[w][seen] = end - 64 + bit;
+        rest &= ~(1ull << bit);
+        ++seen;
       }
     }
-  }
-  if (i >= T || seen == 0) return;
-  double* h = hist + (int64_t)i * Hn;
-  const int c = count[i];
-  if (c + seen <= Hn && seen < Hn) {  // (seen == Hn may mean more matches: always the shift branch)
-    for (int j = 0; j < seen; ++j) h[c + j] = loss[keep[seen - 1 - j]];
-    count[i] = c + seen;
-  } else {
-    const int kn = min(seen, Hn), ko = Hn - kn;
-    double old[16];
-    for (int j = 0; j < ko; ++j) old[j] = h[c - ko + j];
-    for (int j = 0; j < ko; ++j) h[j] = old[j];
-    for (int j = 0; j < kn; ++j) h[ko + j] = loss[keep[kn - 1 - j]];
-    count[i] = Hn;
+    if (seen == 0) continue;
+    double* h = hist + (int64_t)i * Hn;
+    const int c = count[i];
+    if (c + seen <= Hn && seen < Hn) {  // (seen == Hn may mean more matches: always the shift branch)
+      if (lane < seen) h[c + lane] = loss[keep[w][seen - 1 - lane]];
+      if (lane == 0) count[i] = c + seen;
+    } else {
+      const int kn = min(seen, Hn), ko = Hn - kn;
+      const double old = lane < ko ? h[c - ko + lane] : 0.0;  // all reads before any write
+      if (lane < ko) h[lane] = old;
+      if (lane < kn) h[ko + lane] = loss[keep[w][kn - 1 - lane]];
+      if (lane == 0) count[i] = Hn;
+    }
   }
 }
 
@@ -493,8 +517,9 @@ extern "C" int gmr_diff_history_update(int32_t B, int32_t T, int32_t hist_len, c
                                        double* hist, int32_t* count, void* stream) {
   GMR_ARG(t && loss && hist && count && B > 0 && T > 0 && T <= 1024, "bad args (T <= 1024)");
   GMR_ARG(hist_len >= 1 && hist_len <= 16, "history length must be 1..16");
-  hipLaunchKernelGGL(lt_update_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, T, hist_len, t, loss, hist,
-                     count);
+  GMR_ARG((size_t)B * sizeof(int) <= 65536, "batch too large for the LDS copy of t (B <= 16384)");
+  hipLaunchKernelGGL(lt_update_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)B, (hipStream_t)stream, B, T,
+                     hist_len, t, loss, hist, count);
   GMR_LAUNCHED();
   return GMR_OK;
 }
@@ -555,7 +580,7 @@ extern "C" int gmr_diff_time_bias(int32_t T, int32_t E, const float* emb_W, cons
                                   float* temb_out, float* emb_out, void* stream) {
   GMR_ARG(emb_W && emb_b && W1 && b1 && EB && T > 0 && H > 0, "bad args");
   GMR_ARG(E >= 1 && E <= 64, "time embedding size must be 1..64");
-  hipLaunchKernelGGL(time_bias_kernel, dim3(gmr::grid_for((int64_t)T * H, 128)), dim3(128), 0, (hipStream_t)stream, T, E,
+  hipLaunchKernelGGL(time_bias_kernel, dim3((unsigned)T), dim3(256), 0, (hipStream_t)stream, T, E,
                      emb_W, emb_b, W1, ld_w1, col_off, b1, H, EB, temb_out, emb_out);
   GMR_LAUNCHED();
   return GMR_OK;
@@ -608,7 +633,8 @@ extern "C" int gmr_diff_time_bwd(int32_t T, int32_t E, int32_t H, const float* S
   GMR_ARG(S && temb && emb && W1 && dW1 && db1 && d_emb_W && d_emb_b && T > 0 && H > 0, "bad args");
   GMR_ARG(E >= 1 && E <= 64, "time embedding size must be 1..64");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(time_bwd_h_kernel, dim3(gmr::grid_for(H, 256)), dim3(256), 0, st, T, E, H, S, emb, dW1, ld_w1,
+  hipLaunchKernelGGL(time_bwd_h_kernel, dim3(gmr::grid_for((int64_t)H * E, 256)), dim3(256), 0, st, T, E, H, S, emb, dW1,
+                     ld_w1,
                      col_off, db1, accumulate);
   GMR_LAUNCHED();
   GMR_ARG((size_t)T * E * sizeof(float) <= 60000, "T * E too large for the LDS staging");
