@@ -766,23 +766,6 @@ __device__ __forceinline__ void cl_store(const float4 (&st)[2], float* dst) {
     st4(dst + (idx >> 4) * kClLd + (idx & 15) * 4, st[q]);
   }
 }
-// 32 x 32 dot tile: rows = the staged block (A operand), columns = the lane's register fragment (B)
-__device__ __forceinline__ clx16 cl_dot(const float* blk, const float4 (&fr)[2][4], int l32, int h) {
-  clx16 s;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) s[e] = 0.f;
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 a = ld4(blk + l32 * kClLd + 32 * u + 16 * h + 4 * q);
-      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, fr[u][q].x, s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, fr[u][q].y, s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, fr[u][q].z, s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, fr[u][q].w, s, 0, 0, 0);
-    }
-  return s;
-}
 // the lane's A operands of cl_acc, read from LDS ahead of the exp phase (issued together, so the
 // MFMA chain of cl_acc does not wait on one LDS round trip per step)
 __device__ __forceinline__ void cl_acc_load(const float* blk, float (&a0)[16], float (&a1)[16], int l32, int h) {
@@ -795,13 +778,39 @@ __device__ __forceinline__ void cl_acc_load(const float* blk, float (&a0)[16], f
   __builtin_amdgcn_sched_barrier(0);  // keep the reads here: hipcc otherwise sinks each next to its MFMA
 }
 // y^T (64 x 32) += blk^T (64 x 32) X, X (32 x 32) in the accumulator registers (row (e&3)+8(e>>2)+4h)
-__device__ __forceinline__ void cl_acc(const float (&a0)[16], const float (&a1)[16], const clx16& X, clx16& y0,
-                                       clx16& y1) {
+// NF fragments against one staged block: each A read from LDS feeds NF independent MFMA chains
+template <int NF>
+__device__ __forceinline__ void cl_dot_n(clx16 (&s)[NF], const float* blk, const float4 (&fr)[NF][2][4], int l32,
+                                         int h) {
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], X[e], y0, 0, 0, 0);
-    y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], X[e], y1, 0, 0, 0);
-  }
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s[f][e] = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 a = ld4(blk + l32 * kClLd + 32 * u + 16 * h + 4 * q);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) s[f] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, fr[f][u][q].x, s[f], 0, 0, 0);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) s[f] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, fr[f][u][q].y, s[f], 0, 0, 0);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) s[f] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, fr[f][u][q].z, s[f], 0, 0, 0);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) s[f] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, fr[f][u][q].w, s[f], 0, 0, 0);
+    }
+}
+template <int NF>
+__device__ __forceinline__ void cl_acc_n(const float (&a0)[16], const float (&a1)[16], const clx16 (&X)[NF],
+                                         clx16 (&y0)[NF], clx16 (&y1)[NF]) {
+#pragma unroll
+  for (int e = 0; e < 16; ++e)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      y0[f] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], X[f][e], y0[f], 0, 0, 0);
+      y1[f] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], X[f][e], y1[f], 0, 0, 0);
+    }
 }
 // the lane's 64-float column of y^T: registers 4g .. 4g+3 hold d = 8g + 4h + 0..3 (+32 in y1)
 __device__ __forceinline__ void cl_put(float* dst, const clx16& y0, const clx16& y1, int h) {
@@ -828,20 +837,26 @@ __device__ __forceinline__ float cl_exp(float inv_t, float x) {
   return expf(inv_t * x);
 }
 
-template <bool FAST>
+template <bool FAST, int NF>
 __global__ void __launch_bounds__(256, 2) cl_rows_kernel(int B, int n, const float* __restrict__ P, int64_t ldp,
                                                       const float* __restrict__ T, int64_t ldt, float inv_t, int chunk,
                                                       float* __restrict__ part_u, float* __restrict__ part_z) {
   __shared__ __attribute__((aligned(16))) float s_blk[2][32 * kClLd];
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-  const int i = blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + l32;  // the lane's row (a column of S^T)
+  // the lane's rows (columns of S^T): NF fragments of 32 rows per wave
+  const int i0r = blockIdx.x * 128 * NF + (threadIdx.x >> 6) * 32 * NF + l32;
   const int c = blockIdx.y, j0 = c * chunk, j1 = min(n, j0 + chunk);
-  float4 fr[2][4];
-  cl_frag(fr, P, ldp, i, B, h);
-  clx16 y0, y1;
+  float4 fr[NF][2][4];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) y0[e] = y1[e] = 0.f;
-  float z = 0.f;
+  for (int f = 0; f < NF; ++f) cl_frag(fr[f], P, ldp, i0r + 32 * f, B, h);
+  clx16 y0[NF], y1[NF];
+  float z[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    z[f] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) y0[f][e] = y1[f][e] = 0.f;
+  }
   float4 st[2];
   cl_load(st, T, ldt, j0, j1);
   cl_store(st, s_blk[0]);
@@ -851,24 +866,31 @@ __global__ void __launch_bounds__(256, 2) cl_rows_kernel(int B, int n, const flo
     const bool more = j + 32 < j1;
     if (more) cl_load(st, T, ldt, j + 32, j1);
     const float* blk = s_blk[cur];
-    clx16 s = cl_dot(blk, fr, l32, h);
+    clx16 s[NF];
+    cl_dot_n<NF>(s, blk, fr, l32, h);
     float a0[16], a1[16];
     cl_acc_load(blk, a0, a1, l32, h);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int r = (e & 3) + 8 * (e >> 2) + 4 * h;
-      s[e] = j + r < j1 ? cl_exp<FAST>(inv_t, s[e]) : 0.f;
-      z += s[e];
-    }
-    cl_acc(a0, a1, s, y0, y1);
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = (e & 3) + 8 * (e >> 2) + 4 * h;
+        s[f][e] = j + r < j1 ? cl_exp<FAST>(inv_t, s[f][e]) : 0.f;
+        z[f] += s[f][e];
+      }
+    cl_acc_n<NF>(a0, a1, s, y0, y1);
     if (more) cl_store(st, s_blk[cur ^ 1]);
     __syncthreads();
     cur ^= 1;
   }
-  z += __shfl_xor(z, 32);
-  if (i < B) {
-    cl_put(part_u + ((int64_t)c * B + i) * 64, y0, y1, h);
-    if (h == 0) part_z[(int64_t)c * B + i] = z;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int i = i0r + 32 * f;
+    const float zf = z[f] + __shfl_xor(z[f], 32);
+    if (i < B) {
+      cl_put(part_u + ((int64_t)c * B + i) * 64, y0[f], y1[f], h);
+      if (h == 0) part_z[(int64_t)c * B + i] = zf;
+    }
   }
 }
 
@@ -913,20 +935,23 @@ __global__ void __launch_bounds__(256) cl_finalize_kernel(int B, int nc, const f
   }
 }
 
-template <bool FAST>
+template <bool FAST, int NF>
 __global__ void __launch_bounds__(256, 2) cl_table_kernel(int B, int n, const float* __restrict__ P, int64_t ldp,
                                                        const float* __restrict__ r, const float* __restrict__ T,
                                                        int64_t ldt, float inv_t, int chunk, float* __restrict__ part_t) {
   __shared__ __attribute__((aligned(16))) float s_blk[2][32 * kClLd];
   __shared__ float s_r[2][32];
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-  const int j = blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + l32;  // the lane's table row
+  const int j0r = blockIdx.x * 128 * NF + (threadIdx.x >> 6) * 32 * NF + l32;  // the lane's table rows
   const int c = blockIdx.y, i0 = c * chunk, i1 = min(B, i0 + chunk);
-  float4 fr[2][4];
-  cl_frag(fr, T, ldt, j, n, h);
-  clx16 y0, y1;
+  float4 fr[NF][2][4];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) y0[e] = y1[e] = 0.f;
+  for (int f = 0; f < NF; ++f) cl_frag(fr[f], T, ldt, j0r + 32 * f, n, h);
+  clx16 y0[NF], y1[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) y0[f][e] = y1[f][e] = 0.f;
   float4 st[2];
   float sr = 0.f;
   cl_load(st, P, ldp, i0, i1);
@@ -942,12 +967,17 @@ __global__ void __launch_bounds__(256, 2) cl_table_kernel(int B, int n, const fl
       if (threadIdx.x < 32) sr = i + 32 + (int)threadIdx.x < i1 ? r[i + 32 + threadIdx.x] : 0.f;
     }
     const float* blk = s_blk[cur];
-    clx16 s = cl_dot(blk, fr, l32, h);  // S' (rows i of the block x the wave's 32 table rows)
+    clx16 s[NF];
+    cl_dot_n<NF>(s, blk, fr, l32, h);  // S' (rows i of the block x the wave's table rows)
     float a0[16], a1[16];
     cl_acc_load(blk, a0, a1, l32, h);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) s[e] = s_r[cur][(e & 3) + 8 * (e >> 2) + 4 * h] * cl_exp<FAST>(inv_t, s[e]);
-    cl_acc(a0, a1, s, y0, y1);  // dT^T += P_blk^T (r E)
+    for (int e = 0; e < 16; ++e) {
+      const float re = s_r[cur][(e & 3) + 8 * (e >> 2) + 4 * h];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) s[f][e] = re * cl_exp<FAST>(inv_t, s[f][e]);
+    }
+    cl_acc_n<NF>(a0, a1, s, y0, y1);  // dT^T += P_blk^T (r E)
     if (more) {
       cl_store(st, s_blk[cur ^ 1]);
       if (threadIdx.x < 32) s_r[cur ^ 1][threadIdx.x] = sr;
@@ -955,7 +985,11 @@ __global__ void __launch_bounds__(256, 2) cl_table_kernel(int B, int n, const fl
     __syncthreads();
     cur ^= 1;
   }
-  if (j < n) cl_put(part_t + ((int64_t)c * n + j) * 64, y0, y1, h);
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int j = j0r + 32 * f;
+    if (j < n) cl_put(part_t + ((int64_t)c * n + j) * 64, y0[f], y1[f], h);
+  }
 }
 
 __global__ void cl_table_reduce_kernel(int n, int nc, const float* __restrict__ part_t, float* __restrict__ dT,
@@ -980,6 +1014,12 @@ __global__ void cl_table_reduce_kernel(int n, int nc, const float* __restrict__ 
 struct ClPlan {
   int nca, chunk_a, ncb, chunk_b;
 };
+// fragments of 32 rows per wave (GMR_CL_NF = 2: each staged block feeds two independent MFMA
+// chains per wave and half the workgroups; the chunking, and so every sum, is the same for 1 and 2)
+int cl_nf() {  // read per call (a getenv), so a test can compare both in one process
+  const char* e = getenv("GMR_CL_NF");
+  return (e && atoi(e) == 2) ? 2 : 1;
+}
 // workgroups per pass (GMR_CL_WG_ROWS / GMR_CL_WG_TABLE override, for tuning)
 int cl_wg_target(const char* env, int dflt) {
   const char* s = getenv(env);
@@ -1029,22 +1069,19 @@ extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int6
     const char* e = getenv("GMR_CL_FASTEXP");
     return !(e && atoi(e) == 0);
   }();
-  if (fast)
-    hipLaunchKernelGGL(cl_rows_kernel<true>, dim3((unsigned)((B + 127) / 128), (unsigned)p.nca), dim3(256), 0, st, B,
-                       (int)n, P, ldp, T, ldt, inv_temp, p.chunk_a, part_u, part_z);
-  else
-    hipLaunchKernelGGL(cl_rows_kernel<false>, dim3((unsigned)((B + 127) / 128), (unsigned)p.nca), dim3(256), 0, st, B,
-                       (int)n, P, ldp, T, ldt, inv_temp, p.chunk_a, part_u, part_z);
+  const int nf = cl_nf();
+  const dim3 ga((unsigned)((B + 128 * nf - 1) / (128 * nf)), (unsigned)p.nca);
+  const dim3 gb((unsigned)((n + 128 * nf - 1) / (128 * nf)), (unsigned)p.ncb);
+  auto rows = fast ? (nf == 2 ? cl_rows_kernel<true, 2> : cl_rows_kernel<true, 1>)
+                   : (nf == 2 ? cl_rows_kernel<false, 2> : cl_rows_kernel<false, 1>);
+  hipLaunchKernelGGL(rows, ga, dim3(256), 0, st, B, (int)n, P, ldp, T, ldt, inv_temp, p.chunk_a, part_u, part_z);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(cl_finalize_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, p.nca, part_u, part_z, CLN,
                      nodes, node_off, inv_temp, coef, loss, contrib, ld_contrib, r);
   GMR_LAUNCHED();
-  if (fast)
-    hipLaunchKernelGGL(cl_table_kernel<true>, dim3((unsigned)((n + 127) / 128), (unsigned)p.ncb), dim3(256), 0, st, B,
-                       (int)n, P, ldp, r, T, ldt, inv_temp, p.chunk_b, part_t);
-  else
-    hipLaunchKernelGGL(cl_table_kernel<false>, dim3((unsigned)((n + 127) / 128), (unsigned)p.ncb), dim3(256), 0, st, B,
-                       (int)n, P, ldp, r, T, ldt, inv_temp, p.chunk_b, part_t);
+  auto table = fast ? (nf == 2 ? cl_table_kernel<true, 2> : cl_table_kernel<true, 1>)
+                    : (nf == 2 ? cl_table_kernel<false, 2> : cl_table_kernel<false, 1>);
+  hipLaunchKernelGGL(table, gb, dim3(256), 0, st, B, (int)n, P, ldp, r, T, ldt, inv_temp, p.chunk_b, part_t);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(cl_table_reduce_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n, p.ncb, part_t,
                      dT, ld_dt);

@@ -251,6 +251,20 @@ __device__ __forceinline__ void gemm_epilogue(const AccT (&acc)[BM / WGM / MF][B
     }
 }
 
+// (tile row, tile column) of linear tile `tile`; tn_packed = tiles_n | group << 20 (tile_group())
+__device__ __forceinline__ void tile_mn(int tile, int tn_packed, int tiles_m, int& tmi, int& tni) {
+  const int tiles_n = tn_packed & 0xFFFFF, G = tn_packed >> 20;
+  if (G <= 1) {
+    tmi = tile / tiles_n;
+    tni = tile - tmi * tiles_n;
+    return;
+  }
+  const int per = G * tiles_n, g = tile / per, first = g * G;
+  const int gs = min(tiles_m - first, G), rem = tile - g * per;
+  tni = rem / gs;
+  tmi = first + rem - tni * gs;
+}
+
 template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, bool VEC, int MF>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t N, int64_t K,
                                                              const float* __restrict__ A, int64_t lda,
@@ -272,8 +286,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_kernel(int64_t M, int64_t
   const int b = blockIdx.x;
   const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
   const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-  const int64_t m0 = (int64_t)(tile / tiles_n) * BM;
-  const int64_t n0 = (int64_t)(tile % tiles_n) * BN;
+  int tmi, tni;
+  tile_mn(tile, tiles_n, (int)((M + BM - 1) / BM), tmi, tni);
+  const int64_t m0 = (int64_t)tmi * BM;
+  const int64_t n0 = (int64_t)tni * BN;
   const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
   const int64_t kend = min(K, kbeg + k_per_split);
 
@@ -619,8 +635,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_glds_kernel(int64_t M, in
   const int b = blockIdx.x;
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int64_t m0 = (int64_t)(tile / tiles_n) * BM;
-  const int64_t n0 = (int64_t)(tile % tiles_n) * BN;
+  int tmi, tni;
+  tile_mn(tile, tiles_n, (int)((M + BM - 1) / BM), tmi, tni);
+  const int64_t m0 = (int64_t)tmi * BM;
+  const int64_t n0 = (int64_t)tni * BN;
   const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
   const int64_t kend = min(K, kbeg + k_per_split);
   const int nk = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;  // k tiles; only the last may be partial
@@ -717,6 +735,18 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const flo
   }
   for (; z < splits; ++z) s += ws[(int64_t)z * slab + idx];
   C[m * ldc + n] = epi_apply(epi, s, m, n, C, ldc);
+}
+
+// tile order inside each XCD's contiguous range: GMR_GEMM_GROUP = G > 1 walks G tile rows per
+// column (the workgroups resident on one XCD then share G A-panels and ~resident/G B-panels of
+// each k slab in its L2 instead of one A-panel and ~resident B-panels); 0/1 = row-major
+int tile_group() {
+  static const int g = [] {
+    const char* e = getenv("GMR_GEMM_GROUP");
+    const int v = e ? atoi(e) : 0;
+    return v < 0 ? 0 : (v > 64 ? 64 : v);
+  }();
+  return g;
 }
 
 bool inkernel_fixup() {
@@ -965,21 +995,22 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   }
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)(tm * tn), 1, (unsigned)splits);
+  const int tnp = (int)tn | (tile_group() << 20);
   switch (tile) {
     case 256:
-      launch_tile<256, 256, 4, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws, counters);
+      launch_tile<256, 256, 4, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
       break;
     case 256128:
-      launch_tile<256, 128, 4, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws, counters);
+      launch_tile<256, 128, 4, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
       break;
     case 128256:
-      launch_tile<128, 256, 2, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws, counters);
+      launch_tile<128, 256, 2, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
       break;
     case 128:
-      launch_tile<128, 128, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws, counters);
+      launch_tile<128, 128, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
       break;
     default:
-      launch_tile<64, 64, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, (int)tn, kps, ws, counters);
+      launch_tile<64, 64, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
   }
   GMR_LAUNCHED();
   if (ws && !counters) {

@@ -185,8 +185,10 @@ int gmr_topk_to_user_csr(int64_t n_users, int32_t k, const int32_t* topk, int64_
  * split_k: 0 auto, else >= 1.
  * gmr_gemm_workspace_floats returns the exact scratch the same call needs (GMR_GEMM_COUNTER_WORDS
  * tile counters + splits*M*N floats of split-K partials, 0 when it does not split); the counter
- * words must be zero before the first call (they are left zero).  With glds staging the slices of
- * a tile are summed in-launch by the last one to finish (same slab order as the reduce pass). */
+ * words must be zero before the first call (they are left zero).  The split slabs are summed in
+ * slab order by a reduce pass; the environment switch GMR_GEMM_FIXUP=1 instead has the last slice
+ * of each tile sum them in-launch (same order and bits; slower on gfx950).
+ * GMR_GEMM_GROUP=G (tuning) walks G tile rows per column inside each XCD's tile range. */
 int64_t gmr_gemm_workspace_floats(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, int32_t tile,
                                   int32_t split_k);
 int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,

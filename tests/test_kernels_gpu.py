@@ -427,6 +427,30 @@ def test_contrast_fused_vs_fp64(K, B, n):
     assert np.isnan(dbuf[:off].cpu().numpy()).all() and np.isnan(dbuf[off:off + n, :64].cpu().numpy()).all()
 
 
+@pytest.mark.parametrize("B,n", [(2048, 19445), (300, 7050), (37, 100)])
+def test_contrast_two_fragments_bit_exact(K, B, n, monkeypatch):
+    """GMR_CL_NF=2 (two 32-row fragments per wave, half the workgroups) keeps the chunking, so the
+    loss, dP and dT are the one-fragment kernels' bit for bit (ragged B and n included)."""
+    rng = _rng(12)
+    C = rng.standard_normal((n, 128)).astype(np.float32)
+    C /= np.linalg.norm(C, axis=1, keepdims=True)
+    nodes = rng.integers(0, n, B).astype(np.int32)
+    Cd, nd = _dev(C), _dev(nodes)
+    P = torch.empty((B, 64), device=DEV)
+    K.gather_rows(Cd[:, :64], nd, P, off=0)
+    ws = K.contrast_workspace(B, n, DEV, "test_cl_nf")
+    outs = []
+    for nf in ("1", "2"):
+        monkeypatch.setenv("GMR_CL_NF", nf)
+        loss = torch.empty(B, device=DEV)
+        contrib = torch.empty((B, 128), device=DEV)
+        dt = torch.empty((n, 128), device=DEV)
+        K.contrast_fused(P, Cd[:, 64:], Cd, nd, 0, 10.0, 0.01 / B, loss, contrib, dt[:, 64:], ws)
+        outs.append((loss.cpu(), contrib.cpu(), dt[:, 64:].cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("nb", [1, 2, 4])
 def test_spmm_chunk_rows_spanning_groups(K, nb):
     """Chunk plan: rows of degree 1..128 packed into 128-entry tasks, many of them crossing the
