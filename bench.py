@@ -49,7 +49,13 @@ STEP_DESC = {"diffmm": "one DiffMMTrainer epoch (diffusion train + graph rebuild
                         "importance-sampled t)"}
 HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFS = 157.3
+# split-bf16 GEMM (gemm_x6_kernel): six v_mfma_f32_32x32x16_bf16 products per fp32 product, so its
+# instruction roofline in fp32-equivalent flop/s is the dense bf16 MFMA peak (256 CUs x 4 SIMDs x
+# 1,024 flop/clk x 2.4 GHz = 2,516.6 TF/s, MI355X_MICROARCH.md) / 6
+X6_PEAK_TFS = round(2516.6 / 6, 1)
 KERNEL_NAMES = {"gemm": "gemm_glds_kernel (fp32 MFMA v_mfma_f32_32x32x2_f32, global_load_lds staging, XCD-aware tiles)",
+                "gemm_x6": "gemm_x6_kernel (fp32 operands split exactly into three bf16 terms, six "
+                           "v_mfma_f32_32x32x16_bf16 products accumulated in fp32: fp32-accurate NT products)",
                 "infonce": "cl_rows_kernel + cl_table_kernel (fused InfoNCE, fp32 MFMA)",
                 "spmm": "spmm_lane_kernel / spmm_lane_jobs_kernel (CSR lane plan, XCD column slices, lane group per "
                         "row, multi-job launches)"}
@@ -125,8 +131,8 @@ def summarize_probe(p, model="diffmm", shape=None):
             continue
         ms = [s.elapsed_time(e) for s, e, _ in recs]
         tot_ms = float(np.sum(ms))
-        if tag in ("gemm", "infonce"):
-            if tag == "gemm":
+        if tag in ("gemm", "gemm_x6", "infonce"):
+            if tag in ("gemm", "gemm_x6"):
                 work = sum(2.0 * r[2][0] * r[2][1] * r[2][2] for r in recs)
                 # operands read once + C written once (+ read for the in-place / aux epilogues)
                 x_epi = (4, 5, 6, 8)  # POSTERIOR, DTANH, ROWSCALE_AUX, DRELU (include/gmr.h)
@@ -135,13 +141,18 @@ def summarize_probe(p, model="diffmm", shape=None):
             else:  # rows pass S = P T^T and U = E T, table pass the same again: 4 B n 64 MACs
                 work = sum(8.0 * r[2][0] * r[2][1] * 64 for r in recs)
             achieved = work / (tot_ms * 1e-3) / 1e12
-            out[tag] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                        "frac": round(achieved / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
+            peak = X6_PEAK_TFS if tag == "gemm_x6" else FP32_MFMA_PEAK_TFS
+            out[tag] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                        "frac": round(achieved / peak, 4), "traffic": None,
                         "launches": len(recs), "avg_us": round(1e3 * tot_ms / len(recs), 2),
                         "total_ms": round(tot_ms, 3), "algorithmic_per_launch": work / len(recs),
                         "algorithmic_unit": "flop", "kernel": KERNEL_NAMES[tag]}
-            if tag == "gemm":
+            if tag in ("gemm", "gemm_x6"):
                 out[tag]["algorithmic_bytes_per_launch"] = round(alg_bytes / len(recs))
+            if tag == "gemm_x6":
+                out[tag]["peak_note"] = ("fp32-equivalent flop (2MNK) vs the split kernel's instruction roofline: "
+                                         "dense bf16 MFMA peak 2516.6 TF/s / 6 products; "
+                                         f"{achieved / FP32_MFMA_PEAK_TFS:.3f} of the fp32-input MFMA peak")
         else:
             # bytes = 8 nnz + 4 (n_rows+1) + 4 d n_cols (X once) + 4 d n_rows (Y once [+ read if beta])
             # (a multi-job launch, key ("jobs", job, ...), moves the sum of its jobs' bytes)
@@ -299,7 +310,7 @@ def run_workload(args, dist_on, barrier, max_over_ranks, with_cpu_baseline):
         # one more epoch, side streams off, every GEMM / SpMM / InfoNCE launch timed on its stream
         serial = K.Streams.SERIAL
         K.Streams.SERIAL = True
-        K.probe_begin(["gemm", "spmm", "infonce"])
+        K.probe_begin(["gemm", "gemm_x6", "spmm", "infonce"])
         t1 = time.time()
         trainer._train_epoch(tl, args.warmup + args.steps)
         torch.cuda.synchronize()
@@ -310,6 +321,8 @@ def run_workload(args, dist_on, barrier, max_over_ranks, with_cpu_baseline):
         if os.environ.get("GMR_PROBE_REPORT"):
             report_shapes(raw)
         mfma_flop = sum(o["algorithmic_per_launch"] * o["launches"] for o in roof.values() if o["bound"] == "mfma")
+        if os.environ.get("GMR_GEMM_X6", "1") != "0" and "gemm_x6" not in roof and args.model == "diffmm":
+            log("note: no split-bf16 GEMM launch in the probed epoch")
         for o in roof.values():
             o["probe_scope"] = ("one extra epoch after the timed region with the side streams off (GMR_SERIAL): "
                                 "HIP events around every launch of the class on its stream")
@@ -404,6 +417,21 @@ def main():
             dp_local = {"error": repr(e)}
         finally:
             os.environ.pop("GMR_DP_MODE", None)
+    # the same headline epoch with every GEMM on the fp32-input MFMA (GMR_GEMM_X6=0, read once by the
+    # library, so a child process), reported beside the value for comparison
+    fp32_only = None
+    if legs and world == 1 and os.environ.get("GMR_GEMM_X6", "1") != "0":
+        import subprocess
+        env = dict(os.environ, GMR_GEMM_X6="0")
+        cmd = [sys.executable, os.path.abspath(__file__), "--model", "diffmm", "--no-legs", "--no-cpu-baseline",
+               "--no-probe", "--steps", str(args.steps), "--warmup", str(args.warmup), "--eval-passes", "1"]
+        try:
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+            j = json.loads(r.stdout.strip().splitlines()[-1])
+            fp32_only = {"value": j["value"], "unit": "users/s", "ms_per_step": j["ms_per_step"],
+                         "eval_recall@20": j["eval_recall@20"], "note": "same epoch, GMR_GEMM_X6=0 (child process)"}
+        except Exception as e:  # noqa: BLE001
+            fp32_only = {"error": repr(e)}
     leg_out = {}
     if legs:
         for key, m, shape, sd in (("diffrec", "diffrec", "baby", None), ("genrecv1_fp16", "genrecv1", "tiktok", "fp16")):
@@ -437,6 +465,14 @@ def main():
             "roofline": dobj, "dominant_kernel": dn, "roofline_by_kernel": roof,
             "lib_sha256": lib_sha256(),
         }
+        line["gemm_arith"] = (
+            "fp32 operands and results; NT products (denoiser forward, p_sample) on the split-bf16 kernel: each fp32 "
+            "operand split exactly into three bf16 terms, six bf16 MFMA products accumulated in fp32 (error vs fp64 "
+            "within the fp32-input MFMA kernel's, tests/test_kernels_gpu.py::test_gemm_x6_fp32_accuracy); the other "
+            "products on the fp32-input MFMA" if os.environ.get("GMR_GEMM_X6", "1") != "0" else
+            "every product on the fp32-input MFMA (GMR_GEMM_X6=0)")
+        if fp32_only:
+            line["fp32_mfma_only"] = fp32_only
         if "cpu_baseline" in head:
             line["cpu_baseline"] = head["cpu_baseline"]
         if leg_out:

@@ -53,6 +53,7 @@ SIGNATURES = {
     "gmr_bipartite_symnorm_build": (I32, [I64, I64, P, P, I64, I32, F64, P, P, P, P, P]),
     "gmr_topk_to_user_csr": (I32, [I64, I32, P, I64, P, P, P]),
     "gmr_gemm_workspace_floats": (I64, [I32, I32, I64, I64, I64, I32, I32]),
+    "gmr_gemm_kernel_kind": (I32, [I32, I32, I64, I64, I64, I32, I32, I32]),
     "gmr_gemm_f32": (I32, [I32, I32, I64, I64, I64, F32, P, I64, P, I64, F32, P, I64, I32, P, P, I64, P, I64, P, P,
                            F32, I32, I32, P, I64, P]),
     "gmr_dmm_combine_fwd": (I32, [I64, P, P, P, P, P, F32, P, P]),

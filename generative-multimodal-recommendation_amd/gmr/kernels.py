@@ -202,6 +202,20 @@ def zero_(t):
 
 
 # ----------------------------------------------------------------------------- GEMM
+_gemm_kinds = {}
+
+
+def _gemm_tag(A, B, trans_a, trans_b, M, N, K, tile, split_k):
+    """Probe class of a GEMM launch: "gemm_x6" when the plan takes the split-bf16 kernel
+    (gmr_gemm_kernel_kind == 6), else "gemm" (fp32-input MFMA)."""
+    aligned = int(A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0 and _ld(A) % 4 == 0 and _ld(B) % 4 == 0)
+    key = (int(trans_a), int(trans_b), M, N, K, tile, split_k, aligned)
+    kind = _gemm_kinds.get(key)
+    if kind is None:
+        kind = _gemm_kinds[key] = int(_lib.load().gmr_gemm_kernel_kind(*key))
+    return "gemm_x6" if kind == 6 else "gemm"
+
+
 def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NONE, bias=None, bias_row=None,
          ld_bias=0, aux=None, rv1=None, rv2=None, slope=0.0, tile=0, split_k=0):
     """C = epi(alpha * op(A) @ op(B) ...), see include/gmr.h gmr_gemm_f32."""
@@ -216,7 +230,8 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
             raise TypeError("gemm is fp32")
     need = _lib.load().gmr_gemm_workspace_floats(int(trans_a), int(trans_b), M, N, K, tile, split_k)
     ws = workspace(need, C.device) if need > 0 else None  # split-K partials only when this call splits
-    with _Probe("gemm", (M, N, K, int(trans_a), int(trans_b), epi)):
+    with _Probe(_gemm_tag(A, B, trans_a, trans_b, M, N, K, tile, split_k) if _probe is not None else "gemm",
+                (M, N, K, int(trans_a), int(trans_b), epi)):
         _lib.call("gmr_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), ptr(A), _ld(A), ptr(B), _ld(B),
                   float(beta), ptr(C), _ld(C), epi, ptr(bias), ptr(bias_row), ld_bias, ptr(aux),
                   _ld(aux) if aux is not None else 0, ptr(rv1), ptr(rv2), float(slope), tile, split_k, ptr(ws),

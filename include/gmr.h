@@ -45,6 +45,8 @@ extern "C" {
 #define GMR_GEMM_REGSTAGE (1 << 23)  /* tile flag: stage operands through registers + ds_write */
 #define GMR_GEMM_MFMA16 (1 << 24)
 #define GMR_GEMM_MFMA32 (1 << 25)
+#define GMR_GEMM_X6 (1 << 26)        /* tile flag: split-bf16 operands on the bf16 MFMA (six products, fp32-accurate) */
+#define GMR_GEMM_F32 (1 << 27)       /* tile flag: force the fp32-input MFMA (overrides GMR_GEMM_X6=1 in the environment) */
 #define GMR_EPI_DRELU 8        /* C = aux[m,n] > 0 ? alpha*acc : 0  ReLU (+ dropout) backward  */
 
 const char* gmr_last_error_string(void);
@@ -175,7 +177,7 @@ int gmr_bipartite_symnorm_build(int64_t n_users, int64_t n_items, const int32_t*
 int gmr_topk_to_user_csr(int64_t n_users, int32_t k, const int32_t* topk, int64_t ld, int32_t* user_ptr,
                          int32_t* user_items, void* stream);
 
-/* ---------------------------------------------------------------- K3/K4/K6/K9 dense GEMM (fp32 MFMA)
+/* ---------------------------------------------------------------- K3/K4/K6/K9 dense GEMM (fp32 operands)
  * C[M,N] = epilogue(alpha * op(A) op(B)); op(A) = A (M x K, lda) or A^T (A stored K x M);
  * op(B) = B (K x N, ldb) or B^T (B stored N x K).  bias[(bias_row ? bias_row[m] : 0)*ld_bias + n].
  * Replaces nn.Linear / torch.mm / matmul: diffmm.py:117,124,277,352-358,472-473; vbpr.py:70,105.
@@ -188,7 +190,16 @@ int gmr_topk_to_user_csr(int64_t n_users, int32_t k, const int32_t* topk, int64_
  * words must be zero before the first call (they are left zero).  The split slabs are summed in
  * slab order by a reduce pass; the environment switch GMR_GEMM_FIXUP=1 instead has the last slice
  * of each tile sum them in-launch (same order and bits; slower on gfx950).
- * GMR_GEMM_GROUP=G (tuning) walks G tile rows per column inside each XCD's tile range. */
+ * GMR_GEMM_GROUP=G (tuning) walks G tile rows per column inside each XCD's tile range.
+ * Split-bf16 products (gemm_x6.hip): NT calls (trans_a = 0, trans_b = 1) with 16-byte aligned A / B and
+ * lda, ldb multiples of 4 on a >= 128^2 tile run on the bf16 matrix cores with every fp32 operand split
+ * exactly into three bf16 terms and six products accumulated in fp32 (fp32-accurate: error vs fp64 within
+ * the fp32-MFMA kernel's bound, tests/test_kernels_gpu.py); | GMR_GEMM_X6 forces it, | GMR_GEMM_F32 (or
+ * any staging / MFMA-shape flag) keeps the fp32-input MFMA, and the environment variable GMR_GEMM_X6=0
+ * turns it off for every call.  gmr_gemm_kernel_kind returns the matrix path a call with these
+ * arguments takes: 6 (split-bf16), 32 (v_mfma_f32_32x32x2_f32) or 16 (v_mfma_f32_16x16x4_f32). */
+int32_t gmr_gemm_kernel_kind(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, int32_t tile,
+                             int32_t split_k, int32_t aligned);
 int64_t gmr_gemm_workspace_floats(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, int32_t tile,
                                   int32_t split_k);
 int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,

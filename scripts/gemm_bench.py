@@ -13,7 +13,7 @@ import torch  # noqa: E402
 
 from gmr import kernels as K  # noqa: E402
 
-MF_FLAG = {32: 1 << 25, 16: 1 << 24}  # GMR_GEMM_MFMA32 / GMR_GEMM_MFMA16 (include/gmr.h)
+MF_FLAG = {32: 1 << 25, 16: 1 << 24, 6: 1 << 26}  # GMR_GEMM_MFMA32 / MFMA16 / X6 (split bf16) (include/gmr.h)
 
 # name, M, N, K, trans_a, trans_b, calls per epoch
 SHAPES = [
@@ -71,7 +71,15 @@ def run(args):
         best = None
         for tile0 in args.tiles:
           for mf in args.mfma:
-           tile = tile0 | (MF_FLAG[mf] if tile0 else 0)
+           tile = tile0 | (MF_FLAG[mf] if (tile0 or mf == 6) else 0)
+           if args.acc and not kw:
+               K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile)
+               a64 = (A.t() if ta else A).double()
+               b64 = (B.t() if tb else B).double()
+               ref = a64 @ b64
+               scale = a64.abs() @ b64.abs()
+               err = ((C.double() - ref).abs() / scale).max().item()
+               print(f"{name:26s} {tile0:7d} m{mf} max |C - C64| / (|A||B|) = {err:.3e}", flush=True)
            for split in args.splits:
             for _ in range(3):
                 K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile, split_k=split, **kw)
@@ -95,7 +103,8 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--splits", default="0")
     ap.add_argument("--only", default="", help="substring filter on shape names")
-    ap.add_argument("--mfma", default="32", help="MFMA shapes to try: 32 (32x32x2) and/or 16 (16x16x4)")
+    ap.add_argument("--mfma", default="32", help="MFMA shapes to try: 32 (32x32x2), 16 (16x16x4), 6 (split-bf16)")
+    ap.add_argument("--acc", action="store_true", help="also print the error vs an fp64 product")
     a = ap.parse_args()
     a.tiles = [int(t) for t in a.tiles.split(",")]
     a.splits = [int(t) for t in a.splits.split(",")]

@@ -596,6 +596,55 @@ def test_gemm_glds_bit_exact_vs_register_staging(K, tile, ta, tb):
         torch.testing.assert_close(outs[0], want, rtol=2e-4, atol=2e-3)
 
 
+X6, F32 = 1 << 26, 1 << 27  # GMR_GEMM_X6 / GMR_GEMM_F32 tile flags (include/gmr.h)
+
+
+@pytest.mark.parametrize("tile", [0, 128, 256128, 128256])
+def test_gemm_x6_fp32_accuracy(K, tile):
+    """Split-bf16 products (GMR_GEMM_X6: x = hi + mid + lo exactly, six bf16 MFMA products) carry fp32
+    accuracy: against an fp64 product the error stays inside the bound the fp32-MFMA kernel is held to
+    (2e-6 of sum |a b|), and the two kernels agree to that bound, on ragged M / N edges, K not a
+    multiple of 32 or of 4 (padded rows), split-K slabs and values spanning 2^-20 .. 2^20."""
+    rng = _rng(37)
+    for M, N, Kd, split in ((300, 200, 1000, 1), (517, 260, 70, 1), (19, 33, 7, 1), (1000, 700, 7050, 4),
+                            (640, 384, 1001, 2)):
+        ldk = (Kd + 3) // 4 * 4
+        a = rng.standard_normal((M, ldk)) * np.exp2(rng.integers(-20, 21, size=(M, 1)))
+        b = rng.standard_normal((N, ldk))
+        A = _dev(a.astype(np.float32))[:, :Kd]
+        B = _dev(b.astype(np.float32))[:, :Kd]
+        ref = A.double() @ B.double().t()
+        scale = A.double().abs() @ B.double().abs().t()
+        outs = []
+        for flag in (X6, F32):
+            C = torch.empty(M, N, device=DEV)
+            K.gemm(A, B, C, trans_b=True, tile=tile | flag if tile else flag, split_k=split)
+            outs.append(C.double())
+            assert ((C.double() - ref).abs() / scale).max().item() <= 2e-6, (M, N, Kd, split, flag)
+        assert ((outs[0] - outs[1]).abs() / scale).max().item() <= 2e-6
+
+
+def test_gemm_x6_epilogues(K):
+    """The split-bf16 kernel runs the denoiser epilogues: BIAS_TANH with a per-row bias table index
+    (the time-embedding collapse) and the in-place p_sample POSTERIOR."""
+    rng = _rng(38)
+    M, N, Kd, T = 600, 520, 1000, 5
+    A = _dev(rng.standard_normal((M, Kd)).astype(np.float32))
+    B = _dev(rng.standard_normal((N, Kd)).astype(np.float32))
+    acc = A.double() @ B.double().t()
+    bound = 2e-6 * (A.double().abs() @ B.double().abs().t()) + 1e-6  # the fp32 product bound (both epilogues are
+    eb = _dev(rng.standard_normal((T, N)).astype(np.float32))           # 1-Lipschitz in the product)
+    t = _dev(rng.integers(0, T, size=M), torch.int32)
+    C = torch.empty(M, N, device=DEV)
+    K.gemm(A, B, C, trans_b=True, epi=K.EPI_BIAS_TANH, bias=eb, bias_row=t, ld_bias=N, tile=128 | X6)
+    assert ((C.double() - torch.tanh(acc + eb.double()[t.long()])).abs() <= bound).all()
+    aux = _dev(rng.standard_normal((M, N)).astype(np.float32))
+    bias = _dev(rng.standard_normal(N).astype(np.float32))
+    C.copy_(aux)
+    K.gemm(A, B, C, trans_b=True, epi=K.EPI_POSTERIOR, bias=bias, aux=C, slope=0.25, beta=0.75, tile=256128 | X6)
+    assert ((C.double() - (0.25 * (acc + bias.double()) + 0.75 * aux.double())).abs() <= bound).all()
+
+
 @pytest.mark.parametrize("nb", [1, 2, 4])
 def test_spmm_row_classes_bit_exact(K, nb):
     """Lane plans with row classes (item rows scheduled before user rows,
