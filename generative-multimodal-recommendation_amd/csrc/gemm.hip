@@ -602,6 +602,7 @@ struct Plan {
   int tile, bm, bn, splits, mf;
   bool glds;
   int64_t tm, tn, kps;
+  int xpose;  // split-bf16 plans of TN / NN / TT calls: 1 = A, 2 = B copied k-contiguous into the workspace
 };
 
 int default_mfma() {
@@ -653,7 +654,7 @@ int auto_splits(int64_t tm, int64_t tn, int bm, int64_t K) {
   return s;
 }
 
-Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int split_k) {
+Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int split_k, bool allow_x6) {
   int mf = default_mfma();
   if (tile & GMR_GEMM_MFMA16) mf = 16;
   if (tile & GMR_GEMM_MFMA32) mf = 32;
@@ -661,7 +662,7 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
   if (tile & GMR_GEMM_GLDS) glds = true;
   if (tile & GMR_GEMM_REGSTAGE) glds = false;
   // (the staging and MFMA-shape flags name fp32-kernel variants, so they select the fp32 kernel too)
-  const bool x6 = ((tile & GMR_GEMM_X6) || default_x6()) &&
+  const bool x6 = allow_x6 && ((tile & GMR_GEMM_X6) || default_x6()) &&
                   !(tile & (GMR_GEMM_F32 | GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32 | GMR_GEMM_GLDS | GMR_GEMM_REGSTAGE));
   tile &= ~(GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32 | GMR_GEMM_GLDS | GMR_GEMM_REGSTAGE | GMR_GEMM_X6 | GMR_GEMM_F32);
   if (tile == 0) {
@@ -696,6 +697,9 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
     else if (!tnm && M * N >= (int64_t)1 << 20 && K >= 4096) tile = 128;
     else tile = 64;
   }
+  // split-bf16 plans take 128^2 instead of 64^2 for products of >= 4M outputs (the denoiser weight
+  // gradients 7050 x 1000 x 2048, TN, run as NT on transposed copies: two 128^2 blocks per CU)
+  if (x6 && tile == 64 && M * N >= ((int64_t)4 << 20) && K >= 256) tile = 128;
   // the split-bf16 kernel (gemm_x6.hip): NT products on 128^2, 256 x 128, 128 x 256 and 256^2 tiles
   // (the 256^2 tile maps to 256 x 128: a 2-wave-per-SIMD 256^2 block spills its prefetch registers)
   if (x6 && tile != 64 && !ta && tb) {
@@ -716,7 +720,40 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
   kps = (kps + BK - 1) / BK * BK;
   p.splits = (int)((K + kps - 1) / kps);
   p.kps = kps;
+  p.xpose = 0;
   return p;
+}
+
+// TN / NN / TT calls whose NT form takes the split-bf16 kernel copy their m- / n-contiguous operands
+// k-contiguous into the workspace (gemm_x6.hip x6_transpose: 2 x 4 bytes per element, a few percent of
+// the product's time at the denoiser shapes) and run as NT; otherwise the fp32-input MFMA plan
+Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int split_k) {
+  if (ta || !tb) {
+    Plan q = make_plan_core(0, 1, M, N, K, tile, split_k, true);
+    if (q.mf == 6) {
+      q.xpose = (ta ? 1 : 0) | (tb ? 0 : 2);
+      return q;
+    }
+    return make_plan_core(ta, tb, M, N, K, tile, split_k, false);
+  }
+  return make_plan_core(ta, tb, M, N, K, tile, split_k, true);
+}
+
+// workspace layout of a plan: [tile counters + split slabs (split-K) | A^T (M x Kp) | B^T (N x Kp)],
+// segments 16-byte aligned, Kp = K rounded up to 4
+struct WsLayout {
+  int64_t slabs, at, bt, total, kp;
+};
+WsLayout ws_layout(const Plan& p, int64_t M, int64_t N, int64_t K) {
+  auto r4 = [](int64_t v) { return (v + 3) / 4 * 4; };
+  WsLayout w;
+  w.kp = r4(K);
+  const int64_t sk = p.splits > 1 ? r4(GMR_GEMM_COUNTER_WORDS + (int64_t)p.splits * M * N) : 0;
+  w.slabs = 0;
+  w.at = sk;
+  w.bt = w.at + ((p.xpose & 1) ? r4(M * w.kp) : 0);
+  w.total = w.bt + ((p.xpose & 2) ? r4(N * w.kp) : 0);
+  return w;
 }
 
 }  // namespace
@@ -725,7 +762,9 @@ extern "C" int32_t gmr_gemm_kernel_kind(int32_t trans_a, int32_t trans_b, int64_
                                         int32_t tile, int32_t split_k, int32_t aligned) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const Plan p = make_plan(trans_a, trans_b, M, N, K, tile, split_k);
-  return p.mf == 6 && !aligned ? 32 : p.mf;  // gmr_gemm_f32: the split-bf16 kernel needs aligned operands
+  if (p.mf == 6 && !aligned && p.xpose != 3)  // gmr_gemm_f32: k-contiguous operands used in place need alignment
+    return make_plan_core(trans_a, trans_b, M, N, K, tile, split_k, false).mf;
+  return p.mf;
 }
 
 extern "C" int64_t gmr_gemm_workspace_floats(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
@@ -734,7 +773,12 @@ extern "C" int64_t gmr_gemm_workspace_floats(int32_t trans_a, int32_t trans_b, i
   // partial sums, 0 without split-K
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const Plan p = make_plan(trans_a, trans_b, M, N, K, tile, split_k);
-  return p.splits > 1 ? GMR_GEMM_COUNTER_WORDS + (int64_t)p.splits * M * N : 0;
+  int64_t need = ws_layout(p, M, N, K).total;
+  if (p.mf == 6) {  // gmr_gemm_f32 falls back to the fp32 plan when the operands are not 16-byte aligned
+    const Plan q = make_plan_core(trans_a, trans_b, M, N, K, tile, split_k, false);
+    need = std::max(need, ws_layout(q, M, N, K).total);
+  }
+  return need;
 }
 
 extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, float alpha,
@@ -768,9 +812,32 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   e.ld_aux = ld_aux;
   e.rv1 = rowvec1;
   e.rv2 = rowvec2;
-  const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
+  const bool a16 = ((uintptr_t)A % 16 == 0) && lda % 4 == 0, b16 = ((uintptr_t)B % 16 == 0) && ldb % 4 == 0;
+  bool vec = a16 && b16;
   Plan pl = make_plan(trans_a, trans_b, M, N, K, tile, split_k);
-  if (pl.mf == 6 && !vec) pl.mf = 32;  // the split-bf16 kernel loads float4 granules only
+  // the split-bf16 kernel loads float4 granules: operands it reads in place must be 16-byte aligned
+  if (pl.mf == 6 && !(((pl.xpose & 1) || a16) && ((pl.xpose & 2) || b16)))
+    pl = make_plan_core(trans_a, trans_b, M, N, K, tile, split_k, false);
+  const WsLayout wl = ws_layout(pl, M, N, K);
+  if (pl.xpose) {
+    GMR_ARG(workspace && workspace_floats >= wl.total, "needs workspace of gmr_gemm_workspace_floats(...) floats");
+    GMR_ARG(((uintptr_t)workspace & 15) == 0, "workspace must be 16-byte aligned");
+    if (pl.xpose & 1) {  // A stored K x M -> A^T (M x Kp)
+      x6_transpose(A, lda, K, M, workspace + wl.at, wl.kp, (hipStream_t)stream);
+      GMR_LAUNCHED();
+      A = workspace + wl.at;
+      lda = wl.kp;
+    }
+    if (pl.xpose & 2) {  // B stored K x N -> B^T (N x Kp)
+      x6_transpose(B, ldb, K, N, workspace + wl.bt, wl.kp, (hipStream_t)stream);
+      GMR_LAUNCHED();
+      B = workspace + wl.bt;
+      ldb = wl.kp;
+    }
+    trans_a = 0;
+    trans_b = 1;
+    vec = true;
+  }
   tile = pl.tile;
   const int64_t tm = pl.tm, tn = pl.tn, kps = pl.kps;
   const int splits = pl.splits;

@@ -256,4 +256,9 @@ __device__ __forceinline__ void tile_mn(int tile, int tn_packed, int tiles_m, in
 int x6_launch(int bm, int bn, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
               const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n, int64_t kps, float* ws);
 
+// dst[c * ld_dst + r] = src[r * ld_src + c] for r < rows, c < cols (the k-contiguous copy of an m- or
+// n-contiguous operand for the split-bf16 kernel)
+void x6_transpose(const float* src, int64_t ld_src, int64_t rows, int64_t cols, float* dst, int64_t ld_dst,
+                  hipStream_t st);
+
 }  // namespace gmr_gemm

@@ -320,9 +320,38 @@ __global__ void __launch_bounds__(64 * WGM * WGN, OCC) gemm_x6_kernel(int64_t M,
   gemm_epilogue<BM, BN, WGM, WGN, 32>(acc, M, N, C, ldc, epi, m0, n0, ws);
 }
 
+// 64 x 64 tiles through LDS (row pad 1: conflict-free column reads), 256 threads, 16 elements each;
+// reads and writes are 256-byte row segments
+__global__ void __launch_bounds__(256) x6_transpose_kernel(const float* __restrict__ src, int64_t ld_src,
+                                                           int64_t rows, int64_t cols, float* __restrict__ dst,
+                                                           int64_t ld_dst, int64_t tiles_c) {
+  __shared__ float t[64][65];
+  const int64_t tr = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+  const int64_t r0 = tr * 64, c0 = tc * 64;
+  const int x = threadIdx.x & 63, y = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t r = r0 + y + 4 * i, c = c0 + x;
+    t[y + 4 * i][x] = (r < rows && c < cols) ? src[r * ld_src + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t c = c0 + y + 4 * i, r = r0 + x;
+    if (c < cols && r < rows) dst[c * ld_dst + r] = t[x][y + 4 * i];
+  }
+}
+
 }  // namespace
 
 namespace gmr_gemm {
+
+void x6_transpose(const float* src, int64_t ld_src, int64_t rows, int64_t cols, float* dst, int64_t ld_dst,
+                  hipStream_t st) {
+  const int64_t tr = (rows + 63) / 64, tc = (cols + 63) / 64;
+  hipLaunchKernelGGL(x6_transpose_kernel, dim3((unsigned)(tr * tc)), dim3(256), 0, st, src, ld_src, rows, cols, dst,
+                     ld_dst, tc);
+}
 
 // GMR_GEMM_X6_PIPE = 1: the double-buffered kernels split the next tile between the MFMAs (A/B)
 static int x6_pipe() {

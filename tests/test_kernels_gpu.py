@@ -600,28 +600,39 @@ X6, F32 = 1 << 26, 1 << 27  # GMR_GEMM_X6 / GMR_GEMM_F32 tile flags (include/gmr
 
 
 @pytest.mark.parametrize("tile", [0, 128, 256128, 128256])
-def test_gemm_x6_fp32_accuracy(K, tile):
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
+def test_gemm_x6_fp32_accuracy(K, tile, ta, tb):
     """Split-bf16 products (GMR_GEMM_X6: x = hi + mid + lo exactly, six bf16 MFMA products) carry fp32
     accuracy: against an fp64 product the error stays inside the bound the fp32-MFMA kernel is held to
     (2e-6 of sum |a b|), and the two kernels agree to that bound, on ragged M / N edges, K not a
-    multiple of 32 or of 4 (padded rows), split-K slabs and values spanning 2^-20 .. 2^20."""
+    multiple of 32 or of 4 (padded rows), split-K slabs and values spanning 2^-20 .. 2^20.  TN / NN / TT
+    calls run as NT on k-contiguous copies of their operands (x6_transpose)."""
     rng = _rng(37)
     for M, N, Kd, split in ((300, 200, 1000, 1), (517, 260, 70, 1), (19, 33, 7, 1), (1000, 700, 7050, 4),
                             (640, 384, 1001, 2)):
-        ldk = (Kd + 3) // 4 * 4
-        a = rng.standard_normal((M, ldk)) * np.exp2(rng.integers(-20, 21, size=(M, 1)))
-        b = rng.standard_normal((N, ldk))
-        A = _dev(a.astype(np.float32))[:, :Kd]
-        B = _dev(b.astype(np.float32))[:, :Kd]
-        ref = A.double() @ B.double().t()
-        scale = A.double().abs() @ B.double().abs().t()
+        a = rng.standard_normal((M, Kd)) * np.exp2(rng.integers(-20, 21, size=(M, 1)))
+        b = rng.standard_normal((N, Kd))
+        pad = lambda x: np.pad(x, ((0, 0), (0, (-x.shape[1]) % 4))).astype(np.float32)  # noqa: E731  16-byte rows
+        A = _dev(pad(a.T) if ta else pad(a))[:, :(M if ta else Kd)]
+        B = _dev(pad(b) if tb else pad(b.T))[:, :(Kd if tb else N)]
+        a64, b64 = torch.as_tensor(a, device=DEV), torch.as_tensor(b, device=DEV)
+        a64, b64 = a64.float().double(), b64.float().double()
+        ref = a64 @ b64.t()
+        scale = a64.abs() @ b64.abs().t()
         outs = []
         for flag in (X6, F32):
             C = torch.empty(M, N, device=DEV)
-            K.gemm(A, B, C, trans_b=True, tile=tile | flag if tile else flag, split_k=split)
+            K.gemm(A, B, C, trans_a=bool(ta), trans_b=bool(tb), tile=tile | flag if tile else flag, split_k=split)
             outs.append(C.double())
             assert ((C.double() - ref).abs() / scale).max().item() <= 2e-6, (M, N, Kd, split, flag)
         assert ((outs[0] - outs[1]).abs() / scale).max().item() <= 2e-6
+    if tile:  # an explicit >= 128^2 tile with GMR_GEMM_X6 takes the split kernel in every layout
+        assert _lib_kind(ta, tb, 1000, 700, 7050, tile | X6) == 6
+
+
+def _lib_kind(ta, tb, M, N, Kd, tile):
+    from gmr import _lib
+    return int(_lib.load().gmr_gemm_kernel_kind(ta, tb, M, N, Kd, tile, 0, 1))
 
 
 def test_gemm_x6_epilogues(K):
