@@ -715,6 +715,15 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
   p.tm = (M + p.bm - 1) / p.bm;
   p.tn = (N + p.bn - 1) / p.bn;
   int splits = split_k;
+  if (splits <= 0 && mf == 6) {
+    // split-bf16 plans: the slabs cost more next to the faster product; split only while the tiles
+    // fill < 80 % of the resident slots (256 x 128: one block per CU; 128^2: two) and slabs stay >= 512
+    // deep (measured: the 7050 x 1000 x 2048 weight gradients 253 -> 222 us unsplit, the 2048-row
+    // diffusion products best at 4 slabs; profiles/r02x6_study.txt)
+    const int64_t slots = p.bm * p.bn == 128 * 128 ? 512 : 256;
+    splits = 1;
+    while (p.tm * p.tn * splits * 5 < slots * 4 && K / (splits * 2) >= 512 && splits < 16) splits *= 2;
+  }
   if (splits <= 0) splits = auto_splits(p.tm, p.tn, p.bm, K);
   int64_t kps = (K + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
