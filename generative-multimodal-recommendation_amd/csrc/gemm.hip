@@ -203,114 +203,6 @@ __device__ __forceinline__ void glds_zero_tail(float* img, int kvalid) {
 
 // Final epilogue of one float4 chunk (row m, columns n .. n + 3): bias / x reads and the C store
 // are 16-byte where aligned, element-wise at the right edge.
-struct EpiCtx {
-  const float* xb;
-  int64_t ldx;
-  bool rx, pure, v_in, v_out;
-};
-__device__ __forceinline__ EpiCtx epi_ctx(const Epi& epi, const float* C, int64_t ldc) {
-  EpiCtx c;
-  c.rx = epi_reads_x(epi);
-  c.pure = !c.rx && !epi.bias_row && !epi.rv1 && !epi.rv2;
-  c.xb = (epi.kind == GMR_EPI_NONE || epi.kind == GMR_EPI_BIAS) ? C : epi.aux;
-  c.ldx = (epi.kind == GMR_EPI_NONE || epi.kind == GMR_EPI_BIAS) ? ldc : epi.ld_aux;
-  c.v_out = ldc % 4 == 0 && ((uintptr_t)C & 15) == 0;
-  c.v_in = (!epi.bias || (((uintptr_t)epi.bias & 15) == 0 && (!epi.bias_row || epi.ld_bias % 4 == 0))) &&
-           (!c.rx || (((uintptr_t)c.xb & 15) == 0 && c.ldx % 4 == 0));
-  return c;
-}
-__device__ __forceinline__ void epi_store4(const Epi& epi, float* __restrict__ C, int64_t ldc, int64_t N, int64_t m,
-                                           int64_t n, const float (&a4)[4], const EpiCtx& ctx) {
-  const bool full = n + 3 < N;
-  float b4[4] = {0.f, 0.f, 0.f, 0.f}, x4[4] = {0.f, 0.f, 0.f, 0.f};
-  const float* bp = epi.bias ? epi.bias + (epi.bias_row ? (int64_t)epi.bias_row[m] * epi.ld_bias : 0) + n : nullptr;
-  const float* xp = ctx.rx ? ctx.xb + m * ctx.ldx + n : nullptr;
-  if (full && ctx.v_in) {
-    if (bp) {
-      const float4 t = *reinterpret_cast<const float4*>(bp);
-      b4[0] = t.x, b4[1] = t.y, b4[2] = t.z, b4[3] = t.w;
-    }
-    if (xp) {
-      const float4 t = *reinterpret_cast<const float4*>(xp);
-      x4[0] = t.x, x4[1] = t.y, x4[2] = t.z, x4[3] = t.w;
-    }
-  } else {
-    for (int q = 0; q < 4 && n + q < N; ++q) {
-      if (bp) b4[q] = bp[q];
-      if (xp) x4[q] = xp[q];
-    }
-  }
-  const float r1 = ctx.pure ? 0.f : epi_r1(epi, m), r2 = ctx.pure ? 0.f : epi_r2(epi, m);
-  float o4[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) o4[q] = epi_fin(epi, a4[q], b4[q], x4[q], r1, r2);
-  float* o = C + m * ldc + n;
-  if (full && ctx.v_out) {
-    *reinterpret_cast<float4*>(o) = make_float4(o4[0], o4[1], o4[2], o4[3]);
-  } else {
-    for (int q = 0; q < 4 && n + q < N; ++q) o[q] = o4[q];
-  }
-}
-
-// Epilogue through LDS (glds kernel): after the k loop the staging buffers are free, so the tile
-// goes to LDS in row blocks of HR rows (fragment element stores: 32 consecutive columns per half
-// wave, conflict-free) and comes back as float4 row chunks: the bias / aux / C traffic and the
-// output stores are 16-byte, coalesced, and no per-element arrays are held in registers (the
-// register epilogue of a 1,024-thread 256^2 tile spills).  Same per-element arithmetic (epi_fin).
-template <int BM, int BN, int WGM, int WGN>
-__device__ __forceinline__ void gemm_epilogue_lds(const floatx16 (&acc)[BM / WGM / 32][BN / WGN / 32], float* smem,
-                                                  int64_t M, int64_t N, float* __restrict__ C, int64_t ldc,
-                                                  const Epi& epi, int64_t m0, int64_t n0, float* __restrict__ ws) {
-  constexpr int NT = 64 * WGM * WGN;
-  constexpr int WTM = BM / WGM, WTN = BN / WGN;
-  constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int AVAIL = 2 * (BM + BN) * BK;                // floats of the two staging buffers
-  constexpr int HR0 = (AVAIL / BN) / 32 * 32;
-  constexpr int HR = HR0 < BM ? HR0 : BM;                   // rows per pass
-  constexpr int C4 = BN / 4;
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int wm = w / WGN, wn = w % WGN;
-  const int h = lane >> 5, l32 = lane & 31;
-  const EpiCtx ctx = epi_ctx(epi, C, ldc);
-  const bool v_out = ws ? (N % 4 == 0 && ((uintptr_t)ws & 15) == 0) : ctx.v_out;
-#pragma unroll
-  for (int r0 = 0; r0 < BM; r0 += HR) {
-    __syncthreads();  // the buffers (first pass: the k loop's last reads; later: the previous pass) are free
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rb = wm * WTM + i * 32;
-      if (rb < r0 || rb >= r0 + HR) continue;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = wn * WTN + j * 32 + l32;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) smem[(rb - r0 + (e & 3) + 8 * (e >> 2) + 4 * h) * BN + col] = acc[i][j][e];
-      }
-    }
-    __syncthreads();
-    const int rows = BM - r0 < HR ? BM - r0 : HR;
-    for (int idx = threadIdx.x; idx < rows * C4; idx += NT) {
-      const int rr = idx / C4, c = (idx % C4) * 4;
-      const int64_t m = m0 + r0 + rr, n = n0 + c;
-      if (m >= M || n >= N) continue;
-      const float4 v = *reinterpret_cast<const float4*>(smem + rr * BN + c);
-      const float a4[4] = {v.x, v.y, v.z, v.w};
-      const bool full = n + 3 < N;
-      if (ws) {
-        float* o = ws + ((int64_t)blockIdx.z * M + m) * N + n;
-        if (full && v_out) {
-          *reinterpret_cast<float4*>(o) = v;
-        } else {
-          for (int q = 0; q < 4 && n + q < N; ++q) o[q] = a4[q];
-        }
-        continue;
-      }
-      epi_store4(epi, C, ldc, N, m, n, a4, ctx);
-    }
-  }
-}
-
 template <bool KC, int R>
 __device__ __forceinline__ float4 gfrag(const float* img, int row, int h, int q) {
   if (KC) return *reinterpret_cast<const float4*>(img + row * BK + 4 * ((4 * h + q) ^ kc_swz(row)));

@@ -317,7 +317,14 @@ __global__ void __launch_bounds__(64 * WGM * WGN, OCC) gemm_x6_kernel(int64_t M,
     }
   }
 
-  gemm_epilogue<BM, BN, WGM, WGN, 32>(acc, M, N, C, ldc, epi, m0, n0, ws);
+  // epilogues that read an aux / C element per output leave through LDS as float4 row chunks (coalesced
+  // C / aux traffic: the p_sample posterior product 870 -> 726 us at 8192 rows); the others store the
+  // accumulator fragments directly (the row passes of the LDS epilogue cost the bias-only products)
+  if (!ws && epi_reads_x(epi))
+    gemm_epilogue_lds<BM, BN, WGM, WGN, NBUF * 3 * (BM + BN) * BK / 2>(acc, reinterpret_cast<float*>(smem), M, N, C,
+                                                                     ldc, epi, m0, n0, ws);
+  else
+    gemm_epilogue<BM, BN, WGM, WGN, 32>(acc, M, N, C, ldc, epi, m0, n0, ws);
 }
 
 // 64 x 64 tiles through LDS (row pad 1: conflict-free column reads), 256 threads, 16 elements each;
