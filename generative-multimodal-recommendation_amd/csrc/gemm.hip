@@ -596,7 +596,9 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
   // (the 256^2 tile maps to 256 x 128: a 2-wave-per-SIMD 256^2 block spills its prefetch registers)
   if (x6 && tile != 64 && !ta && tb) {
     mf = 6;
-    if (tile == 256) tile = 256128;
+    // products with >= 768 128^2 tiles run three 128^2 blocks per CU (gemm_x6.hip), which beat
+    // 256 x 128 there (19445 x 1000 x 7050: 1852 -> 1605 us); smaller ones keep 256 x 128
+    if (tile == 256) tile = ((M + 127) / 128) * ((N + 127) / 128) >= 768 ? 128 : 256128;
   }
   Plan p;
   p.mf = mf;

@@ -372,7 +372,7 @@ static int x6_pipe() {
 static int x6_nb128() {
   static const int v = [] {
     const char* e = getenv("GMR_GEMM_X6_NB128");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   return v;
 }
@@ -389,13 +389,18 @@ int x6_launch(int bm, int bn, dim3 grid, hipStream_t st, int64_t M, int64_t N, i
                          st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);                              \
     return 0;                                                                                                      \
   }
-  // 256 x 128 / 128 x 256: one 8-wave block per CU, LDS double-buffered (144 KiB); 128^2: two 4-wave
-  // blocks per CU, single-buffered (48 KiB each), so one block's split / barrier phase overlaps the
-  // other's MFMA steps (GMR_GEMM_X6_NB128 = 2: one double-buffered block per CU, for A/B runs)
+  // 256 x 128 / 128 x 256: one 8-wave block per CU, LDS double-buffered (144 KiB); 128^2: two or three
+  // 4-wave blocks per CU, single-buffered (48 KiB each), so one block's split / barrier phase overlaps
+  // the others' MFMA steps (GMR_GEMM_X6_NB128 = 1 / 3: always two / three single-buffered blocks,
+  // = 2: one double-buffered block per CU; for A/B runs)
   if (bm == 256 && bn == 128) GMR_X6(256, 128, 4, 2, 2, 1)
   if (bm == 128 && bn == 256) GMR_X6(128, 256, 2, 4, 2, 1)
   if (bm == 128 && bn == 128) {
-    if (x6_nb128() == 2) GMR_X6(128, 128, 2, 2, 2, 1)
+    // three blocks per CU (168 VGPRs) when the grid fills them: the 19445-row p_sample products -4..-8 %;
+    // two below that (the 448-tile weight gradients +4 % at three; profiles/r02x6_study.txt)
+    const int nb = x6_nb128();
+    if (nb == 2) GMR_X6(128, 128, 2, 2, 2, 1)
+    if (nb == 3 || (nb == 0 && (int64_t)grid.x * grid.z >= 768)) GMR_X6(128, 128, 2, 2, 1, 3)
     GMR_X6(128, 128, 2, 2, 1, 2)
   }
 #undef GMR_X6
