@@ -325,7 +325,8 @@ def run_workload(args, dist_on, barrier, max_over_ranks, with_cpu_baseline):
             log("note: no split-bf16 GEMM launch in the probed epoch")
         for o in roof.values():
             o["probe_scope"] = ("one extra epoch after the timed region with the side streams off (GMR_SERIAL): "
-                                "HIP events around every launch of the class on its stream")
+                                "HIP events around every launch of the class on its stream (a GEMM call: its "
+                                "k-contiguous operand copies, the kernel and the split-K reduce)")
         roof["_epoch"] = {"mfma_flop_per_epoch": mfma_flop, "serial_epoch_ms": round(serial_ms, 2),
                           "epoch_mfma_frac": round(mfma_flop / (dt / args.steps) / 1e12 / FP32_MFMA_PEAK_TFS, 4),
                           "note": "algorithmic GEMM + InfoNCE flop of one epoch / timed ms_per_step / fp32 MFMA peak"}
