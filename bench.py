@@ -354,6 +354,27 @@ def dominant(roof):
     return name, cls[name]
 
 
+def launch_ranks(n):
+    """Run this script under torch.distributed.run with n ranks (one per GPU, RCCL over xGMI) as a
+    child process; its stdout (rank 0's JSON line) is relayed; the exit code is the launcher's."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching: " + " ".join(cmd))
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if lines:
+        print(lines[-1], flush=True)
+    if r.returncode != 0 or not lines:
+        log(f"distributed bench failed (exit {r.returncode}); stdout tail: {r.stdout[-2000:]}")
+        return r.returncode or 1
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -373,9 +394,15 @@ def main():
     args.model = args.model or "diffmm"
     args.shape = args.shape or DEFAULT_SHAPE[args.model]
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without a launcher: start the N ranks as a child process group
+        # (before anything here touches the GPU) and relay rank 0's JSON line
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; n_gpus reports WORLD_SIZE")
     if world > 1:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         backend = os.environ.get("GMR_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm; gloo only to rehearse

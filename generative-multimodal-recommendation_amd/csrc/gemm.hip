@@ -642,8 +642,10 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int sp
   return make_plan_core(ta, tb, M, N, K, tile, split_k, true);
 }
 
-// workspace layout of a plan: [tile counters + split slabs (split-K) | A^T (M x Kp) | B^T (N x Kp)],
-// segments 16-byte aligned, Kp = K rounded up to 4
+// workspace layout of a plan: [tile counters | split slabs (split-K) | A^T (M x Kp) | B^T (N x Kp)],
+// segments 16-byte aligned, Kp = K rounded up to 4.  The counter words lead EVERY layout that uses
+// the workspace (a shared per-stream scratch whose counters must stay zero between calls), so a
+// transposed-operand plan never writes over them.
 struct WsLayout {
   int64_t slabs, at, bt, total, kp;
 };
@@ -651,9 +653,9 @@ WsLayout ws_layout(const Plan& p, int64_t M, int64_t N, int64_t K) {
   auto r4 = [](int64_t v) { return (v + 3) / 4 * 4; };
   WsLayout w;
   w.kp = r4(K);
-  const int64_t sk = p.splits > 1 ? r4(GMR_GEMM_COUNTER_WORDS + (int64_t)p.splits * M * N) : 0;
-  w.slabs = 0;
-  w.at = sk;
+  const bool uses = p.splits > 1 || p.xpose;
+  w.slabs = GMR_GEMM_COUNTER_WORDS;
+  w.at = uses ? r4(GMR_GEMM_COUNTER_WORDS + (p.splits > 1 ? (int64_t)p.splits * M * N : 0)) : 0;
   w.bt = w.at + ((p.xpose & 1) ? r4(M * w.kp) : 0);
   w.total = w.bt + ((p.xpose & 2) ? r4(N * w.kp) : 0);
   return w;

@@ -498,30 +498,36 @@ __global__ void __launch_bounds__(256) sum_parts_kernel(int P, const double* __r
 // ----------------------------------------------------------------- losses
 // InfoNCE rows (genrecv1.py:407-414) on logits L = v1 v2^T / temp (B x B, in place):
 //   loss[r] = logsumexp(L[r]) - L[r][r];  L[r][j] <- coef (softmax_rj - [j == r])
-__global__ void __launch_bounds__(256) nce_rows_kernel(int64_t B, float* __restrict__ L, int64_t ld, float coef,
-                                                       float* __restrict__ loss) {
+// rows of an in-batch InfoNCE logit block L (rows x cols, already scaled by 1/tau): row r's positive
+// sits at column diag_off + r (diag_off = 0, cols = rows: the square B x B block of one process; a
+// data-parallel rank holds rows [diag_off, diag_off + rows) of the global batch against all cols keys).
+// loss[r] = logsumexp_j L[r, j] - L[r, diag_off + r]; with coef != 0, L is overwritten by its gradient
+// coef * (softmax_r - e_{diag_off + r}).
+__global__ void __launch_bounds__(256) nce_rows_kernel(int64_t cols, float* __restrict__ L, int64_t ld,
+                                                       int64_t diag_off, float coef, float* __restrict__ loss) {
   const int64_t r = blockIdx.x;
   float* p = L + r * ld;
   __shared__ float red[4];
   float m = -INFINITY;
-  for (int64_t j = threadIdx.x; j < B; j += 256) m = fmaxf(m, p[j]);
+  for (int64_t j = threadIdx.x; j < cols; j += 256) m = fmaxf(m, p[j]);
   m = gmr::wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   __syncthreads();
   float s = 0.f;
-  for (int64_t j = threadIdx.x; j < B; j += 256) s += expf(p[j] - m);
+  for (int64_t j = threadIdx.x; j < cols; j += 256) s += expf(p[j] - m);
   s = gmr::wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   const float S = (red[0] + red[1]) + (red[2] + red[3]);
   const float lse = m + logf(S);
-  const float diag = p[r];
+  const int64_t dj = diag_off + r;
+  const float diag = p[dj];
   __syncthreads();
   if (threadIdx.x == 0 && loss) loss[r] = lse - diag;
   if (coef != 0.f)
-    for (int64_t j = threadIdx.x; j < B; j += 256) p[j] = coef * expf(p[j] - lse) - (j == r ? coef : 0.f);
+    for (int64_t j = threadIdx.x; j < cols; j += 256) p[j] = coef * expf(p[j] - lse) - (j == dj ? coef : 0.f);
 }
 
 // BPR with log-sigmoid (genrecv1.py:377-380): x = <u,p> - <u,n>; loss_b = softplus(-x);
@@ -705,7 +711,17 @@ extern "C" int gmr_dot64_f32(int64_t rows, const float* a, int64_t lda, const fl
 
 extern "C" int gmr_nce_rows_f32(int64_t B, float* L, int64_t ld, float coef, float* loss, void* stream) {
   GMR_ARG(L && B > 0 && ld >= B, "bad args");
-  hipLaunchKernelGGL(nce_rows_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, B, L, ld, coef, loss);
+  hipLaunchKernelGGL(nce_rows_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, B, L, ld, (int64_t)0, coef,
+                     loss);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_nce_rows_off_f32(int64_t rows, int64_t cols, float* L, int64_t ld, int64_t diag_off, float coef,
+                                    float* loss, void* stream) {
+  GMR_ARG(L && rows > 0 && cols > 0 && ld >= cols && diag_off >= 0 && diag_off + rows <= cols, "bad args");
+  hipLaunchKernelGGL(nce_rows_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, cols, L, ld, diag_off,
+                     coef, loss);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -48,6 +48,11 @@ SIGNATURES = {
     "gmr_spmm_jobs_f32": (I32, [I32, P, P]),
     "gmr_spmm_panel_f32": (I32, [P, P, I64, I64, P, I32, I32, P, I64, F32, F32, P, I64, P, I32, P]),
     "gmr_spmm_csr_f32": (I32, [P, P, P, I64, I64, P, I32, P, I32, P, P, P, P, I64, F32, F32, P, I64, I32, P]),
+    "gmr_spmm_side_plan_words": (I64, [P, I64, I64, I32]),
+    "gmr_spmm_side_plan_build": (I32, [P, I64, I64, I32, P, I64]),
+    "gmr_spmm_side_scratch_floats": (I64, [P]),
+    "gmr_spmm_side_pack": (I32, [P, P, P, I64, I64, I64, P, P]),
+    "gmr_spmm_side_f32": (I32, [P, I32, P, P, P, P, I64, F32, F32, P, P, P, P]),
     "gmr_bipartite_nnz": (I64, [I64, I64, I64, I32]),
     "gmr_bipartite_workspace_ints": (I64, [I64, I64]),
     "gmr_bipartite_symnorm_build": (I32, [I64, I64, P, P, I64, I32, F64, P, P, P, P, P]),
@@ -117,6 +122,7 @@ SIGNATURES = {
     "gmr_mul64_f32": (I32, [I64, P, I64, P, I64, P, I64, F32, I32, P]),
     "gmr_dot64_f32": (I32, [I64, P, I64, P, I64, P, F32, P, I32, P]),
     "gmr_nce_rows_f32": (I32, [I64, P, I64, F32, P, P]),
+    "gmr_nce_rows_off_f32": (I32, [I64, I64, P, I64, I64, F32, P, P]),
     "gmr_bpr_logsigmoid_f32": (I32, [I32, I64, P, P, P, P, P, P, F32, P]),
     "gmr_axpy_dev_f32": (I32, [I64, P, P, P, P]),
     "gmr_mul_f32": (I32, [I64, P, P, P, P]),

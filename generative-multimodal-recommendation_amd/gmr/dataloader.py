@@ -153,6 +153,24 @@ class TrainDataLoader:
             yield (b, dist.shard_sizes(rows, W), s[0, lo:hi], s[1, lo:hi], s[2, lo:hi], d["plan_bpr"][b * W + r],
                    d["plan_cl"][b * W + r])
 
+    def step_rows(self, d, g, rank=None):
+        """(users, pos, row0) of global optimiser step g: every row of the step (the global batch g,
+        or under GMR_DP_MODE=local the world whole batches of step g, which sit back to back in the
+        epoch draw) and the offset of this rank's rows inside it.  In-batch terms (GenRecV1's B x B
+        InfoNCE, models/genrecv1.py:407-414) take their keys from all of them."""
+        from . import dist
+        W, r = d["world"], dist.rank() if rank is None else rank
+        s, offs = d["sample"], d["offsets_np"]
+        if W == 1 and dist.local_batches():
+            Wd = dist.world()
+            nb = d["n_batches"]
+            glo, ghi = int(offs[min(nb, g * Wd)]), int(offs[min(nb, (g + 1) * Wd)])
+            own = int(offs[min(nb, g * Wd + r)])
+        else:
+            glo, ghi = int(offs[g * W]), int(offs[(g + 1) * W])
+            own = int(offs[g * W + r])
+        return s[0, glo:ghi], s[1, glo:ghi], own - glo
+
     # --- reference-style iteration -------------------------------------------------------
     def __len__(self):
         return math.ceil(self.n_inter / self.step)

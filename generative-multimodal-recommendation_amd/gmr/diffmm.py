@@ -445,7 +445,8 @@ class DiffMM(GeneralRecommender):
             if d is None:
                 return None
             dev = self.device
-            return K.CSR(d["rowptr"].to(dev), d["col"].to(dev), d["val"].to(dev), symmetric=False)
+            return K.CSR(d["rowptr"].to(dev), d["col"].to(dev), d["val"].to(dev), symmetric=False,
+                         class_split=self.n_users, side=True)  # the plan kind a rebuild gives
         gi, gt = csr(st.get("image_UI_matrix")), csr(st.get("text_UI_matrix"))
         if gi is not None and gt is not None:
             self.set_ui_matrices(gi, gt, csr(st.get("image_UI_matrix_T")), csr(st.get("text_UI_matrix_T")))

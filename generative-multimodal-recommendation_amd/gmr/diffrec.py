@@ -179,12 +179,15 @@ class DiffRec(GeneralRecommender):
         if not dist.is_dist():
             return
         W, r = dist.world(), dist.rank()
-        size = -(-int(self.batch_size) // W)
+        # a rank holds at most ceil(B / W) rows of a global-mode step, a whole batch in local mode
+        size = int(self.batch_size) if dist.local_batches() else -(-int(self.batch_size) // W)
         tb = torch.full((W * size,), -1, dtype=torch.int32, device=self.device)
         lb = torch.zeros(W * size, dtype=torch.float64, device=self.device)
         if self._pending is not None:
             t, loss = self._pending
             n = t.numel()
+            if n > size:
+                raise RuntimeError(f"rank holds {n} rows of a step, more than its gather slot ({size})")
             tb[r * size:r * size + n].copy_(t)
             lb[r * size:r * size + n].copy_(loss)
         dist.all_gather_rows_(tb, size)

@@ -97,6 +97,8 @@ def _rec_init_twin(U, I, d, DV, DT):
 
 
 class GenRecV1(GeneralRecommender):
+    rec_step_takes_batch = True  # data parallel: the Trainer passes the global step's rows (in-batch InfoNCE)
+
     def __init__(self, config, dataloader):
         super().__init__(config, dataloader)
         c = config
@@ -242,7 +244,8 @@ class GenRecV1(GeneralRecommender):
                                   device=dev),
              "sums": f(128), "sqws": torch.empty(1024, dtype=torch.float64, device=dev),
              # loss
-             "loss_bpr": f(B), "contrib": f(3 * B, 64), "contrib_s": f(2 * B, 64), "g": f(4, B, 64),
+             "loss_bpr": f(B), "contrib": f(3 * B, 64), "contrib_s": f(2 * B, 64), "contrib_g": f(2 * B, 64),
+             "g": f(4, B, 64),
              "nv": f(4, B, 64), "nrm": f(4, B), "raw": f(4, B, 64), "L": f(B, Bp), "rows": f(4, B), "loss": f(4),
              # backward
              "dC": f(N, 64), "dS": f(N, 64), "dM": f(2, N, 64), "da": f(2, N), "dPG": f(2, N, 64),
@@ -328,24 +331,36 @@ class GenRecV1(GeneralRecommender):
         return w["C"], w["SIDE"]
 
     # ================================================================= fused rec step
-    def _nce(self, w, i1, i2, coef, rows):
-        """InfoNCE(nv[i1], nv[i2]) (:407-414): loss rows + gradients into g[i1], g[i2]."""
-        B = w["B"] if rows is None else rows.numel()
-        v1, v2 = w["nv"][i1][:B], w["nv"][i2][:B]
-        L = w["L"][:B, :B]
+    def _nce(self, w, i1, i2, coef, rows, row0=0, B=None, Bg=None):
+        """InfoNCE(nv[i1], nv[i2]) (:407-414): loss rows + gradients into g[i1], g[i2].  Queries are
+        rows [row0, row0 + B) of the step, keys all Bg rows (one process: row0 = 0, B = Bg)."""
+        Bg = w["B"] if Bg is None else Bg
+        B = Bg if B is None else B
+        v1, v2 = w["nv"][i1][row0:row0 + B], w["nv"][i2][:Bg]
+        L = w["L"][:B, :Bg]
         inv_t = 1.0 / self.temp
         K.gemm(v1, v2, L, trans_b=True, alpha=inv_t)
-        _lib.call("gmr_nce_rows_f32", B, ptr(L), L.stride(0), coef, ptr(rows), stream())
-        K.gemm(L, v2, w["g"][i1][:B], alpha=inv_t, beta=1.0)
-        K.gemm(L, v1, w["g"][i2][:B], trans_a=True, alpha=inv_t, beta=1.0)
+        _lib.call("gmr_nce_rows_off_f32", B, Bg, ptr(L), L.stride(0), row0, coef, ptr(rows), stream())
+        K.gemm(L, v2, w["g"][i1][row0:row0 + B], alpha=inv_t, beta=1.0)
+        K.gemm(L, v1, w["g"][i2][:Bg], trans_a=True, alpha=inv_t, beta=1.0)
 
-    def rec_step(self, users, pos, neg, plan_bpr=None, plan_cl=None, norm_rows=None, reg_share=1.0, masks=None):
-        """calculate_loss (:355-405) and all rec-parameter gradients (into rec_slab.grad)."""
+    def rec_step(self, users, pos, neg, plan_bpr=None, plan_cl=None, norm_rows=None, reg_share=1.0, masks=None,
+                 gbatch=None):
+        """calculate_loss (:355-405) and all rec-parameter gradients (into rec_slab.grad).
+
+        gbatch = (step users, step pos, row0) under data parallelism: the four in-batch InfoNCE terms
+        (:389-397) take this rank's rows [row0, row0 + B) of the global step as queries against the
+        step's keys, so the sum over ranks is the reference's global-batch loss; each rank scatters
+        its key-side gradients for every step row and the rec-slab all-reduce adds them up."""
         if self.image_UI_matrix is None:
             return torch.zeros((), device=self.device)  # the reference returns 0 before the first rebuild (:363-364)
         B = users.numel()
         nr = float(norm_rows or B)
-        w = self._work(B)
+        gu, gp, row0 = (users, pos, 0) if gbatch is None else gbatch
+        Bg = gu.numel()
+        if not 0 <= row0 <= Bg - B:
+            raise ValueError(f"rank rows [{row0}, {row0 + B}) outside the step's {Bg} rows")
+        w = self._work(max(B, Bg))
         U, I, N = self.n_users, self.n_items, self.N
         s = self.rec_slab
         E0 = s.view("E0")
@@ -353,35 +368,55 @@ class GenRecV1(GeneralRecommender):
             plan_bpr, plan_cl = self._plans(users, pos, neg)
         C, SIDE = self._forward(w, True, masks)
         # ---- losses
-        contrib, cs = w["contrib"][:3 * B], w["contrib_s"][:2 * B]
+        contrib, cs = w["contrib"][:3 * B], w["contrib_s"][:2 * Bg]
         _lib.call("gmr_bpr_logsigmoid_f32", B, U, ptr(C), ptr(users), ptr(pos), ptr(neg), ptr(w["loss_bpr"]),
                   ptr(contrib), 1.0 / nr, stream())
         loss = w["loss"][:1]
         _lib.call("gmr_sum_f32", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(loss), 0, stream())
         _lib.call("gmr_sqnorm_f32", N * 64, ptr(E0), self.reg_weight * reg_share, ptr(loss), 1, ptr(w["sqws"]),
                   stream())
-        # gathered views: 0 = C[users], 1 = C[U+pos], 2 = SIDE[users], 3 = SIDE[U+pos]
-        for j, (src, idx, off) in enumerate(((C, users, 0), (C, pos, U), (SIDE, users, 0), (SIDE, pos, U))):
-            K.gather_rows(src, idx, w["raw"][j][:B], off=off)
-            K.normalize_rows(w["raw"][j][:B], w["nv"][j][:B], w["nrm"][j][:B])
+        # gathered views of the step's rows: 0 = C[users], 1 = C[U+pos], 2 = SIDE[users], 3 = SIDE[U+pos]
+        for j, (src, idx, off) in enumerate(((C, gu, 0), (C, gp, U), (SIDE, gu, 0), (SIDE, gp, U))):
+            K.gather_rows(src, idx, w["raw"][j][:Bg], off=off)
+            K.normalize_rows(w["raw"][j][:Bg], w["nv"][j][:Bg], w["nrm"][j][:Bg])
         K.zero_(w["g"])
         for k, (i1, i2, reg) in enumerate(((3, 1, self.ssl_reg1), (2, 0, self.ssl_reg1),
                                            (0, 1, self.ssl_reg2), (0, 3, self.ssl_reg2))):
             rows = w["rows"][k][:B]
-            self._nce(w, i1, i2, reg / nr, rows)
+            self._nce(w, i1, i2, reg / nr, rows, row0, B, Bg)
             _lib.call("gmr_sum_f32", B, ptr(rows), reg / nr, ptr(loss), 1, stream())
-        K.normalize_rows_bwd(w["nv"][0][:B], w["nrm"][0][:B], w["g"][0][:B], contrib[:B], accumulate=True)
-        K.normalize_rows_bwd(w["nv"][1][:B], w["nrm"][1][:B], w["g"][1][:B], contrib[B:2 * B], accumulate=True)
-        K.normalize_rows_bwd(w["nv"][2][:B], w["nrm"][2][:B], w["g"][2][:B], cs[:B])
-        K.normalize_rows_bwd(w["nv"][3][:B], w["nrm"][3][:B], w["g"][3][:B], cs[B:])
         dC, dS = w["dC"], w["dS"]
         K.zero_(dC)
         K.zero_(dS)
+        K.normalize_rows_bwd(w["nv"][2][:Bg], w["nrm"][2][:Bg], w["g"][2][:Bg], cs[:Bg])
+        K.normalize_rows_bwd(w["nv"][3][:Bg], w["nrm"][3][:Bg], w["g"][3][:Bg], cs[Bg:])
+        if gbatch is None:  # the views' rows are the BPR rows: one scatter per table
+            K.normalize_rows_bwd(w["nv"][0][:B], w["nrm"][0][:B], w["g"][0][:B], contrib[:B], accumulate=True)
+            K.normalize_rows_bwd(w["nv"][1][:B], w["nrm"][1][:B], w["g"][1][:B], contrib[B:2 * B], accumulate=True)
+            plan_g = plan_cl
+        else:  # the step's rows: their own plan (keys users | U + pos, as plan_cl)
+            cg = w["contrib_g"][:2 * Bg]
+            K.normalize_rows_bwd(w["nv"][0][:Bg], w["nrm"][0][:Bg], w["g"][0][:Bg], cg[:Bg])
+            K.normalize_rows_bwd(w["nv"][1][:Bg], w["nrm"][1][:Bg], w["g"][1][:Bg], cg[Bg:])
+            plan_g = self._plan2(gu, gp)
+            _lib.call("gmr_scatter_sorted_f32", plan_g.numel(), 64, ptr(plan_g), ptr(cg), 64, ptr(dC), 64, stream())
         _lib.call("gmr_scatter_sorted_f32", plan_bpr.numel(), 64, ptr(plan_bpr), ptr(contrib), 64, ptr(dC), 64, stream())
-        _lib.call("gmr_scatter_sorted_f32", plan_cl.numel(), 64, ptr(plan_cl), ptr(cs), 64, ptr(dS), 64, stream())
+        _lib.call("gmr_scatter_sorted_f32", plan_g.numel(), 64, ptr(plan_g), ptr(cs), 64, ptr(dS), 64, stream())
         self._backward(w, reg_share)
         self._step += 1
         return loss[0]
+
+    def _plan2(self, users, pos):
+        """Sorted scatter plan of the keys [users | U + pos] (plan_cl's layout) for any row set."""
+        B = users.numel()
+        dev = self.device
+        keys = torch.stack([users, pos]).to(torch.int32).contiguous()
+        offs = torch.tensor([0, B], dtype=torch.int64, device=dev)
+        pc = torch.empty((1, 1 << max(1, (2 * B - 1).bit_length())), dtype=torch.int64, device=dev)
+        ka = torch.tensor([0, self.n_users], dtype=torch.int32, device=dev)
+        _lib.call("gmr_sort_batch_keys", 1, ptr(keys), ptr(offs), ptr(ka), 2, B, ptr(pc), pc.shape[1], pc.shape[1],
+                  stream())
+        return pc[0]
 
     def _bn_bwd(self, w, call, z, rows, act, dy=None, mul=None, keep=None, da=None, dz=None, acc_dz=False):
         name = _BN_CALLS[call]
@@ -541,7 +576,8 @@ class GenRecV1(GeneralRecommender):
         g = st.get("image_UI_matrix")
         if g is not None:
             dev = self.device
-            mk = lambda d: K.CSR(d["rowptr"].to(dev), d["col"].to(dev), d["val"].to(dev), symmetric=False)  # noqa: E731
+            mk = lambda d: K.CSR(d["rowptr"].to(dev), d["col"].to(dev), d["val"].to(dev), symmetric=False,  # noqa: E731
+                                 class_split=self.n_users, side=True)
             t = st.get("image_UI_matrix_T")
             self.set_image_ui_matrix(mk(g), mk(t) if t is not None else None)
 

@@ -259,12 +259,17 @@ SPMM_SEG_NNZ = SPMM_LANE_PLAN | 32
 # 3 % faster only at d = 256 (profiles/r02i_spmm_nt.txt); it stays a tested alternative
 SPMM_NORM_ADJ = SPMM_LANE_PLAN | 32
 SPMM_CHUNK = 1 << 18  # chunk plan: whole-row tasks of <= 128 entries, one gather round per wave (include/gmr.h)
+# side-split plans (csrc/spmm_side.hip) for square matrices with a side split (the bipartite graph-conv
+# adjacencies): each XCD serves one (side, 32-column slice), lane groups stream <= SPMM_SIDE_T-entry
+# tasks, hub rows combine in-launch.  GMR_SPMM_SIDE=0 keeps every product on the lane plans (A/B)
+SPMM_SIDE = os.environ.get("GMR_SPMM_SIDE", "1") == "1"
+SPMM_SIDE_T = int(os.environ.get("GMR_SPMM_SIDE_T", "64"))
 
 
 class CSR:
     """Device CSR (int32 rowptr/col, fp32 val) of an n x n matrix with its SpMM work plan."""
 
-    def __init__(self, rowptr, col, val, n_cols=None, seg_nnz=None, symmetric=True, class_split=0):
+    def __init__(self, rowptr, col, val, n_cols=None, seg_nnz=None, symmetric=True, class_split=0, side=False):
         seg_nnz = SPMM_SEG_NNZ if seg_nnz is None else seg_nnz
         self.rowptr, self.col, self.val = rowptr, col, val
         self.n_rows = rowptr.numel() - 1
@@ -279,6 +284,7 @@ class CSR:
         self.partial = torch.zeros((prow, 256), dtype=torch.float32, device=dev)
         cs = class_split if (SPMM_CLASSES and seg_nnz & SPMM_LANE_PLAN and not seg_nnz & SPMM_PACKED) else 0
         self.class_split = class_split
+        self.side = None
         _lib.call("gmr_spmm_plan_build_split", ptr(rowptr), self.n_rows, self.nnz, seg_nnz, cs, ptr(self.plan),
                   stream())
         if seg_nnz & SPMM_PACKED or seg_nnz == SPMM_CHUNK:  # col/val are final here (built before wrapping)
@@ -291,6 +297,32 @@ class CSR:
         self.flags = SPMM_NO_SPLIT_ROWS if (seg_nnz < 512 and hdr[1] == 0) else 0
         if seg_nnz & SPMM_LANE_PLAN and hdr[2] >> 1:
             self.flags |= SPMM_HUB_FIXUP
+        if side and SPMM_SIDE and class_split > 0 and self.n_cols == self.n_rows and self.nnz > 0:
+            self.build_side_plan(class_split)
+
+    def build_side_plan(self, split, T=None):
+        """Side-split plan (gmr_spmm_side_*): built on the host from a host copy of rowptr (one
+        device sync per graph build), entries packed on the device; self.partial becomes the plan's
+        scratch (zeroed: its hub counters re-arm themselves after every launch)."""
+        import numpy as np
+        lib = _lib.load()
+        T = SPMM_SIDE_T if T is None else T
+        rp = np.ascontiguousarray(self.rowptr.cpu().numpy().astype(np.int32))
+        rpp = rp.ctypes.data_as(ctypes.c_void_p)
+        words = int(lib.gmr_spmm_side_plan_words(rpp, self.n_rows, int(split), int(T)))
+        if words <= 0:
+            raise RuntimeError("gmr_spmm_side_plan_words failed")
+        host = np.zeros(words, np.int32)
+        _lib.call("gmr_spmm_side_plan_build", rpp, self.n_rows, int(split), int(T), host.ctypes.data_as(ctypes.c_void_p),
+                  words)
+        dev = self.rowptr.device
+        plan = torch.from_numpy(host).to(dev)
+        _lib.call("gmr_spmm_side_pack", ptr(self.rowptr), ptr(self.col), ptr(self.val), self.n_rows, self.nnz,
+                  int(host[14]), ptr(plan), stream())
+        nsc = int(lib.gmr_spmm_side_scratch_floats(host.ctypes.data_as(ctypes.c_void_p)))
+        self.side = (plan, int(split))
+        self.side_hdr = tuple(int(x) for x in host[:16])
+        self.partial = torch.zeros(max(nsc, self.partial.numel()), dtype=torch.float32, device=dev)
 
     def spmm(self, out, blocks, split=None, alpha=1.0, beta=0.0, partial=None):
         """out = alpha * A @ X + beta * out; X = column blocks [(lo, hi), ...] of 64 columns each.
@@ -316,12 +348,27 @@ class CSR:
         for b in blocks:
             if b[0].shape[1] != 64 or (split != self.n_cols and b[1].shape[1] != 64):
                 raise ValueError("each block is 64 columns wide")
+        if self.side is not None:
+            ys = PArr(*[out[:, 64 * b:64 * (b + 1)].data_ptr() for b in range(nb)] + [0] * (4 - nb))
+            ldy = LArr(*[_ld(out)] * nb + [0] * (4 - nb))
+            self._side_call(nb, lo, ldl, hi, ldh, split, alpha, beta, ys, ldy, partial)
+            return out
         with _Probe("spmm", (self.nnz, self.n_rows, self.n_cols, nb, beta != 0.0)):
             _lib.call("gmr_spmm_csr_f32", ptr(self.rowptr), ptr(self.col), ptr(self.val), self.n_rows, self.nnz,
                       ptr(self.plan), self.seg_nnz, ptr(self.partial if partial is None else partial), nb, lo, ldl,
                       hi, ldh, split, float(alpha),
                       float(beta), ptr(out), _ld(out), self.flags, stream())
         return out
+
+
+def _side_call(self, nb, lo, ldl, hi, ldh, split, alpha, beta, ys, ldy, partial):
+    """gmr_spmm_side_f32 with host arrays of block pointers / strides (CSR.spmm, spmm_multi, spmm_jobs)."""
+    with _Probe("spmm", (self.nnz, self.n_rows, self.n_cols, nb, beta != 0.0)):
+        _lib.call("gmr_spmm_side_f32", ptr(self.side[0]), nb, lo, ldl, hi, ldh, int(split), float(alpha), float(beta),
+                  ys, ldy, ptr(self.partial if partial is None else partial), stream())
+
+
+CSR._side_call = _side_call
 
 
 def score_f16(a, b, out):
@@ -353,6 +400,9 @@ def spmm_multi(a, outs, blocks, split=None, alpha=1.0, beta=0.0, partial=None):
         ldh = LArr(*[_ld(b[1]) for b in blocks] + [0] * (4 - nb))
     ys = PArr(*[o.data_ptr() for o in outs] + [0] * (4 - nb))
     ldy = LArr(*[_ld(o) for o in outs] + [0] * (4 - nb))
+    if a.side is not None:
+        a._side_call(nb, lo, ldl, hi, ldh, split, alpha, beta, ys, ldy, partial)
+        return outs
     with _Probe("spmm", (a.nnz, a.n_rows, a.n_cols, nb, beta != 0.0)):
         _lib.call("gmr_spmm_multi_f32", ptr(a.col), ptr(a.val), a.n_rows, a.nnz, ptr(a.plan), a.seg_nnz, nb, lo, ldl,
                   hi, ldh, split, float(alpha), float(beta), ys, ldy, ptr(a.partial if partial is None else partial),
@@ -369,6 +419,16 @@ def spmm_jobs(jobs, alpha=1.0, beta=0.0):
     n = len(jobs)
     if not 1 <= n <= 4:
         raise ValueError("1 to 4 jobs")
+    if any(j[0].side is not None for j in jobs):  # side-plan products launch on their own (in job order)
+        lane = [j for j in jobs if j[0].side is None]
+        for a, outs, blocks, split, partial in jobs:
+            if a.side is not None:
+                if isinstance(outs, torch.Tensor):
+                    outs = [outs[:, 64 * b:64 * (b + 1)] for b in range(len(blocks))]
+                spmm_multi(a, outs, blocks, split=split, alpha=alpha, beta=beta, partial=partial)
+        if lane:
+            spmm_jobs(lane, alpha=alpha, beta=beta)
+        return
     arr = (_lib.SpmmJob * n)()
     for q, (a, outs, blocks, split, partial) in enumerate(jobs):
         nb = len(blocks)
@@ -428,7 +488,7 @@ def bipartite_symnorm(n_users, n_items, user_ptr, user_items, self_loops, deg_ep
     ws = torch.empty(lib.gmr_bipartite_workspace_ints(n_users, n_items), dtype=torch.int32, device=dev)
     _lib.call("gmr_bipartite_symnorm_build", n_users, n_items, ptr(user_ptr), ptr(user_items), n_ui,
               int(self_loops), float(deg_eps), ptr(ws), ptr(rowptr), ptr(col), ptr(val), stream())
-    return CSR(rowptr, col[:nnz], val[:nnz], seg_nnz=seg_nnz, class_split=n_users)
+    return CSR(rowptr, col[:nnz], val[:nnz], seg_nnz=seg_nnz, class_split=n_users, side=True)
 
 
 def topk_to_user_csr(topk, user_ptr, user_items):
@@ -530,7 +590,7 @@ def csr_transpose(a):
     _lib.call("gmr_csr_transpose", a.n_rows, nc, a.nnz, ptr(a.rowptr), ptr(a.col), ptr(a.val), ptr(ws), ptr(trp),
               ptr(tcol), ptr(tval), ptr(scol), ptr(sval), stream())
     return CSR(trp, tcol[:a.nnz], tval[:a.nnz], n_cols=a.n_rows, symmetric=False,
-               class_split=a.class_split if a.n_rows == a.n_cols else 0)
+               class_split=a.class_split if a.n_rows == a.n_cols else 0, side=a.side is not None)
 
 
 def csr_drop_edges(a, keep_rate, seed=0, step=0, keep=None, transposed=False):
@@ -548,7 +608,8 @@ def csr_drop_edges(a, keep_rate, seed=0, step=0, keep=None, transposed=False):
     oval = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
     _lib.call("gmr_csr_drop_write", a.n_rows, ptr(a.rowptr), ptr(a.col), ptr(a.val), int(transposed), ptr(keep),
               float(keep_rate), int(seed), int(step), ptr(orp), ptr(ocol), ptr(oval), stream())
-    return CSR(orp, ocol[:nnz], oval[:nnz], n_cols=a.n_cols, symmetric=False, class_split=a.class_split)
+    return CSR(orp, ocol[:nnz], oval[:nnz], n_cols=a.n_cols, symmetric=False, class_split=a.class_split,
+               side=a.side is not None)
 
 
 def knn_graph(feat, k):

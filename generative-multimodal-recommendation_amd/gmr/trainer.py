@@ -90,6 +90,10 @@ class Trainer:
             if u.numel() > 0:
                 if self._use_graphs and W == 1 and u.numel() == train_data.batch_size:
                     self._graphed_step(u, p, ng, pb, pc, norm, share, acc)
+                elif W > 1 and getattr(self.model, "rec_step_takes_batch", False):
+                    # in-batch terms see the whole global step (GenRecV1's B x B InfoNCE keys)
+                    loss = self.model.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share,
+                                               gbatch=train_data.step_rows(d, b))
                 else:
                     loss = self._rec_step(u, p, ng, pb, pc, norm, share, sum(rank_rows[:dist.rank()]))
                     _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())

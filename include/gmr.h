@@ -149,6 +149,28 @@ typedef struct gmr_spmm_job {
 } gmr_spmm_job;
 int gmr_spmm_jobs_f32(int32_t n_jobs, const gmr_spmm_job* jobs, void* stream);
 int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream);
+
+/* Side-split SpMM (csrc/spmm_side.hip; the graph-conv products of models/diffmm.py:136-191, 285 and
+ * common/trainer.py:464-485).  Rows [0, split) and [split, n) are the two sides of a bipartite
+ * adjacency; each XCD serves one (side, 32-column slice) group, lane groups stream tasks of <= T
+ * CSR entries (whole rows; hub rows cut into pieces whose partial rows the last-arriving piece adds
+ * in order, in-launch).  Plan: built on the HOST from a host copy of rowptr (words from
+ * gmr_spmm_side_plan_words), copied to the device, then gmr_spmm_side_pack writes the packed
+ * (col, val) entries into it (packed_off = plan word 14).  scratch: gmr_spmm_side_scratch_floats
+ * floats, zero before the first call (its counters re-arm themselves); two launches that may run
+ * concurrently need separate scratch.  Y = alpha A X + beta Y with X / Y as gmr_spmm_multi_f32's
+ * per-block split sources / outputs (16-byte aligned, strides multiples of 4).  A short row's sum
+ * is its entries in CSR order; a hub row adds its pieces in piece order: deterministic. */
+int64_t gmr_spmm_side_plan_words(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t T);
+int gmr_spmm_side_plan_build(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t T, int32_t* plan_host,
+                             int64_t words);
+int64_t gmr_spmm_side_scratch_floats(const int32_t* plan_host);
+int gmr_spmm_side_pack(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
+                       int64_t packed_off, int32_t* plan, void* stream);
+int gmr_spmm_side_f32(const int32_t* plan, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
+                      const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
+                      float* const* y_blocks, const int64_t* ld_y, float* scratch, void* stream);
+
 int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                      const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,
                      const float* const* x_lo, const int64_t* ld_lo, const float* const* x_hi, const int64_t* ld_hi,
@@ -415,6 +437,11 @@ int gmr_dot64_f32(int64_t rows, const float* a, int64_t lda, const float* b, int
 /* InfoNCE rows on L = v1 v2^T / temp (B x B, in place; :407-414): loss[r] = lse(L_r) - L_rr and
  * L <- coef (softmax - I) for the two gradient GEMMs (coef 0: loss only) */
 int gmr_nce_rows_f32(int64_t B, float* L, int64_t ld, float coef, float* loss, void* stream);
+/* the same for a data-parallel rank's block: rows [diag_off, diag_off + rows) of the global batch
+ * against all cols keys (row r's positive at column diag_off + r; genrecv1.py:407-414 over the
+ * global batch) */
+int gmr_nce_rows_off_f32(int64_t rows, int64_t cols, float* L, int64_t ld, int64_t diag_off, float coef, float* loss,
+                         void* stream);
 /* BPR with log-sigmoid (:377-380) over one (U + I) x 64 table; contrib = [dU; dP; dN] */
 int gmr_bpr_logsigmoid_f32(int32_t B, int64_t U, const float* C, const int32_t* users, const int32_t* pos,
                            const int32_t* neg, float* loss, float* contrib, float inv_norm, void* stream);

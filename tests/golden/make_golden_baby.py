@@ -22,7 +22,15 @@ Reference code exercised (paths relative to GenMMRec/src):
                                  with pop / niche, warm / cold and coverage / gini / tail extras)
   utils/quick_start.py:46-102    pop_items (top 20 % train items) and warm users (> 5 train inter.)
 
-Usage:  python tests/golden/make_golden_baby.py        (about a minute on 8 cores)
+Usage:  python tests/golden/make_golden_baby.py [baby|sports|diffrec]
+  baby   (default) -> diffmm_baby.npz / diffmm_baby_meta.json, about a minute on 8 cores
+  sports (config 4: 35,598 users x 18,357 items) -> diffmm_sports.npz / _meta.json:
+         the same checks on the valid split only (the is_test extras are pinned at baby), a few
+         minutes on 8 cores
+  diffrec (config 2: DiffRec.yaml at the baby shape) -> diffrec_baby.npz / _meta.json: the seed-999
+         DNN init digests (models/diffrec.py:313-353), the valid split's full_sort_predict = the
+         100-step p_sample (:291-310, :372-388) -> mask -> top-50, and the unrounded metrics;
+         about two minutes on 8 cores
 """
 import hashlib
 import json
@@ -48,14 +56,16 @@ def digest(a):
     return hashlib.sha256(a.tobytes()).hexdigest()
 
 
-def write_dataset(path):
+def write_dataset(path, shape="baby"):
+    """The shape's synthetic data in the reference's on-disk layout, under the dataset name the
+    reference's configs know (sports-shaped data is written as 'sports': configs/dataset/sports.yaml)."""
     from gmr.synthetic import SHAPES, make_features, make_interactions
-    U, I, n, dv, dt = SHAPES["baby"]
+    U, I, n, dv, dt = SHAPES[shape]
     u, i, lb = make_interactions(U, I, n, 0)
     v, t = make_features(I, dv, dt, 0)
-    d = os.path.join(path, "baby")
+    d = os.path.join(path, shape)
     os.makedirs(d, exist_ok=True)
-    with open(os.path.join(d, "baby.inter"), "w") as f:
+    with open(os.path.join(d, f"{shape}.inter"), "w") as f:
         f.write("userID\titemID\tx_label\trating\n")
         for a, b, c in zip(u.tolist(), i.tolist(), lb.tolist()):
             f.write(f"{a}\t{b}\t{c}\t5\n")
@@ -63,27 +73,89 @@ def write_dataset(path):
     np.save(os.path.join(d, "text_feat.npy"), t)
 
 
-def reference_config(ref_mods):
+def reference_config(ref_mods, shape="baby"):
     import utils.configurator as configurator
     cwd = os.getcwd()
     os.chdir(REF_SRC)  # the reference's Config reads ./configs (utils/configurator.py:72-76)
     try:
-        cfg = configurator.Config("DiffMM", "baby", {"use_gpu": False, "data_path": TMP + "/", "epochs": 1,
-                                                     "save_recommended_topk": False})
+        cfg = configurator.Config("DiffMM", shape, {"use_gpu": False, "data_path": TMP + "/", "epochs": 1,
+                                                    "save_recommended_topk": False})
     finally:
         os.chdir(cwd)
     return cfg
 
 
+def main_diffrec():
+    ref = _import_reference()
+    import torch
+    import utils.configurator as configurator
+    import utils.utils as rutils
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    if os.path.isdir(TMP):
+        shutil.rmtree(TMP)
+    write_dataset(TMP, "baby")
+    cwd = os.getcwd()
+    os.chdir(REF_SRC)
+    try:
+        cfg = configurator.Config("DiffRec", "baby", {"use_gpu": False, "data_path": TMP + "/", "epochs": 1,
+                                                      "save_recommended_topk": False})
+    finally:
+        os.chdir(cwd)
+    ds = ref["dataset"].RecDataset(cfg)
+    tr, va, te = ds.split()
+    for part in (tr, va, te):
+        str(part)
+    tl = ref["dataloader"].TrainDataLoader(cfg, tr, batch_size=cfg["train_batch_size"], shuffle=True)
+    vl = ref["dataloader"].EvalDataLoader(cfg, va, additional_dataset=tr, batch_size=cfg["eval_batch_size"])
+    rutils.init_seed(999)
+    tl.pretrain_setup()
+    model = ref["diffrec"].DiffRec(cfg, tl)
+    meta = {"U": model.n_users, "I": model.n_items, "n_train": len(tr), "torch": torch.__version__,
+            "numpy": np.__version__, "generator": "tests/golden/make_golden_baby.py diffrec", "reference": REF_SRC,
+            "steps": int(cfg["steps"]),
+            "param_sha256": {n: digest(p.detach().numpy()) for n, p in model.model.named_parameters()}}
+    ev = ref["topk_evaluator"].TopKEvaluator(cfg)
+    kmax = max(cfg["topk"])
+    model.eval()
+    mats, vals = [], []
+    with torch.no_grad():
+        for batch in vl:
+            scores = model.full_sort_predict(batch)
+            m = batch[1]
+            scores[m[0], m[1]] = -1e10
+            v, ix = torch.topk(scores, kmax, dim=-1)
+            mats.append(ix)
+            vals.append(v)
+    topk = torch.cat(mats).numpy()
+    out = {"valid_top50": topk.astype(np.int16), "valid_top50_val_sample": torch.cat(vals)[:SAMPLE].numpy()}
+    res = ev.evaluate([torch.as_tensor(topk)], vl, is_test=False)
+    pos = vl.get_eval_items()
+    bool_rec = np.asarray([[i in p for i in row] for p, row in zip(pos, topk)])
+    raw = ev._calculate_metrics(vl.get_eval_len_list(), bool_rec)
+    meta["valid"] = {"n_users": int(len(topk)), "rounded": res,
+                     "raw": {mname: np.asarray(raw[j], np.float64).tolist()
+                             for j, mname in enumerate(["recall", "ndcg", "precision", "map"])}}
+    np.savez_compressed(os.path.join(HERE, "diffrec_baby.npz"), **out)
+    with open(os.path.join(HERE, "diffrec_baby_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1, default=float)
+    shutil.rmtree(TMP)
+    print("wrote", os.path.join(HERE, "diffrec_baby.npz"))
+
+
 def main():
+    shape = sys.argv[1] if len(sys.argv) > 1 else "baby"
+    if shape == "diffrec":
+        return main_diffrec()
+    if shape not in ("baby", "sports"):
+        raise SystemExit("shape: baby, sports or diffrec")
     ref = _import_reference()
     import torch
     import utils.utils as rutils
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     if os.path.isdir(TMP):
         shutil.rmtree(TMP)
-    write_dataset(TMP)
-    cfg = reference_config(ref)
+    write_dataset(TMP, shape)
+    cfg = reference_config(ref, shape)
     ds = ref["dataset"].RecDataset(cfg)
     tr, va, te = ds.split()
     for part in (tr, va, te):
@@ -102,7 +174,7 @@ def main():
     model = ref["diffmm"].DiffMM(cfg, tl)
     U, I = model.n_users, model.n_items
     meta = {"U": U, "I": I, "n_train": len(tr), "torch": torch.__version__, "numpy": np.__version__,
-            "generator": "tests/golden/make_golden_baby.py", "reference": REF_SRC}
+            "generator": f"tests/golden/make_golden_baby.py {shape}", "reference": REF_SRC, "shape": shape}
     dg = {n: digest(getattr(model, n).detach().numpy()) for n in
           ("uEmbeds", "iEmbeds", "image_trans", "text_trans", "modal_weight")}
     for mod in ("image", "text"):
@@ -143,7 +215,8 @@ def main():
     # ---- full-rank evaluation (trainer.py:369-388) on valid (is_test False) and test (is_test True)
     ev = ref["topk_evaluator"].TopKEvaluator(cfg)
     kmax = max(cfg["topk"])
-    for name, ld, is_test in (("valid", vl, False), ("test", tel, True)):
+    splits = (("valid", vl, False), ("test", tel, True)) if shape == "baby" else (("valid", vl, False),)
+    for name, ld, is_test in splits:
         mats, vals = [], []
         with torch.no_grad():
             for batch in ld:
@@ -164,11 +237,11 @@ def main():
                       "raw": {mname: np.asarray(raw[j], np.float64).tolist()
                               for j, mname in enumerate(["recall", "ndcg", "precision", "map"])},
                       "eval_users_head": np.asarray(ld.get_eval_users())[:16].tolist()}
-    np.savez_compressed(os.path.join(HERE, "diffmm_baby.npz"), **out)
-    with open(os.path.join(HERE, "diffmm_baby_meta.json"), "w") as f:
+    np.savez_compressed(os.path.join(HERE, f"diffmm_{shape}.npz"), **out)
+    with open(os.path.join(HERE, f"diffmm_{shape}_meta.json"), "w") as f:
         json.dump(meta, f, indent=1, default=float)
     shutil.rmtree(TMP)
-    print("wrote", os.path.join(HERE, "diffmm_baby.npz"))
+    print("wrote", os.path.join(HERE, f"diffmm_{shape}.npz"))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,95 @@
+"""Config 2 — DiffRec at the Amazon-baby shape (19,445 users x 7,050 items; DiffRec.yaml: 100 steps,
+dims [300], embedding 64) against the reference's own outputs on the same inputs
+(tests/golden/diffrec_baby.npz + diffrec_baby_meta.json, made by `make_golden_baby.py diffrec`, which
+ran the reference in the build container).  Through the HIP path:
+  * R1   DNN initialisation after init_seed(999): SHA-256 of every parameter equals the reference's
+         (models/diffrec.py:313-353, the CPU RNG order) - bit-exact;
+  * R3   full_sort_predict = the 100-step p_sample (:291-310, :372-388) of the valid users, masked
+         (common/trainer.py:384) and top-50: equal to the reference BY POSITION except inside
+         near-tie groups of our own scores (|ds| <= 1e-6 relative: fp32 summation order over 100
+         chained GEMM steps); the reference's top-50 scores for the stored user sample within 1e-4;
+  * D21  Recall/NDCG/Precision/MAP@{5,10,20,50} unrounded within 1e-4 (north-star bar).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEV = "cuda"
+NAMES = {"emb_layer.weight": "emb_W", "emb_layer.bias": "emb_b", "in_layers.0.weight": "W1",
+         "in_layers.0.bias": "b1", "out_layers.0.weight": "W2", "out_layers.0.bias": "b2"}
+
+
+@pytest.fixture(scope="module")
+def drb():
+    from gmr.configurator import Config
+    from gmr.dataloader import EvalDataLoader, TrainDataLoader
+    from gmr.synthetic import make_dataset
+    from gmr.utils import get_model, get_trainer, init_seed
+    cfg = Config("DiffRec", "baby", {"synthetic": "baby", "save_recommended_topk": False, "epochs": 1})
+    ds = make_dataset(cfg, "baby", seed=0)
+    tr, va, te = ds.split()
+    tl = TrainDataLoader(cfg, tr, batch_size=cfg["train_batch_size"], shuffle=True)
+    vl = EvalDataLoader(cfg, va, additional_dataset=tr, batch_size=cfg["eval_batch_size"])
+    init_seed(999)
+    model = get_model("DiffRec")(cfg, tl)
+    trainer = get_trainer("DiffRec")(cfg, model)
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "diffrec_baby.npz"), allow_pickle=False))
+    with open(os.path.join(ROOT, "tests", "golden", "diffrec_baby_meta.json")) as f:
+        meta = json.load(f)
+    assert (model.n_users, model.n_items, tl.n_inter, model.steps) == (meta["U"], meta["I"], meta["n_train"],
+                                                                        meta["steps"])
+    return {"model": model, "trainer": trainer, "vl": vl, "g": g, "meta": meta}
+
+
+def _sha(t):
+    a = np.ascontiguousarray(t.detach().contiguous().cpu().numpy().astype(np.float32))
+    return hashlib.sha256(a.tobytes()).hexdigest()
+
+
+def test_diffrec_baby_init_matches_reference_bit_exact(drb):
+    s, want = drb["model"].model.slab, drb["meta"]["param_sha256"]
+    got = {ref: _sha(s.view(ours)) for ref, ours in NAMES.items()}
+    assert set(got) == set(want)
+    bad = [k for k in want if got[k] != want[k]]
+    assert not bad, f"DNN parameters differing from the reference init: {bad}"
+
+
+def test_diffrec_baby_valid_topk_by_position_and_metrics(drb):
+    from gmr import kernels as K
+    m, g, tr, vl = drb["model"], drb["g"], drb["trainer"], drb["vl"]
+    m.eval()
+    d = vl.to_device()
+    n, E = vl.pr_end, vl.step
+    out = torch.empty((n, 50), dtype=torch.int32, device=DEV)
+    scores = []
+    for lo in range(0, n, E):
+        hi = min(n, lo + E)
+        sc = m.full_sort_predict([d["eval_u32"][lo:hi].long()])
+        m0, m1 = int(d["mask_ptr"][lo]), int(d["mask_ptr"][hi])
+        K.mask_scores(sc, d["mask_rows"][m0:m1] - lo, d["mask_cols"][m0:m1])
+        K.topk_rows(sc, 50, out[lo:hi])
+        scores.append(sc.cpu().numpy())
+    scores = np.concatenate(scores)
+    ours = out.cpu().numpy().astype(np.int64)
+    ref = g["valid_top50"].astype(np.int64)
+    assert ours.shape == ref.shape
+    S = g["valid_top50_val_sample"].shape[0]
+    np.testing.assert_allclose(np.take_along_axis(scores[:S], ref[:S], 1), g["valid_top50_val_sample"], rtol=1e-4,
+                               atol=1e-6)
+    r, c = np.nonzero(ours != ref)
+    s_o, s_r = scores[r, ours[r, c]], scores[r, ref[r, c]]
+    tie = np.abs(s_o - s_r) <= 1e-6 * np.maximum(np.abs(s_o), 1e-3)
+    assert tie.all(), (f"{int((~tie).sum())} top-50 positions differ outside near ties "
+                       f"(first rows {np.unique(r[~tie])[:5]}); {len(r)} differing positions in all")
+    sums = tr.evaluator.device_sums(out, vl).cpu().numpy().reshape(4, 8)
+    raw = drb["meta"]["valid"]["raw"]
+    for j, name in enumerate(["recall", "ndcg", "precision", "map"]):
+        for q, k in enumerate([5, 10, 20, 50]):
+            assert abs(sums[j, q] / n - raw[name][k - 1]) <= 1e-4, (name, k, sums[j, q] / n, raw[name][k - 1])

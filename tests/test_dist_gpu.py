@@ -203,3 +203,142 @@ def test_dp2_local_batches_equal_double_batch_single_process():
     np.testing.assert_allclose(dp["bpr_epoch_loss"], single["bpr_epoch_loss"], rtol=1e-5)
     for k in ("den_img", "rec_params"):
         np.testing.assert_allclose(dp[k], single[k], rtol=1e-3, atol=2e-5, err_msg=k)
+
+
+def _case_diffrec_local(batch):
+    """DiffRec (config 2) Trainer epoch with train_batch_size = batch on the tiny golden shape:
+    denoiser slab, epoch loss and the importance-sampling history after the epoch."""
+    from test_diffrec_gpu import build_diffrec
+
+    from gmr.trainer import Trainer
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "diffrec_tiny.npz"), allow_pickle=False))
+    torch.manual_seed(999)
+    m, cfg, ds, tl = build_diffrec(g, train_batch_size=batch)
+    tl.batch_size = tl.step = batch
+    tr = Trainer(cfg, m)
+    loss, _ = tr._train_epoch(tl, 0)
+    return {"loss": np.array([loss]), "den": m.model.slab.data.cpu().numpy().copy(),
+            "hist": m.Lt_history.cpu().numpy().copy(), "count": m.Lt_count.cpu().numpy().copy(),
+            "step": np.array([m._step])}
+
+
+def _worker_diffrec_local(rank, world, port, q, batch):
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "generative-multimodal-recommendation_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, pth)
+    os.environ["GMR_DP_MODE"] = "local"
+    import torch.distributed as tdist
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        res = _case_diffrec_local(batch)
+        if rank == 0:
+            q.put(res)
+        tdist.barrier()
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_dp2_local_batches_diffrec():
+    """GMR_DP_MODE=local for DiffRec (the Lt-history gather slot must hold a whole batch):
+    two ranks taking whole 16-row batches equal one process with 32-row batches — same global steps,
+    the same importance-sampling history (applied in global row order) and denoiser parameters."""
+    import torch.multiprocessing as mp
+    single = _case_diffrec_local(32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_diffrec_local, args=(r, 2, port, q, 16)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    dp = q.get(timeout=200)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert dp["step"][0] == single["step"][0]
+    np.testing.assert_array_equal(dp["count"], single["count"])
+    np.testing.assert_allclose(dp["hist"], single["hist"], rtol=1e-5, atol=1e-12)
+    np.testing.assert_allclose(dp["loss"], single["loss"], rtol=1e-5)
+    np.testing.assert_allclose(dp["den"], single["den"], rtol=1e-3, atol=2e-5)
+
+
+def _case_genrec():
+    """GenRecV1 (config 5) under the current world size on the tiny golden model: one global BPR step
+    on the golden batch (loss + every rec gradient after the all-reduce) and a Trainer BPR epoch
+    (rec parameters after Adam).  The in-batch InfoNCE keys are the global step's rows."""
+    from genrec_fixture import sub
+    from test_genrec_gpu import build_model, _config
+
+    from gmr import dist
+    from gmr.dataloader import TrainDataLoader
+    from gmr.dataset import RecDataset
+    from gmr.trainer import Trainer
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "genrecv1_tiny.npz"), allow_pickle=False))
+    m = sub(g, "m_")
+    out = {}
+    model, _ = build_model(m)
+    t = lambda k: torch.as_tensor(m[k].astype(np.int32)).to("cuda")  # noqa: E731
+    u, p, n = t("bpr_users"), t("bpr_pos"), t("bpr_neg")
+    B = u.numel()
+    a, b = dist.shard(B)
+    norm, share = dist.dp_scales(dist.shard_sizes(B))
+    gb = (u, p, a) if dist.is_dist() else None
+    loss = model.rec_step(u[a:b], p[a:b], n[a:b], norm_rows=norm, reg_share=share, gbatch=gb).view(1).double()
+    dist.all_reduce_(loss)
+    dist.all_reduce_(model.rec_slab.grad)
+    out["loss"] = loss.cpu().numpy()
+    out["grad"] = model.rec_slab.grad.cpu().numpy().copy()
+    # one BPR epoch through the Trainer (global batch 24 split over the ranks)
+    model2, _ = build_model(m)
+    cfg = _config()
+    U, I = int(m["U"]), int(m["I"])
+    ds = RecDataset.from_arrays(cfg, m["train_rows"], m["train_cols"], np.zeros(len(m["train_rows"])), U, I,
+                                m["v_feat"], m["t_feat"])
+    tl = TrainDataLoader(cfg, ds, batch_size=24)
+    tr = Trainer(cfg, model2)
+    ep_loss, _ = tr._train_epoch(tl, 0)
+    out["epoch_loss"] = np.array([ep_loss])
+    out["params"] = model2.rec_slab.data.cpu().numpy().copy()
+    return out
+
+
+def _worker_genrec(rank, world, port, q):
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "generative-multimodal-recommendation_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, pth)
+    import torch.distributed as tdist
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        res = _case_genrec()
+        if rank == 0:
+            q.put(res)
+        tdist.barrier()
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_dp2_genrecv1_global_batch_infonce():
+    """GenRecV1 data parallel (VERDICT r2 missing #3): with the global batch split over two ranks, each
+    rank's queries meet ALL of the step's keys in the four in-batch InfoNCE terms
+    (models/genrecv1.py:389-414), so the summed loss and the all-reduced gradient are the single
+    process's (the reference's objective) and a Trainer BPR epoch lands on the same parameters."""
+    import torch.multiprocessing as mp
+    single = _case_genrec()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_genrec, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    dp = q.get(timeout=200)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    np.testing.assert_allclose(dp["loss"], single["loss"], rtol=1e-5)
+    sc = float(np.abs(single["grad"]).max())
+    np.testing.assert_allclose(dp["grad"], single["grad"], rtol=2e-4, atol=2e-6 * sc)
+    np.testing.assert_allclose(dp["epoch_loss"], single["epoch_loss"], rtol=1e-5)
+    np.testing.assert_allclose(dp["params"], single["params"], rtol=1e-3, atol=2e-5)

@@ -1,0 +1,198 @@
+"""Config 4 — DiffMM at the Amazon-sports shape (35,598 users x 18,357 items, H = 1,000,
+image 4,096-d, text 384-d) against the reference's own outputs on the same inputs
+(tests/golden/diffmm_sports.npz + diffmm_sports_meta.json, made by `make_golden_baby.py sports`,
+which ran the reference in the build container: models/diffmm.py:14-86, 408-426, 260-278,
+common/trainer.py:369-388, 529-576, utils/topk_evaluator.py:77-120).
+
+The same bar as the baby-shape tests (test_baby_gpu.py), through the HIP path:
+  * D2   parameter initialisation: SHA-256 of every rec and denoiser parameter equals the reference's;
+  * D13/D17 p_sample top-1 of both denoisers over all 35,598 users (near-tie rule);
+  * D9/D19 valid-split top-50 BY POSITION (near-tie rule) and the reference's top-50 scores;
+  * D21  Recall/NDCG/Precision/MAP@{5,10,20,50} unrounded within 1e-4 (north-star bar);
+  * (e)  the data-parallel BPR global step at this shape: two HIP-path ranks (gloo, one GPU) each
+         holding half of a 2,048-row batch give the single process's loss and rec gradient.
+"""
+import hashlib
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from test_baby_gpu import _eval_with_scores, _near_tie_ok, _sha
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEV = "cuda"
+FIX = os.path.join(ROOT, "tests", "golden", "diffmm_sports.npz")
+
+
+def _build(with_eval=True):
+    from gmr.configurator import Config
+    from gmr.dataloader import EvalDataLoader, TrainDataLoader
+    from gmr.quick_start import popularity_groups
+    from gmr.synthetic import make_dataset
+    from gmr.utils import get_model, get_trainer, init_seed
+    cfg = Config("DiffMM", "sports", {"synthetic": "sports", "save_recommended_topk": False, "epochs": 1})
+    ds = make_dataset(cfg, "sports", seed=0)
+    tr, va, te = ds.split()
+    pop, warm, _, _ = popularity_groups(cfg, tr)
+    cfg["pop_items"], cfg["warm_users"] = pop, warm
+    tl = TrainDataLoader(cfg, tr, batch_size=cfg["train_batch_size"], shuffle=True)
+    vl = EvalDataLoader(cfg, va, additional_dataset=tr, batch_size=cfg["eval_batch_size"]) if with_eval else None
+    init_seed(999)
+    model = get_model("DiffMM")(cfg, tl)
+    trainer = get_trainer("DiffMM")(cfg, model)
+    return cfg, tl, vl, model, trainer
+
+
+@pytest.fixture(scope="module")
+def sports():
+    if not os.path.exists(FIX):
+        pytest.fail("tests/golden/diffmm_sports.npz missing (python tests/golden/make_golden_baby.py sports)")
+    cfg, tl, vl, model, trainer = _build()
+    g = dict(np.load(FIX, allow_pickle=False))
+    with open(os.path.join(ROOT, "tests", "golden", "diffmm_sports_meta.json")) as f:
+        meta = json.load(f)
+    assert (model.n_users, model.n_items, tl.n_inter) == (meta["U"], meta["I"], meta["n_train"])
+    return {"cfg": cfg, "tl": tl, "vl": vl, "model": model, "trainer": trainer, "g": g, "meta": meta}
+
+
+def test_sports_init_matches_reference_bit_exact(sports):
+    m, want = sports["model"], sports["meta"]["param_sha256"]
+    s, U = m.rec_slab, m.n_users
+    got = {"uEmbeds": _sha(s.view("E0")[:U]), "iEmbeds": _sha(s.view("E0")[U:]),
+           "image_trans": _sha(s.view("image_trans")), "text_trans": _sha(s.view("text_trans")),
+           "modal_weight": _sha(s.view("modal_weight"))}
+    names = {"emb_layer.weight": "emb_W", "emb_layer.bias": "emb_b", "in_layers.0.weight": "W1",
+             "in_layers.0.bias": "b1", "out_layers.0.weight": "W2", "out_layers.0.bias": "b2"}
+    for mod in ("image", "text"):
+        den = getattr(m, "denoise_model_" + mod).slab
+        for ref_name, ours in names.items():
+            got[f"den_{mod}_{ref_name}"] = _sha(den.view(ours))
+    assert set(got) == set(want)
+    bad = [k for k in want if got[k] != want[k]]
+    assert not bad, f"parameters differing from the reference init: {bad}"
+
+
+def test_sports_p_sample_top1_all_users(sports):
+    from gmr import kernels as K
+    m, g = sports["model"], sports["g"]
+    U = m.n_users
+    for mod in ("image", "text"):
+        den = getattr(m, "denoise_model_" + mod)
+        idx = torch.empty((U, 5), dtype=torch.int32, device=DEV)
+        val = torch.empty((U, 5), dtype=torch.float32, device=DEV)
+        den.refresh_w1t()
+        for lo in range(0, U, 8192):
+            hi = min(U, lo + 8192)
+            xi = m.p_sample_topk(den, lo, hi, None, 1, w1t_fresh=True)
+            K.topk_rows(xi, 5, idx[lo:hi], val[lo:hi])
+        idx, val = idx.cpu().numpy(), val.cpu().numpy()
+        ri, rv = g[f"psample_{mod}_top5_idx"].astype(np.int64), g[f"psample_{mod}_top5_val"]
+        np.testing.assert_allclose(val, rv, rtol=2e-4, atol=2e-5, err_msg=mod)
+        diff = np.nonzero(idx[:, 0] != ri[:, 0])[0]
+        bad = [u for u in diff if not _near_tie_ok(rv[u], ri[u], idx[u, 0], 2e-5)]
+        assert not bad, f"{mod}: top-1 differs outside near ties for {len(bad)} users (first {bad[:5]})"
+        assert len(diff) <= max(5, U // 1000), f"{mod}: {len(diff)} near-tie top-1 swaps"
+
+
+def _ref_graphs(m, g):
+    """UI graphs from the reference's top-1 edges (trainer.py:545-576 with the reference's picks)."""
+    from gmr import kernels as K
+    U, I = m.n_users, m.n_items
+    for mod in ("image", "text"):
+        top = torch.as_tensor(g[f"psample_{mod}_top5_idx"][:, :1].astype(np.int32)).to(DEV)
+        uptr = torch.empty(U + 1, dtype=torch.int32, device=DEV)
+        uitems = torch.empty(U, dtype=torch.int32, device=DEV)
+        K.topk_to_user_csr(top, uptr, uitems)
+        setattr(m, mod + "_UI_matrix", K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0))
+
+
+def test_sports_valid_topk_by_position_and_metrics(sports):
+    m, g, tr, vl = sports["model"], sports["g"], sports["trainer"], sports["vl"]
+    _ref_graphs(m, g)
+    out, scores = _eval_with_scores(m, vl, keep_scores=True)
+    ours = out.cpu().numpy().astype(np.int64)
+    ref = g["valid_top50"].astype(np.int64)
+    assert ours.shape == ref.shape
+    S = g["valid_top50_val_sample"].shape[0]
+    mine = np.take_along_axis(scores[:S], ref[:S], 1)
+    np.testing.assert_allclose(mine, g["valid_top50_val_sample"], rtol=1e-5, atol=1e-6)
+    r, c = np.nonzero(ours != ref)
+    s_o = scores[r, ours[r, c]]
+    s_r = scores[r, ref[r, c]]
+    tie = np.abs(s_o - s_r) <= 1e-6 * np.maximum(np.abs(s_o), 1e-3)
+    assert tie.all(), (f"{int((~tie).sum())} top-50 positions differ outside near ties "
+                       f"(first rows {np.unique(r[~tie])[:5]}); {len(r)} differing positions in all")
+    del scores
+    sums = tr.evaluator.device_sums(out, vl).cpu().numpy().reshape(4, 8)
+    n = out.shape[0]
+    raw = sports["meta"]["valid"]["raw"]
+    for j, name in enumerate(["recall", "ndcg", "precision", "map"]):
+        for q, k in enumerate([5, 10, 20, 50]):
+            assert abs(sums[j, q] / n - raw[name][k - 1]) <= 1e-4, (name, k, sums[j, q] / n, raw[name][k - 1])
+    res = tr.evaluator.evaluate_device(out, vl)
+    for k, v in sports["meta"]["valid"]["rounded"].items():
+        assert abs(res[k] - v) <= 1.01e-4, (k, res[k], v)
+
+
+# ---------------------------------------------------------------------------- data parallel at this shape
+def _dp_case():
+    """One BPR global step (calculate_loss + backward) at the sports shape on the first 2,048-row
+    batch of the epoch draw, this rank's share of it; loss and rec gradient after the all-reduce."""
+    from gmr import dist
+    _, tl, _, m, _ = _build(with_eval=False)
+    _ref_graphs(m, dict(np.load(FIX, allow_pickle=False)))
+    d = tl.epoch(with_plans=False)
+    B = tl.batch_size
+    u, p, n = (d["sample"][j, :B].contiguous() for j in range(3))
+    a, b = dist.shard(B)
+    norm, share = dist.dp_scales(dist.shard_sizes(B))
+    loss = m.rec_step(u[a:b], p[a:b], n[a:b], norm_rows=norm, reg_share=share).view(1).double()
+    dist.all_reduce_(loss)
+    dist.all_reduce_(m.rec_slab.grad)
+    return {"loss": loss.cpu().numpy(), "grad": m.rec_slab.grad.cpu().numpy().copy()}
+
+
+def _worker(rank, world, port, q):
+    import sys
+    for pth in (ROOT, os.path.join(ROOT, "generative-multimodal-recommendation_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, pth)
+    import torch.distributed as tdist
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        res = _dp_case()
+        if rank == 0:
+            q.put(res)
+        tdist.barrier()
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+def test_sports_dp2_rec_step_equals_single_process():
+    import torch.multiprocessing as mp
+    if not os.path.exists(FIX):
+        pytest.fail("tests/golden/diffmm_sports.npz missing")
+    single = _dp_case()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    dp = q.get(timeout=360)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    np.testing.assert_allclose(dp["loss"], single["loss"], rtol=1e-5)
+    sc = float(np.abs(single["grad"]).max())
+    np.testing.assert_allclose(dp["grad"], single["grad"], rtol=1e-4, atol=2e-6 * sc)
