@@ -26,18 +26,16 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int x6_swz(int r) { return (r >> 2) & 3; }
 
-// Edge values: a finite |x| at or above the last bf16 that rounds below bf16's max
-// (0x1.fep127 + half an ulp) would round hi to inf, so it takes hi by truncation instead (exact, no
-// overflow); inf / NaN pass through as hi with mid = lo = 0, so the product is what fp32 gives.
+// Edge values: rounding a finite |x| above bf16's largest value (0x1.fep127) to bf16 gives
+// inf and then NaN terms, so x is clamped into bf16's range first (one v_med3_f32): hi = +-0x1.fep127
+// exactly and x - hi (same binade, Sterbenz) is exact, so the split stays exact up to FLT_MAX.  An inf
+// operand still splits into hi = 0x1.fep127, mid = inf, lo = NaN: its products come out non-finite
+// (NaN where fp32 gives inf), as an inf input to the fp32 kernel does.
 __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
-  const float ax = fabsf(x);
-  const bool finite = ax <= 0x1.fffffep127f;  // false for inf and NaN
-  const float hf = (finite && ax >= 0x1.ff0000p127f) ? __uint_as_float(__float_as_uint(x) & 0xffff0000u)
-                                                      : (float)(__bf16)x;
-  h = (__bf16)hf;                                  // exact: hf is a bf16 value (inf / NaN pass through)
-  const float r1 = finite ? x - hf : 0.f;          // exact; 0 for inf / NaN
+  h = (__bf16)__builtin_amdgcn_fmed3f(x, -0x1.fep127f, 0x1.fep127f);
+  const float r1 = x - (float)h;  // exact
   m = (__bf16)r1;
-  l = (__bf16)(r1 - (float)m);                     // exact: at most 8 significand bits remain
+  l = (__bf16)(r1 - (float)m);    // exact: at most 8 significand bits remain
 }
 
 // register tile -> the three bf16 planes of one LDS stage (plane stride PL elements)

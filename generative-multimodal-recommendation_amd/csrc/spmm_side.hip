@@ -13,23 +13,27 @@
 //     x 2 sides = one group per XCD; d = 64: 2 XCDs per group; d = 256: two phases per XCD).  An
 //     XCD's L2 then holds only the OTHER side's 128-byte slice of X (items 7,050 x 128 B = 0.9 MB,
 //     users 19,445 x 128 B = 2.5 MB at baby) and every gather is ONE whole line;
-//   * entry-stream tasks: each side's CSR entries are cut, at row boundaries, into tasks of <= T
-//     consecutive entries (several whole rows); a lane group of 8 lanes (32 columns = 8 x float4)
-//     streams a task EB entries at a time with the next EB (col, val) pairs in flight, crossing row
-//     ends inside the stream (a packed entry carries a row-end bit), so no per-row descriptor round
-//     trip and no idle gather slots on short rows;
-//   * hub rows (degree > T: the Zipf-popular items) are cut into pieces of <= T entries, each an
-//     ordinary task whose sum goes to a partial row (write-through sc1 stores); the lane group whose
-//     agent-scope counter add comes last sums the pieces IN PIECE ORDER (sc1 loads) and writes the row,
-//     then re-arms the counter: one launch, deterministic sums (the MI355X_MICROARCH.md hand-off form
-//     "agent-scope atomic add ... the workgroup whose add came last ... sc1 stores and loads");
-//   * a short-row entry sum runs in CSR order from zero (acc = fma(v, x, acc)), the order of the lane
-//     plan's short rows; hub rows add their pieces in order.
+//   * entry-stream tasks: each side's rows of degree <= T are cut, at row boundaries, into tasks of
+//     <= T consecutive CSR entries (several whole rows); a lane group of 8 lanes (32 columns = 8 x
+//     float4) streams a task EB entries at a time, the next EB (col, val) pairs (and after the last
+//     round the NEXT task's first ones) in flight while the gathers land, crossing row ends inside
+//     the stream (a packed entry carries a row-end bit): no per-row descriptor round trip and no idle
+//     gather slots on short rows;
+//   * hub rows (degree > T: the Zipf-popular items) are wave tasks, longest first: blocks of <= 8 TW
+//     entries whose 8 lane groups split the block evenly and meet in a xor butterfly.  A row of
+//     several blocks publishes each block sum write-through (sc1); the WAVE whose agent-scope counter
+//     add comes last loads all block sums (sc1, 8 lane groups in parallel), adds them in a fixed order
+//     and writes the row, then re-arms the counter (the MI355X_MICROARCH.md hand-off form "agent-scope
+//     atomic add ... the workgroup whose add came last ... sc1 stores and loads").  One launch; a
+//     one-lane-group serial combine of many pieces was the tail (profiles/r03b_sweep.txt);
+//   * a short row's sum runs in CSR order from zero (acc = fma(v, x, acc)), the order of the lane
+//     plan's short rows; a hub row's sum order is fixed by its plan: deterministic.
 // Plan (int32 words, built on the host by gmr_spmm_side_plan_build, entries packed on the device by
-// gmr_spmm_side_pack): header[16], tasks int4 {beg, end, first row, slot | -1} (side 0 then side 1),
-// empty rows, hubs int4 {row, first slot, pieces, 0}, slot -> hub, packed int2 {col | last << 31, val}.
-// Scratch (caller-owned, zeroed once): kSideCounters ints of per-(hub, slice) counters, then one
-// 256-float partial row per slot.
+// gmr_spmm_side_pack): header[32], lane tasks int4 {beg, end, first row, -1} (side 0 then side 1),
+// wave tasks int4 {beg, end, row, slot | -1}, empty rows, hubs int4 {row, first slot, blocks, 0},
+// slot -> hub, packed int2 {col | last << 31, val}.
+// Scratch (caller-owned, zeroed once): per-(hub, slice) counters, then one 256-float partial row
+// per slot.
 #include <stdlib.h>
 
 #include <algorithm>
@@ -39,13 +43,13 @@
 
 namespace {
 
-constexpr int kSideHdr = 16;
-constexpr int kSideMagic = 0x53494445;  // 'SIDE'
+constexpr int kSideHdr = 32;
+constexpr int kSideMagic = 0x53494446;  // 'SIDF'
 constexpr int kSideThreads = 256;
 constexpr int64_t kSideCounterWords = 8;  // counters per hub (one per 32-column slice, d <= 256)
 
 enum { H_MAGIC, H_NROWS, H_SPLIT, H_T, H_TASK, H_NT0, H_NT1, H_EMPTY, H_NE0, H_NE1, H_HUB, H_NHUB, H_SLOT, H_NSLOT,
-       H_PACKED, H_NNZ };
+       H_PACKED, H_NNZ, H_WAVE, H_NW0, H_NW1, H_TW };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -63,6 +67,13 @@ struct SideDst {
 };
 
 __device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ float4 shx(float4 v, int m) { return gmr::shfl_xor_f4(v, m); }
+// sum over the 8 lane groups of a wave (xor butterfly: every group ends with the same bits)
+__device__ __forceinline__ float4 wave_groups_sum(float4 a) {
+  a = gmr::f4_add(a, shx(a, 8));
+  a = gmr::f4_add(a, shx(a, 16));
+  return gmr::f4_add(a, shx(a, 32));
+}
 
 // NS = 32-column slices of the product (d = 32 NS), EB = entries in flight per lane group
 template <int EB, int NS>
@@ -73,11 +84,13 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
   constexpr int PHASES = G > 8 ? G / 8 : 1;    // groups per XCD, one after the other
   constexpr int P = G >= 8 ? 1 : 8 / G;        // XCDs per group
   constexpr int EPL = EB / 8;                  // packed entries per lane per round
+  constexpr int NWV = kSideThreads / 64;       // waves per workgroup
   const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int grp = lane >> 3, sub = lane & 7, gbase = grp * 8;
   const int* hdr = plan;
   const int4* __restrict__ tasks = reinterpret_cast<const int4*>(plan + hdr[H_TASK]);
+  const int4* __restrict__ wtasks = reinterpret_cast<const int4*>(plan + hdr[H_WAVE]);
   const int* __restrict__ empty = plan + hdr[H_EMPTY];
   const int4* __restrict__ hubs = reinterpret_cast<const int4*>(plan + hdr[H_HUB]);
   const int* __restrict__ slotmap = plan + hdr[H_SLOT];
@@ -98,8 +111,6 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
     const int64_t ldl = src.ld_lo[blk], ldh = src.ld_hi[blk];
     float* __restrict__ yc = dst.y[blk] + cin;
     const int64_t ldy = dst.ld[blk];
-    const int n_lg = P * wpx * (kSideThreads / 8);
-    const int lg = (part_i * wpx + k) * (kSideThreads / 8) + wid * 8 + grp;
     auto store = [&](int row, float4 acc) {
       float* yp = yc + (int64_t)row * ldy;
       float4 o = gmr::f4_scale(alpha, acc);
@@ -111,48 +122,124 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
         *reinterpret_cast<float4*>(yp) = o;
       }
     };
-    // empty rows of this side: Y = beta Y (alpha A X is zero there)
-    const int e0 = side == 0 ? 0 : hdr[H_NE0], ne = side == 0 ? hdr[H_NE0] : hdr[H_NE1];
-    for (int i = lg; i < ne; i += n_lg) store(empty[e0 + i], f4_zero());
-    const int t0 = side == 0 ? 0 : hdr[H_NT0], ntk = side == 0 ? hdr[H_NT0] : hdr[H_NT1];
+    auto gather = [&](int c) -> float4 {
+      return *reinterpret_cast<const float4*>(c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh);
+    };
+    // ---- hub rows (degree > T): wave tasks, longest first.  The 8 lane groups split the block's
+    // entries evenly and meet in a butterfly; a row of several blocks publishes each block sum
+    // write-through and the wave whose counter add comes last adds the blocks in order.
+    {
+      const int n_wv = P * wpx * NWV, wv = (part_i * wpx + k) * NWV + wid;
+      const int w0 = side == 0 ? 0 : hdr[H_NW0], nwk = side == 0 ? hdr[H_NW0] : hdr[H_NW1];
 #pragma unroll 1
-    for (int ti = lg; ti < ntk; ti += n_lg) {
-      const int4 tk = tasks[t0 + ti];
+      for (int wi = wv; wi < nwk; wi += n_wv) {
+        const int4 tk = wtasks[w0 + wi];
+        const int pl = (tk.y - tk.x + 7) >> 3;
+        const int b = tk.x + grp * pl, end = min(tk.y, b + pl);
+        float4 acc = f4_zero();
+        int2 rec[EPL];
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+          const int i = b + q * 8 + sub;
+          rec[q] = i < end ? packed[i] : make_int2(0, 0);
+        }
+#pragma unroll 1
+        for (int e = b; e < end; e += EB) {
+          float4 xs[EB];
+          int2 cur[EPL];  // this round's entries: their values are shuffled out again at the FMAs
+#pragma unroll
+          for (int u = 0; u < EB; ++u) {
+            const int c = __shfl(rec[u / 8].x, gbase + u % 8) & 0x7fffffff;
+            xs[u] = f4_zero();
+            if (e + u < end) xs[u] = gather(c);
+          }
+#pragma unroll
+          for (int q = 0; q < EPL; ++q) {
+            cur[q] = rec[q];
+            const int i = e + EB + q * 8 + sub;
+            rec[q] = i < end ? packed[i] : make_int2(0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < EB; ++u)
+            if (e + u < end) acc = gmr::f4_fma(__int_as_float(__shfl(cur[u / 8].y, gbase + u % 8)), xs[u], acc);
+        }
+        acc = wave_groups_sum(acc);
+        if (tk.w < 0) {
+          if (grp == 0) store(tk.z, acc);
+          continue;
+        }
+        if (grp == 0) {
+          f32x4 pv = {acc.x, acc.y, acc.z, acc.w};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pv), prs, (tk.w * 256 + c0) * 4, 0, 16);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int h = slotmap[tk.w];
+        const int4 hb = hubs[h];
+        int* cnt = counters + (int64_t)h * kSideCounterWords + slice;
+        int old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = __shfl(old, 0);
+        if (old == hb.z - 1) {  // last block of the row: every block sum is published
+          float4 s = f4_zero();
+          for (int j = grp; j < hb.z; j += 8) {
+            const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(prs, ((hb.y + j) * 256 + c0) * 4, 0, 16);
+            const f32x4 f = __builtin_bit_cast(f32x4, r);
+            s = gmr::f4_add(s, make_float4(f.x, f.y, f.z, f.w));
+          }
+          s = wave_groups_sum(s);
+          if (grp == 0) store(hb.x, s);
+          if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    // ---- short rows: lane-group tasks of <= T entries (whole rows), the next task's descriptor and
+    // first entries in flight while the current one gathers
+    // lane groups numbered from the last wave down: the waves that took hub blocks (numbered from the
+    // first wave up) get short-row tasks last
+    const int n_lg = P * wpx * (kSideThreads / 8);
+    const int lg = n_lg - 1 - ((part_i * wpx + k) * (kSideThreads / 8) + wid * 8 + grp);
+    const int e0 = side == 0 ? 0 : hdr[H_NE0], ne = side == 0 ? hdr[H_NE0] : hdr[H_NE1];
+    for (int i = lg; i < ne; i += n_lg) store(empty[e0 + i], f4_zero());  // Y = beta Y on empty rows
+    const int t0 = side == 0 ? 0 : hdr[H_NT0], ntk = side == 0 ? hdr[H_NT0] : hdr[H_NT1];
+    int ti = lg;
+    int4 tk = ti < ntk ? tasks[t0 + ti] : make_int4(0, 0, 0, 0);
+    int2 rec[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+      const int i = tk.x + q * 8 + sub;
+      rec[q] = i < tk.y ? packed[i] : make_int2(0, 0);
+    }
+#pragma unroll 1
+    while (ti < ntk) {
+      const int tn = ti + n_lg;
+      const int4 tkn = tn < ntk ? tasks[t0 + tn] : make_int4(0, 0, 0, 0);
       const int end = tk.y;
       int row = tk.z;
-      const bool piece = tk.w >= 0;
       float4 acc = f4_zero();
-      int2 rec[EPL];
-#pragma unroll
-      for (int q = 0; q < EPL; ++q) {
-        const int i = tk.x + q * 8 + sub;
-        rec[q] = i < end ? packed[i] : make_int2(0, 0);
-      }
 #pragma unroll 1
       for (int e = tk.x; e < end; e += EB) {
         float4 xs[EB];
-        float vs[EB];
-        int cs[EB];
+        int2 cur[EPL];  // this round's entries: col (row-end bit) and val are shuffled out again at the FMAs
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-          cs[u] = __shfl(rec[u / 8].x, gbase + u % 8);
-          vs[u] = __int_as_float(__shfl(rec[u / 8].y, gbase + u % 8));
-          const int c = cs[u] & 0x7fffffff;
           xs[u] = f4_zero();
-          if (e + u < end)
-            xs[u] = *reinterpret_cast<const float4*>(c < split ? lo + (int64_t)c * ldl : hi + (int64_t)(c - split) * ldh);
+          if (e + u < end) xs[u] = gather(__shfl(rec[u / 8].x, gbase + u % 8) & 0x7fffffff);
         }
-        const int en = e + EB;  // the next round's entries travel while these gathers land
+        // the next round's entries (the next task's first ones after the last round) travel while
+        // these gathers land
+        const bool last = e + EB >= end;
+        const int nb = last ? tkn.x : e + EB, nend = last ? tkn.y : end;
 #pragma unroll
         for (int q = 0; q < EPL; ++q) {
-          const int i = en + q * 8 + sub;
-          rec[q] = i < end ? packed[i] : make_int2(0, 0);
+          cur[q] = rec[q];
+          const int i = nb + q * 8 + sub;
+          rec[q] = i < nend ? packed[i] : make_int2(0, 0);
         }
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
           if (e + u < end) {
-            acc = gmr::f4_fma(vs[u], xs[u], acc);
-            if (cs[u] < 0 && !piece) {  // row end inside a whole-row task
+            acc = gmr::f4_fma(__int_as_float(__shfl(cur[u / 8].y, gbase + u % 8)), xs[u], acc);
+            if (__shfl(cur[u / 8].x, gbase + u % 8) < 0) {  // row end
               store(row, acc);
               ++row;
               acc = f4_zero();
@@ -160,31 +247,8 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
           }
         }
       }
-      if (piece) {
-        // hub piece: partial row tk.w, write-through; the last arriving piece of (hub, slice) adds
-        // all pieces in order and writes the row
-        const int slot = tk.w;
-        f32x4 pv = {acc.x, acc.y, acc.z, acc.w};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pv), prs, (slot * 256 + c0) * 4, 0, 16);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int h = slotmap[slot];
-        const int4 hb = hubs[h];
-        int* cnt = counters + (int64_t)h * kSideCounterWords + slice;
-        int old = 0;
-        if (sub == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        old = __shfl(old, gbase);
-        if (old == hb.z - 1) {
-          float4 s = f4_zero();
-#pragma unroll 4
-          for (int j = 0; j < hb.z; ++j) {
-            const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(prs, ((hb.y + j) * 256 + c0) * 4, 0, 16);
-            const f32x4 f = __builtin_bit_cast(f32x4, r);
-            s = gmr::f4_add(s, make_float4(f.x, f.y, f.z, f.w));
-          }
-          store(hb.x, s);
-          if (sub == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
+      tk = tkn;
+      ti = tn;
     }
   }
 }
@@ -201,11 +265,13 @@ __global__ void __launch_bounds__(256) side_pack_kernel(const int* __restrict__ 
 }
 
 struct SidePlanHost {
-  std::vector<int4> tasks[2], hubs;
+  std::vector<int4> tasks[2], waves[2], hubs;
   std::vector<int> empty[2], slotmap;
 };
 
-void side_plan_host(const int32_t* rp, int64_t n_rows, int64_t split, int T, SidePlanHost& p) {
+// rows of degree <= T: lane-group tasks of <= T entries (whole rows, cut at empty rows); longer rows:
+// wave tasks of <= 8 TW entries (blocks), a row of several blocks gets a hub record and slots
+void side_plan_host(const int32_t* rp, int64_t n_rows, int64_t split, int T, int TW, SidePlanHost& p) {
   int slot = 0;
   for (int s = 0; s < 2; ++s) {
     const int64_t r0 = s == 0 ? 0 : split, r1 = s == 0 ? split : n_rows;
@@ -222,14 +288,18 @@ void side_plan_host(const int32_t* rp, int64_t n_rows, int64_t split, int T, Sid
         p.empty[s].push_back((int)r);
       } else if (deg > T) {
         flush();
-        const int pieces = (deg + T - 1) / T, pl = (deg + pieces - 1) / pieces;
+        const int blocks = (deg + 8 * TW - 1) / (8 * TW), bl = (deg + blocks - 1) / blocks;
+        if (blocks == 1) {
+          p.waves[s].push_back(make_int4(b, e, (int)r, -1));
+          continue;
+        }
         const int h = (int)p.hubs.size();
-        p.hubs.push_back(make_int4((int)r, slot, pieces, 0));
-        for (int j = 0; j < pieces; ++j) {
-          p.tasks[s].push_back(make_int4(b + j * pl, std::min(e, b + (j + 1) * pl), (int)r, slot + j));
+        p.hubs.push_back(make_int4((int)r, slot, blocks, 0));
+        for (int j = 0; j < blocks; ++j) {
+          p.waves[s].push_back(make_int4(b + j * bl, std::min(e, b + (j + 1) * bl), (int)r, slot + j));
           p.slotmap.push_back(h);
         }
-        slot += pieces;
+        slot += blocks;
       } else {
         if (cnt + deg > T) flush();
         if (beg < 0) {
@@ -241,18 +311,21 @@ void side_plan_host(const int32_t* rp, int64_t n_rows, int64_t split, int T, Sid
       }
     }
     flush();
+    std::stable_sort(p.waves[s].begin(), p.waves[s].end(),
+                     [](const int4& a, const int4& c) { return a.y - a.x > c.y - c.x; });  // longest first
   }
 }
 
 int64_t r4(int64_t v) { return (v + 3) / 4 * 4; }
 
 struct SideLayout {
-  int64_t task, empty, hub, slot, packed, words;
+  int64_t task, wave, empty, hub, slot, packed, words;
 };
 SideLayout side_layout(const SidePlanHost& p, int64_t nnz) {
   SideLayout l;
   l.task = kSideHdr;
-  l.empty = l.task + 4 * (int64_t)(p.tasks[0].size() + p.tasks[1].size());
+  l.wave = l.task + 4 * (int64_t)(p.tasks[0].size() + p.tasks[1].size());
+  l.empty = l.wave + 4 * (int64_t)(p.waves[0].size() + p.waves[1].size());
   l.hub = r4(l.empty + (int64_t)(p.empty[0].size() + p.empty[1].size()));
   l.slot = l.hub + 4 * (int64_t)p.hubs.size();
   l.packed = r4(l.slot + (int64_t)p.slotmap.size());
@@ -260,21 +333,24 @@ SideLayout side_layout(const SidePlanHost& p, int64_t nnz) {
   return l;
 }
 
-int side_wpx() {  // workgroups per XCD (GMR_SPMM_SIDE_WPX overrides, for tuning)
-  static const int v = [] {
+// launch shape: workgroups per XCD and entries in flight per lane group (GMR_SPMM_SIDE_WPX /
+// GMR_SPMM_SIDE_EB at first use; gmr_spmm_side_tune sets them at run time, for sweeps)
+int g_side_wpx = -1, g_side_eb = -1;
+bool g_side_tuned = false;  // gmr_spmm_side_tune overrides the caller's per-graph wpx
+int side_wpx() {
+  if (g_side_wpx < 0) {
     const char* s = getenv("GMR_SPMM_SIDE_WPX");
     const int x = s ? atoi(s) : 0;
-    return x > 0 && x <= 1024 ? x : 64;
-  }();
-  return v;
+    g_side_wpx = x > 0 && x <= 1024 ? x : 64;
+  }
+  return g_side_wpx;
 }
-
-int side_eb() {  // entries in flight per lane group (GMR_SPMM_SIDE_EB = 8 or 16)
-  static const int v = [] {
+int side_eb() {
+  if (g_side_eb < 0) {
     const char* s = getenv("GMR_SPMM_SIDE_EB");
-    return s && atoi(s) == 8 ? 8 : 16;
-  }();
-  return v;
+    g_side_eb = s && atoi(s) == 8 ? 8 : 16;
+  }
+  return g_side_eb;
 }
 
 int side_nt() {  // non-temporal Y stores (GMR_SPMM_NT semantics: 0 = plain)
@@ -298,20 +374,35 @@ void side_launch(int eb, const int* plan, const SideSrc& src, float alpha, float
 
 }  // namespace
 
-extern "C" int64_t gmr_spmm_side_plan_words(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t T) {
-  if (!rowptr_host || n_rows <= 0 || split < 0 || split > n_rows || T < 8 || T > 4096) return -1;
+extern "C" int gmr_spmm_side_tune(int32_t wpx, int32_t eb) {
+  GMR_ARG(wpx > 0 && wpx <= 1024 && (eb == 8 || eb == 16), "wpx in [1, 1024], eb 8 or 16");
+  g_side_wpx = wpx;
+  g_side_eb = eb;
+  g_side_tuned = true;
+  return GMR_OK;
+}
+
+// T argument: bits 0-15 = T (entries of a short-row task, rows of degree > T are hub rows), bits
+// 16-23 = TW (entries per lane group of a hub block: blocks of 8 TW; 0 = 32)
+inline int side_T(int32_t Tw) { return Tw & 0xFFFF; }
+inline int side_TW(int32_t Tw) { return (Tw >> 16) & 0xFF ? (Tw >> 16) & 0xFF : 32; }
+
+extern "C" int64_t gmr_spmm_side_plan_words(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t Tw) {
+  const int T = side_T(Tw), TW = side_TW(Tw);
+  if (!rowptr_host || n_rows <= 0 || split < 0 || split > n_rows || T < 8 || T > 4096 || TW < 4) return -1;
   SidePlanHost p;
-  side_plan_host(rowptr_host, n_rows, split, T, p);
+  side_plan_host(rowptr_host, n_rows, split, T, TW, p);
   return side_layout(p, rowptr_host[n_rows]).words;
 }
 
-extern "C" int gmr_spmm_side_plan_build(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t T,
+extern "C" int gmr_spmm_side_plan_build(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t Tw,
                                         int32_t* plan_host, int64_t words) {
+  const int T = side_T(Tw), TW = side_TW(Tw);
   GMR_ARG(rowptr_host && plan_host && n_rows > 0 && split >= 0 && split <= n_rows, "bad args");
-  GMR_ARG(T >= 8 && T <= 4096, "T must be in [8, 4096]");
+  GMR_ARG(T >= 8 && T <= 4096 && TW >= 4, "T must be in [8, 4096], TW >= 4");
   GMR_ARG(n_rows < (1 << 30) && rowptr_host[n_rows] < (1ll << 31) - 1, "too large for int32 plans");
   SidePlanHost p;
-  side_plan_host(rowptr_host, n_rows, split, T, p);
+  side_plan_host(rowptr_host, n_rows, split, T, TW, p);
   const int64_t nnz = rowptr_host[n_rows];
   const SideLayout l = side_layout(p, nnz);
   GMR_ARG(words >= l.words, "plan buffer smaller than gmr_spmm_side_plan_words(...)");
@@ -332,9 +423,16 @@ extern "C" int gmr_spmm_side_plan_build(const int32_t* rowptr_host, int64_t n_ro
   h[H_NSLOT] = (int)p.slotmap.size();
   h[H_PACKED] = (int)l.packed;
   h[H_NNZ] = (int)nnz;
+  h[H_WAVE] = (int)l.wave;
+  h[H_NW0] = (int)p.waves[0].size();
+  h[H_NW1] = (int)p.waves[1].size();
+  h[H_TW] = TW;
+  for (int i = H_TW + 1; i < kSideHdr; ++i) h[i] = 0;
   int4* t = reinterpret_cast<int4*>(h + l.task);
   for (int s = 0; s < 2; ++s)
     for (const int4& x : p.tasks[s]) *t++ = x;
+  for (int s = 0; s < 2; ++s)
+    for (const int4& x : p.waves[s]) *t++ = x;
   int* e = h + l.empty;
   for (int s = 0; s < 2; ++s)
     for (int r : p.empty[s]) *e++ = r;
@@ -364,8 +462,9 @@ extern "C" int gmr_spmm_side_pack(const int32_t* rowptr, const int32_t* col, con
 
 extern "C" int gmr_spmm_side_f32(const int32_t* plan, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
                                  const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
-                                 float* const* y, const int64_t* ld_y, float* scratch, void* stream) {
+                                 float* const* y, const int64_t* ld_y, float* scratch, int32_t wpx, void* stream) {
   GMR_ARG(plan && scratch && x_lo && ld_lo && x_hi && ld_hi && y && ld_y, "null argument");
+  GMR_ARG(wpx >= 0 && wpx <= 1024, "wpx in [0, 1024] (0 = default)");
   GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "1, 2 or 4 blocks of 64 columns");
   SideSrc s;
   SideDst d;
@@ -386,7 +485,8 @@ extern "C" int gmr_spmm_side_f32(const int32_t* plan, int32_t n_blocks, const fl
   }
   s.split = split;
   const hipStream_t st = (hipStream_t)stream;
-  const int eb = side_eb(), wpx = side_wpx(), nt = side_nt();
+  const int eb = side_eb(), nt = side_nt();
+  if (wpx == 0 || getenv("GMR_SPMM_SIDE_WPX") || g_side_tuned) wpx = side_wpx();
   if (n_blocks == 1)
     side_launch<2>(eb, plan, s, alpha, beta, d, scratch, wpx, nt, st);
   else if (n_blocks == 2)

@@ -263,7 +263,10 @@ SPMM_CHUNK = 1 << 18  # chunk plan: whole-row tasks of <= 128 entries, one gathe
 # adjacencies): each XCD serves one (side, 32-column slice), lane groups stream <= SPMM_SIDE_T-entry
 # tasks, hub rows combine in-launch.  GMR_SPMM_SIDE=0 keeps every product on the lane plans (A/B)
 SPMM_SIDE = os.environ.get("GMR_SPMM_SIDE", "1") == "1"
-SPMM_SIDE_T = int(os.environ.get("GMR_SPMM_SIDE_T", "64"))
+# short-row task entries: 16 for the rebuilt UI graphs (average degree ~2.5: many small tasks), 32 for
+# norm_adj (average degree ~9); GMR_SPMM_SIDE_T overrides (profiles/r03b_sweep.txt)
+SPMM_SIDE_T = int(os.environ.get("GMR_SPMM_SIDE_T", "0"))
+SPMM_SIDE_TW = int(os.environ.get("GMR_SPMM_SIDE_TW", "32"))
 
 
 class CSR:
@@ -306,7 +309,11 @@ class CSR:
         scratch (zeroed: its hub counters re-arm themselves after every launch)."""
         import numpy as np
         lib = _lib.load()
-        T = SPMM_SIDE_T if T is None else T
+        if T is None:
+            T = SPMM_SIDE_T or (16 if self.nnz < 4 * self.n_rows else 32)
+        T = int(T)
+        if not T >> 16:
+            T |= SPMM_SIDE_TW << 16
         rp = np.ascontiguousarray(self.rowptr.cpu().numpy().astype(np.int32))
         rpp = rp.ctypes.data_as(ctypes.c_void_p)
         words = int(lib.gmr_spmm_side_plan_words(rpp, self.n_rows, int(split), int(T)))
@@ -321,6 +328,10 @@ class CSR:
                   int(host[14]), ptr(plan), stream())
         nsc = int(lib.gmr_spmm_side_scratch_floats(host.ctypes.data_as(ctypes.c_void_p)))
         self.side = (plan, int(split))
+        # workgroups per XCD by product width (profiles/r03b_sweep.txt): the short-task UI graphs and
+        # the 64-column products fill the XCDs with 128, the wider norm_adj products with 256
+        short = self.nnz < 4 * self.n_rows
+        self.side_wpx = {1: 128, 2: 128 if short else 256, 4: 128 if short else 256}
         self.side_hdr = tuple(int(x) for x in host[:16])
         self.partial = torch.zeros(max(nsc, self.partial.numel()), dtype=torch.float32, device=dev)
 
@@ -365,7 +376,7 @@ def _side_call(self, nb, lo, ldl, hi, ldh, split, alpha, beta, ys, ldy, partial)
     """gmr_spmm_side_f32 with host arrays of block pointers / strides (CSR.spmm, spmm_multi, spmm_jobs)."""
     with _Probe("spmm", (self.nnz, self.n_rows, self.n_cols, nb, beta != 0.0)):
         _lib.call("gmr_spmm_side_f32", ptr(self.side[0]), nb, lo, ldl, hi, ldh, int(split), float(alpha), float(beta),
-                  ys, ldy, ptr(self.partial if partial is None else partial), stream())
+                  ys, ldy, ptr(self.partial if partial is None else partial), self.side_wpx[nb], stream())
 
 
 CSR._side_call = _side_call

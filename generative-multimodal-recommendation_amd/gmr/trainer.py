@@ -94,6 +94,7 @@ class Trainer:
                     # in-batch terms see the whole global step (GenRecV1's B x B InfoNCE keys)
                     loss = self.model.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share,
                                                gbatch=train_data.step_rows(d, b))
+                    _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
                 else:
                     loss = self._rec_step(u, p, ng, pb, pc, norm, share, sum(rank_rows[:dist.rank()]))
                     _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())

@@ -161,15 +161,21 @@ int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream);
  * concurrently need separate scratch.  Y = alpha A X + beta Y with X / Y as gmr_spmm_multi_f32's
  * per-block split sources / outputs (16-byte aligned, strides multiples of 4).  A short row's sum
  * is its entries in CSR order; a hub row adds its pieces in piece order: deterministic. */
+/* T: bits 0-15 = entries per short-row task (rows of degree > T are hub rows), bits 16-23 = entries
+ * per lane group of a hub block (blocks of 8 x that; 0 = 32) */
 int64_t gmr_spmm_side_plan_words(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t T);
 int gmr_spmm_side_plan_build(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t T, int32_t* plan_host,
                              int64_t words);
 int64_t gmr_spmm_side_scratch_floats(const int32_t* plan_host);
 int gmr_spmm_side_pack(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                        int64_t packed_off, int32_t* plan, void* stream);
+/* launch shape for tuning sweeps: workgroups per XCD and entries in flight per lane group (8 / 16);
+ * defaults GMR_SPMM_SIDE_WPX / GMR_SPMM_SIDE_EB (64 / 16) */
+int gmr_spmm_side_tune(int32_t wpx, int32_t eb);
+/* wpx: workgroups per XCD of the launch (0 = GMR_SPMM_SIDE_WPX or 64); gmr_spmm_side_tune overrides it */
 int gmr_spmm_side_f32(const int32_t* plan, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
                       const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
-                      float* const* y_blocks, const int64_t* ld_y, float* scratch, void* stream);
+                      float* const* y_blocks, const int64_t* ld_y, float* scratch, int32_t wpx, void* stream);
 
 int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                      const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,

