@@ -57,8 +57,8 @@ KERNEL_NAMES = {"gemm": "gemm_glds_kernel (fp32 MFMA v_mfma_f32_32x32x2_f32, glo
                 "gemm_x6": "gemm_x6_kernel (fp32 operands split exactly into three bf16 terms, six "
                            "v_mfma_f32_32x32x16_bf16 products accumulated in fp32: fp32-accurate NT products)",
                 "infonce": "cl_rows_kernel + cl_table_kernel (fused InfoNCE, fp32 MFMA)",
-                "spmm": "spmm_lane_kernel / spmm_lane_jobs_kernel (CSR lane plan, XCD column slices, lane group per "
-                        "row, multi-job launches)"}
+                "spmm": "spmm_side_kernel (bipartite side x 32-column slice per XCD, lane-group entry-stream tasks, "
+                        "wave hub blocks combined in-launch) + spmm_lane_kernel for the non-bipartite graphs"}
 
 
 def log(*a):

@@ -1011,6 +1011,171 @@ __global__ void cl_table_reduce_kernel(int n, int nc, const float* __restrict__ 
   st4(dT + j * ld + c4, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same two passes on the bf16 matrix cores (GMR_CL_X6, default): every fp32 operand is split
+// exactly into three bf16 terms (hi + mid + lo, as gemm_x6.hip) and each 32 x 32 x 16 product is
+// accumulated in fp32 from six v_mfma_f32_32x32x16_bf16 (hi.hi + hi.mid + mid.hi + hi.lo + lo.hi +
+// mid.mid; the dropped terms are below 2^-23 |ab|), so S, E and U keep fp32 accuracy at 6 x 32 cycles
+// per 32 x 32 x 16 block instead of 8 x 64 on v_mfma_f32_32x32x2_f32.
+// Per staged 32-row block the workgroup converts the fp32 rows once into LDS as three row-major bf16
+// planes [32 rows][64 d] (A operand of S^T = Stg F^T) and three transposed planes [64 d][32 slots]
+// (A operand of Y^T += Stg^T E^T), slots permuted so that the 8 staged rows a lane half feeds to one
+// K-step of the second product are contiguous: a K position pairs the exp'd accumulator register
+// e = 8 t + q (staged row (q & 3) + 8 (q >> 2) + 16 t + 4 h) with the same staged row of Stg^T.
+// The fragment rows (queries, or table rows in the table pass) are split once into registers.
+typedef __bf16 c6bf8 __attribute__((ext_vector_type(8)));
+constexpr int kC6A = 72;                              // bf16 row stride, row-major planes (conflict-free b128)
+constexpr int kC6B = 40;                              // bf16 row stride, transposed planes
+constexpr int kC6PA = 32 * kC6A, kC6PB = 64 * kC6B;   // bf16 elements per plane
+constexpr int kC6Stage = 3 * (kC6PA + kC6PB);         // bf16 elements per staged block
+
+__device__ __forceinline__ void c6_split8(const float (&v)[8], c6bf8 (&o)[3]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 hh = (__bf16)__builtin_amdgcn_fmed3f(v[e], -0x1.fep127f, 0x1.fep127f);
+    const float r1 = v[e] - (float)hh;  // exact
+    const __bf16 mm = (__bf16)r1;
+    o[0][e] = hh;
+    o[1][e] = mm;
+    o[2][e] = (__bf16)(r1 - (float)mm);  // exact
+  }
+}
+
+// fp32 block (32 x 64, stride kClLd) -> the three row-major and the three transposed bf16 planes
+__device__ __forceinline__ void c6_convert(const float* sf, __bf16* stg) {
+  const int t = threadIdx.x;
+  {  // row-major: thread -> row t / 8, columns 8 (t % 8) .. + 8
+    const int r = t >> 3, c = (t & 7) * 8;
+    const float4 a = ld4(sf + r * kClLd + c), b = ld4(sf + r * kClLd + c + 4);
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    c6bf8 o[3];
+    c6_split8(v, o);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<c6bf8*>(stg + p * kC6PA + r * kC6A + c) = o[p];
+  }
+  {  // transposed: thread -> column d = t / 4, slot group g = t % 4 (slots 8 g .. 8 g + 7)
+    const int d = t >> 2, g = t & 3;
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = sf[(16 * (g >> 1) + 4 * (g & 1) + (q & 3) + 8 * (q >> 2)) * kClLd + d];
+    c6bf8 o[3];
+    c6_split8(v, o);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<c6bf8*>(stg + 3 * kC6PA + p * kC6PB + d * kC6B + 8 * g) = o[p];
+  }
+}
+
+__device__ __forceinline__ clx16 c6_mfma6(const c6bf8 (&a)[3], const c6bf8 (&b)[3], clx16 c) {  // small terms first
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+}
+
+// TABLE = false (rows pass): F = P (queries), Stg = T (keys), part_y / part_z per query chunk;
+// TABLE = true (table pass): F = T rows, Stg = P rows weighted by w = r_i, part_y = dT partials
+template <bool FAST, bool TABLE>
+__global__ void __launch_bounds__(256, 2) cl6_kernel(int nf, int ns, const float* __restrict__ F, int64_t ldf,
+                                                     const float* __restrict__ Stg, int64_t lds,
+                                                     const float* __restrict__ w, float inv_t, int chunk,
+                                                     float* __restrict__ part_y, float* __restrict__ part_z) {
+  __shared__ __attribute__((aligned(16))) __bf16 s_stg[2 * kC6Stage];
+  __shared__ __attribute__((aligned(16))) float s_f[32 * kClLd];
+  __shared__ float s_w[2][32];
+  const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const int f = blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + l32;  // the lane's fragment row
+  const int c = blockIdx.y, s0 = c * chunk, s1 = min(ns, s0 + chunk);
+  c6bf8 fr[4][3];  // K-step k: d = 16 k + 8 h + 0..7
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float4 a = f4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (f < nf) {
+      a = ld4(F + (int64_t)f * ldf + 16 * k + 8 * h);
+      b = ld4(F + (int64_t)f * ldf + 16 * k + 8 * h + 4);
+    }
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    c6_split8(v, fr[k]);
+  }
+  clx16 y0, y1;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) y0[e] = y1[e] = 0.f;
+  float z = 0.f, sw = 0.f;
+  float4 st[2];
+  cl_load(st, Stg, lds, s0, s1);
+  if (TABLE && threadIdx.x < 32) sw = s0 + (int)threadIdx.x < s1 ? w[s0 + threadIdx.x] : 0.f;
+  cl_store(st, s_f);
+  __syncthreads();
+  c6_convert(s_f, s_stg);
+  if (TABLE && threadIdx.x < 32) s_w[0][threadIdx.x] = sw;
+  __syncthreads();
+  int cur = 0;
+  for (int j = s0; j < s1; j += 32) {
+    const bool more = j + 32 < s1;
+    if (more) {
+      cl_load(st, Stg, lds, j + 32, s1);
+      if (TABLE && threadIdx.x < 32) sw = j + 32 + (int)threadIdx.x < s1 ? w[j + 32 + threadIdx.x] : 0.f;
+    }
+    const __bf16* A = s_stg + cur * kC6Stage;
+    clx16 sacc;  // S^T: row = staged row (e & 3) + 8 (e >> 2) + 4 h, column = fragment row l32
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sacc[e] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c6bf8 a[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const c6bf8*>(A + p * kC6PA + l32 * kC6A + 16 * k + 8 * h);
+      sacc = c6_mfma6(a, fr[k], sacc);
+    }
+    float ev[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int r = (e & 3) + 8 * (e >> 2) + 4 * h;
+      const float x = j + r < s1 ? cl_exp<FAST>(inv_t, sacc[e]) : 0.f;
+      if (TABLE) {
+        ev[e] = s_w[cur][r] * x;
+      } else {
+        ev[e] = x;
+        z += x;
+      }
+    }
+    const __bf16* Bt = A + 3 * kC6PA;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {  // Y^T (64 d x 32) += Stg^T E^T, K = 32 staged rows in two steps
+      const float evs[8] = {ev[8 * t2], ev[8 * t2 + 1], ev[8 * t2 + 2], ev[8 * t2 + 3],
+                            ev[8 * t2 + 4], ev[8 * t2 + 5], ev[8 * t2 + 6], ev[8 * t2 + 7]};
+      c6bf8 eb[3], a0[3], a1[3];
+      c6_split8(evs, eb);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        a0[p] = *reinterpret_cast<const c6bf8*>(Bt + p * kC6PB + l32 * kC6B + 8 * (2 * t2 + h));
+        a1[p] = *reinterpret_cast<const c6bf8*>(Bt + p * kC6PB + (32 + l32) * kC6B + 8 * (2 * t2 + h));
+      }
+      y0 = c6_mfma6(a0, eb, y0);
+      y1 = c6_mfma6(a1, eb, y1);
+    }
+    if (more) {  // s_f's last reader (the convert) finished before the previous barrier
+      cl_store(st, s_f);
+      __syncthreads();
+      c6_convert(s_f, s_stg + (cur ^ 1) * kC6Stage);
+      if (TABLE && threadIdx.x < 32) s_w[cur ^ 1][threadIdx.x] = sw;
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (f < nf) cl_put(part_y + ((int64_t)c * nf + f) * 64, y0, y1, h);
+  if (!TABLE) {
+    const float zf = z + __shfl_xor(z, 32);
+    if (f < nf && h == 0) part_z[(int64_t)c * nf + f] = zf;
+  }
+}
+
+int cl_x6() {  // read per call (a getenv), so a test can compare both pipes in one process
+  const char* e = getenv("GMR_CL_X6");
+  return !(e && atoi(e) == 0);
+}
+
 struct ClPlan {
   int nca, chunk_a, ncb, chunk_b;
 };
@@ -1069,6 +1234,24 @@ extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int6
     const char* e = getenv("GMR_CL_FASTEXP");
     return !(e && atoi(e) == 0);
   }();
+  if (cl_x6()) {  // split-bf16 passes (128 fragment rows per workgroup)
+    const dim3 ga((unsigned)((B + 127) / 128), (unsigned)p.nca), gb((unsigned)((n + 127) / 128), (unsigned)p.ncb);
+    auto rows6 = fast ? cl6_kernel<true, false> : cl6_kernel<false, false>;
+    auto table6 = fast ? cl6_kernel<true, true> : cl6_kernel<false, true>;
+    hipLaunchKernelGGL(rows6, ga, dim3(256), 0, st, B, (int)n, P, ldp, T, ldt, nullptr, inv_temp, p.chunk_a, part_u,
+                       part_z);
+    GMR_LAUNCHED();
+    hipLaunchKernelGGL(cl_finalize_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, p.nca, part_u, part_z,
+                       CLN, nodes, node_off, inv_temp, coef, loss, contrib, ld_contrib, r);
+    GMR_LAUNCHED();
+    hipLaunchKernelGGL(table6, gb, dim3(256), 0, st, (int)n, B, T, ldt, P, ldp, r, inv_temp, p.chunk_b, part_t,
+                       nullptr);
+    GMR_LAUNCHED();
+    hipLaunchKernelGGL(cl_table_reduce_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n, p.ncb,
+                       part_t, dT, ld_dt);
+    GMR_LAUNCHED();
+    return GMR_OK;
+  }
   const int nf = cl_nf();
   const dim3 ga((unsigned)((B + 128 * nf - 1) / (128 * nf)), (unsigned)p.nca);
   const dim3 gb((unsigned)((n + 128 * nf - 1) / (128 * nf)), (unsigned)p.ncb);

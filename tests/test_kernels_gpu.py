@@ -389,10 +389,13 @@ def test_normalize_rows_and_bwd(K):
 
 
 @pytest.mark.parametrize("B,n", [(2048, 19445), (974, 7050), (37, 100), (300, 33)])
-def test_contrast_fused_vs_fp64(K, B, n):
+@pytest.mark.parametrize("pipe", ["x6", "f32"])
+def test_contrast_fused_vs_fp64(K, B, n, pipe, monkeypatch):
     """K8 fused InfoNCE (gmr_contrast_fused_f32: contrastLoss fwd + bwd without the B x n logits)
     vs a float64 restatement of models/diffmm.py:251-258 on unit rows (|logit| <= 1/temp, no max
-    subtraction, as the reference).  Loss rows rtol 1e-5; gradients rtol 2e-4 of their scale."""
+    subtraction, as the reference).  Loss rows rtol 1e-5; gradients rtol 2e-4 of their scale.  Both
+    pipes: the split-bf16 MFMA passes (GMR_CL_X6, default) and the fp32-input MFMA ones."""
+    monkeypatch.setenv("GMR_CL_X6", "1" if pipe == "x6" else "0")
     rng = _rng(11)
     off = 5
     N = off + n + 3
