@@ -196,6 +196,19 @@ class DiffRec(GeneralRecommender):
         self._pending = None
         self._step += 1
 
+    def extra_state(self):
+        """Importance-sampling state a resumed run needs (not parameters, so not in state_dict):
+        Lt_history / Lt_count (diffrec.py:279-286) and the Philox step counter."""
+        return {"Lt_history": self.Lt_history.cpu(), "Lt_count": self.Lt_count.cpu(),
+                "counters": {"step": self._step}}
+
+    def load_extra_state(self, st):
+        """Inverse of extra_state."""
+        self.Lt_history.copy_(st["Lt_history"].to(self.device))
+        self.Lt_count.copy_(st["Lt_count"].to(self.device))
+        self._step = int(st["counters"]["step"])
+        self._pending = None
+
     def calculate_loss(self, interaction):
         users = interaction[0].to(torch.int32).contiguous()
         params = self.model.params()

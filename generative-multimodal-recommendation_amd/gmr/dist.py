@@ -12,7 +12,12 @@ F2); this module holds the sharding rules used by the trainers:
   * evaluation       — eval users are sharded; the top-K index rows are all-gathered.
 The global batch is the reference's train_batch_size at every world size, so the number of
 optimiser steps per epoch, and the trajectory up to fp32 reassociation of the sums, are the
-single-process ones (the per-GPU batch shrinks as B / world: strong scaling).
+single-process ones (the per-GPU batch shrinks as B / world: strong scaling).  DiffMM and DiffRec
+key every device draw by (global step, global row), so their draws are also the single-process
+ones at any world size; GenRecV1's diffusion phase and rebuild key their Philox streams by
+(step, rank) and the value-only InfoNCE of its diffusion loss (genrecv1.py:577-582) is taken over
+the rank's rows, so its DP run is the same objective with differently drawn noise (its rec step's
+in-batch InfoNCE is the global batch's, tests/test_dist_gpu.py).
 
 Opt-in GMR_DP_MODE=local ("partition users across the GPUs", BASELINE north star): every rank
 takes whole train_batch_size batches (rank r takes batch g * world + r of global step g), so one

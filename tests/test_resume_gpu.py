@@ -71,3 +71,35 @@ def test_resume_continues_the_same_run(golden, tmp_path):
 def test_resume_with_dropped_graphs(golden, tmp_path):
     ck = _run(golden, tmp_path, keep_rate=0.5)
     assert "image_UI_matrix_T" in ck["generated_graphs"]
+
+
+def test_resume_diffrec_importance_state(golden, tmp_path):
+    """DiffRec's importance-sampling state (Lt_history / Lt_count, diffrec.py:279-286) and its Philox
+    step travel with the checkpoint: the resumed epochs equal the uninterrupted ones bit for bit."""
+    from gmr.trainer import Trainer
+    from gmr.utils import init_seed
+    from test_diffrec_gpu import build_diffrec
+    g = golden("diffrec_tiny")
+
+    def fresh():
+        init_seed(999)
+        m, cfg, ds, tl = build_diffrec(g, checkpoint_dir=str(tmp_path))
+        return tl, m, Trainer(cfg, m)
+
+    tl, m, tr = fresh()
+    tr._train_data = tl
+    losses = []
+    for e in range(4):
+        losses.append(tr._train_epoch(tl, e)[0])
+        if e == 1:
+            tr._save_checkpoint(1)
+    assert int(m.Lt_count.sum()) > 0
+    want = (m.model.slab.data.cpu().numpy(), m.Lt_history.cpu().numpy(), m.Lt_count.cpu().numpy(), m._step)
+    tl2, m2, tr2 = fresh()
+    tr2.resume_checkpoint(str(tmp_path / "DiffRec-baby.pth"), train_data=tl2)
+    assert tr2.start_epoch == 2
+    assert [tr2._train_epoch(tl2, e)[0] for e in (2, 3)] == losses[2:]
+    np.testing.assert_array_equal(m2.model.slab.data.cpu().numpy(), want[0])
+    np.testing.assert_array_equal(m2.Lt_history.cpu().numpy(), want[1])
+    np.testing.assert_array_equal(m2.Lt_count.cpu().numpy(), want[2])
+    assert m2._step == want[3]
