@@ -56,7 +56,9 @@ X6_PEAK_TFS = round(2516.6 / 6, 1)
 KERNEL_NAMES = {"gemm": "gemm_glds_kernel (fp32 MFMA v_mfma_f32_32x32x2_f32, global_load_lds staging, XCD-aware tiles)",
                 "gemm_x6": "gemm_x6_kernel (fp32 operands split exactly into three bf16 terms, six "
                            "v_mfma_f32_32x32x16_bf16 products accumulated in fp32: fp32-accurate NT products)",
-                "infonce": "cl_rows_kernel + cl_table_kernel (fused InfoNCE, fp32 MFMA)",
+                "infonce": "cl6_kernel rows + table passes (fused InfoNCE on the split-bf16 pipe: fp32 operands split "
+                           "exactly into three bf16 terms, six v_mfma_f32_32x32x16_bf16 products, fp32 accumulation)",
+                "infonce_f32": "cl_rows_kernel + cl_table_kernel (fused InfoNCE, fp32 MFMA)",
                 "spmm": "spmm_side_kernel (bipartite side x 32-column slice per XCD, lane-group entry-stream tasks, "
                         "wave hub blocks combined in-launch) + spmm_lane_kernel for the non-bipartite graphs"}
 
@@ -141,15 +143,17 @@ def summarize_probe(p, model="diffmm", shape=None):
             else:  # rows pass S = P T^T and U = E T, table pass the same again: 4 B n 64 MACs
                 work = sum(8.0 * r[2][0] * r[2][1] * 64 for r in recs)
             achieved = work / (tot_ms * 1e-3) / 1e12
-            peak = X6_PEAK_TFS if tag == "gemm_x6" else FP32_MFMA_PEAK_TFS
+            cl_x6 = tag == "infonce" and os.environ.get("GMR_CL_X6", "1") != "0"
+            peak = X6_PEAK_TFS if tag == "gemm_x6" or cl_x6 else FP32_MFMA_PEAK_TFS
             out[tag] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                         "frac": round(achieved / peak, 4), "traffic": None,
                         "launches": len(recs), "avg_us": round(1e3 * tot_ms / len(recs), 2),
                         "total_ms": round(tot_ms, 3), "algorithmic_per_launch": work / len(recs),
-                        "algorithmic_unit": "flop", "kernel": KERNEL_NAMES[tag]}
+                        "algorithmic_unit": "flop",
+                        "kernel": KERNEL_NAMES["infonce_f32" if tag == "infonce" and not cl_x6 else tag]}
             if tag in ("gemm", "gemm_x6"):
                 out[tag]["algorithmic_bytes_per_launch"] = round(alg_bytes / len(recs))
-            if tag == "gemm_x6":
+            if tag == "gemm_x6" or cl_x6:
                 out[tag]["peak_note"] = ("fp32-equivalent flop (2MNK) vs the split kernel's instruction roofline: "
                                          "dense bf16 MFMA peak 2516.6 TF/s / 6 products; "
                                          f"{achieved / FP32_MFMA_PEAK_TFS:.3f} of the fp32-input MFMA peak")

@@ -253,14 +253,18 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
   }
 }
 
-// packed entries: {col | (last entry of its row) << 31, val}
-__global__ void __launch_bounds__(256) side_pack_kernel(const int* __restrict__ rowptr, const int* __restrict__ col,
-                                                        const float* __restrict__ val, int64_t n_rows,
+// packed entries: {col | (last entry of its row) << 31, val}: one thread per entry (coalesced), then one
+// per row sets its last entry's bit (a per-row loop serialised the hub rows of a rebuilt graph: 790 us)
+__global__ void __launch_bounds__(256) side_pack_kernel(const int* __restrict__ col, const float* __restrict__ val,
+                                                        int64_t nnz, int2* __restrict__ packed) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * blockDim.x)
+    packed[e] = make_int2(col[e], __float_as_int(val[e]));
+}
+__global__ void __launch_bounds__(256) side_last_kernel(const int* __restrict__ rowptr, int64_t n_rows,
                                                         int2* __restrict__ packed) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_rows; r += (int64_t)gridDim.x * blockDim.x) {
     const int beg = rowptr[r], end = rowptr[r + 1];
-    for (int e = beg; e < end; ++e)
-      packed[e] = make_int2(col[e] | (e == end - 1 ? (int)0x80000000u : 0), __float_as_int(val[e]));
+    if (end > beg) packed[end - 1].x |= (int)0x80000000u;
   }
 }
 
@@ -454,8 +458,12 @@ extern "C" int gmr_spmm_side_pack(const int32_t* rowptr, const int32_t* col, con
                                   int64_t nnz, int64_t packed_off, int32_t* plan, void* stream) {
   GMR_ARG(rowptr && col && val && plan && n_rows > 0 && packed_off > 0 && packed_off % 2 == 0, "bad args");
   if (nnz == 0) return GMR_OK;
-  hipLaunchKernelGGL(side_pack_kernel, dim3(gmr::grid_for(n_rows, 256, 4096)), dim3(256), 0, (hipStream_t)stream,
-                     rowptr, col, val, n_rows, reinterpret_cast<int2*>(plan + packed_off));
+  int2* packed = reinterpret_cast<int2*>(plan + packed_off);
+  hipLaunchKernelGGL(side_pack_kernel, dim3(gmr::grid_for(nnz, 256, 8192)), dim3(256), 0, (hipStream_t)stream, col, val,
+                     nnz, packed);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(side_last_kernel, dim3(gmr::grid_for(n_rows, 256, 4096)), dim3(256), 0, (hipStream_t)stream, rowptr,
+                     n_rows, packed);
   GMR_LAUNCHED();
   return GMR_OK;
 }

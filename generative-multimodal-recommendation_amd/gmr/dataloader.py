@@ -225,7 +225,10 @@ class EvalDataLoader:
             sorted_items = np.concatenate([np.sort(x) for x in self.eval_items_per_u]) if len(
                 self.eval_items_per_u) else np.zeros(0, np.int64)
             mptr = np.concatenate([[0], np.cumsum(self.train_pos_len)]).astype(np.int64)
+            by_row = np.lexsort((self.mask_cols_np, self.mask_rows_np))  # the fused eval kernel's mask order
             self._dev = {
+                "mask_ptr_dev": torch.as_tensor(mptr).to(d),
+                "mask_cols_sorted": torch.as_tensor(self.mask_cols_np[by_row].astype(np.int32)).to(d),
                 "eval_u32": torch.as_tensor(self.eval_u_np.astype(np.int32)).to(d),
                 "eval_u": torch.as_tensor(self.eval_u_np).to(d),
                 "mask_rows": torch.as_tensor(self.mask_rows_np.astype(np.int32)).to(d),

@@ -540,6 +540,12 @@ class GenRecV1(GeneralRecommender):
         self._score(ub, itm, scores)
         return scores
 
+    @property
+    def fused_eval(self):
+        """The trainer's fused score -> mask -> top-k kernel computes fp32 scores; the opt-in fp16
+        scoring keeps its own MFMA GEMM + mask + top-k."""
+        return self.scoring_dtype == "fp32"
+
     def _score(self, ub, itm, out):
         """usr[users] @ itm^T (genrecv1.py:419-427): fp32 MFMA GEMM, or the opt-in fp16 MFMA one."""
         if self.scoring_dtype == "fp16":

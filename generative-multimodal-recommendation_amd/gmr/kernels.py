@@ -528,6 +528,17 @@ def topk_rows(scores, k, out_idx, out_val=None):
     return out_idx
 
 
+def score_topk(usr, itm, users, mask_ptr, mask_cols, k, out_idx, out_val=None, fill=-1e10):
+    """Fused eval (gmr_score_topk_f32): top-k of usr[users] . itm^T with each row's train positives
+    (mask_cols[mask_ptr[r]:mask_ptr[r+1]], sorted) set to fill; no rows x items score buffer."""
+    n = users.numel() if users is not None else out_idx.shape[0]
+    if out_idx.shape[0] < n or mask_ptr.numel() < n + 1 or mask_ptr.dtype != torch.int64:
+        raise ValueError("score_topk: out_idx / mask_ptr (int64, n + 1) too small for the rows")
+    _lib.call("gmr_score_topk_f32", n, ptr(users), ptr(usr), _ld(usr), itm.shape[0], ptr(itm), _ld(itm), itm.shape[1],
+              ptr(mask_ptr), ptr(mask_cols), float(fill), int(k), ptr(out_idx), _ld(out_idx), ptr(out_val), stream())
+    return out_idx
+
+
 def mask_scores(scores, rows, cols, fill=-1e10):
     _lib.call("gmr_mask_scores_f32", rows.numel(), ptr(rows), ptr(cols), ptr(scores), _ld(scores), float(fill),
               stream())

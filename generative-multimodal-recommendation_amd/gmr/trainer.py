@@ -25,6 +25,10 @@ from .slab import FlatAdam
 from .topk_evaluator import TopKEvaluator
 from .utils import dict2str, early_stopping
 
+# full-rank eval through the fused score -> mask -> top-k kernel (gmr_score_topk_f32); GMR_EVAL_FUSED=0
+# keeps the score GEMM + mask + radix top-k over an E x I buffer (A/B)
+FUSED_EVAL = os.environ.get("GMR_EVAL_FUSED", "1") != "0"
+
 
 class Trainer:
     def __init__(self, config, model, mg=False):
@@ -296,15 +300,21 @@ class Trainer:
             out = torch.zeros((W * size, kmax), dtype=torch.int32, device=self.device)
             self._topk_buf = out
         m = self.model
+        fused = False
         if hasattr(m, "forward_embeddings"):
             usr, itm = m.forward_embeddings()  # identical for every batch of the pass (no_grad)
-            sb = getattr(self, "_score_buf", None)
-            if sb is None or sb.shape[0] < min(E, n):
-                sb = torch.empty((min(E, n), (m.n_items + 3) // 4 * 4), dtype=torch.float32, device=self.device)
-                self._score_buf = sb
+            fused = FUSED_EVAL and getattr(m, "fused_eval", True) and usr.shape[1] in (64, 128) and hi_r > lo_r
+            if not fused:
+                sb = getattr(self, "_score_buf", None)
+                if sb is None or sb.shape[0] < min(E, n):
+                    sb = torch.empty((min(E, n), (m.n_items + 3) // 4 * 4), dtype=torch.float32, device=self.device)
+                    self._score_buf = sb
         mptr = d["mask_ptr"]
         off = dist.rank() * size - lo_r  # row of user lo_r inside the padded gather buffer
-        for lo in range(lo_r, hi_r, E):
+        if fused:  # scores -> mask -> top-k in one launch over the whole shard: no E x I buffer
+            K.score_topk(usr, itm, d["eval_u32"][lo_r:hi_r], d["mask_ptr_dev"][lo_r:], d["mask_cols_sorted"], kmax,
+                         out[off + lo_r:off + hi_r])
+        for lo in range(lo_r, hi_r, E) if not fused else ():
             hi = min(hi_r, lo + E)
             users = d["eval_u32"][lo:hi]
             m0, m1 = int(mptr[lo]), int(mptr[hi])

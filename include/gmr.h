@@ -383,6 +383,16 @@ int gmr_mask_scores_f32(int64_t n, const int32_t* rows, const int32_t* cols, flo
                         void* stream);
 int gmr_topk_rows_f32(int64_t n_rows, int64_t n_cols, const float* scores, int64_t ld, int32_t k, int32_t* out_idx,
                       int64_t ld_idx, float* out_val, void* stream);
+/* K9 + K10 fused (common/trainer.py:379-386 with models/diffmm.py:276-277): per eval row r,
+ * scores = user_table[users[r]] . item_table^T (users NULL: row r is user r), the row's train positives
+ * mask_cols[mask_ptr[r] .. mask_ptr[r+1]) (sorted ascending within a row) set to `fill` (-1e10), then
+ * the top-k item indices (score desc, ties -> lowest index) into out_idx[r * ld_idx + j] and,
+ * if out_val is not NULL, their scores.  No n_rows x n_items buffer; dim 64 or 128; k <= 64.
+ * mask_ptr holds n_rows + 1 absolute offsets into mask_cols (pass &ptr[first row] for a slice). */
+int gmr_score_topk_f32(int64_t n_rows, const int32_t* users, const float* user_table, int64_t ld_user, int64_t n_items,
+                       const float* item_table, int64_t ld_item, int64_t dim, const int64_t* mask_ptr,
+                       const int32_t* mask_cols, float fill, int32_t k, int32_t* out_idx, int64_t ld_idx,
+                       float* out_val, void* stream);
 /* Recall/NDCG/Precision/MAP sums over users at ks (topk_evaluator.py:107-120, metrics.py):
  * out_sums[metric*8 + j], metric 0 recall 1 ndcg 2 precision 3 map, j < n_ks (fp64). */
 int64_t gmr_eval_metrics_partials(int64_t n_users);

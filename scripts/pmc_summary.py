@@ -21,13 +21,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLASSES = {"gemm": ("gemm_kernel", "gemm_glds_kernel", "splitk_reduce_kernel"), "gemm_x6": ("gemm_x6_kernel",),
            "spmm": ("spmm_seg_kernel", "spmm_fix_kernel", "spmm_lane_kernel", "spmm_lane_jobs_kernel",
                     "lane_fix_kernel", "lane_fix_jobs_kernel", "spmm_blk_kernel", "spmm_chunk_kernel", "spmm_side_kernel"),
-           "infonce": ("cl_rows_kernel", "cl_table_kernel", "cl_finalize_kernel", "cl_table_reduce_kernel")}
+           "infonce": ("cl_rows_kernel", "cl_table_kernel", "cl6_kernel", "cl_finalize_kernel", "cl_table_reduce_kernel")}
 # launches of a class = launches of its primary kernels (one per gmr_* call)
 PRIMARY = {"gemm": ("gemm_kernel", "gemm_glds_kernel"), "gemm_x6": ("gemm_x6_kernel",),
            "spmm": ("spmm_seg_kernel", "spmm_lane_kernel", "spmm_lane_jobs_kernel", "spmm_blk_kernel",
                     "spmm_chunk_kernel", "spmm_side_kernel"),
-           "infonce": ("cl_rows_kernel",)}
-UTIL = {"gemm": ("gemm_kernel", "gemm_glds_kernel"), "gemm_x6": ("gemm_x6_kernel",), "spmm": (), "infonce": ("cl_rows_kernel", "cl_table_kernel")}
+           "infonce": ("cl_rows_kernel", "cl6_rows")}
+UTIL = {"gemm": ("gemm_kernel", "gemm_glds_kernel"), "gemm_x6": ("gemm_x6_kernel",), "spmm": (), "infonce": ("cl_rows_kernel", "cl_table_kernel", "cl6_kernel")}
 
 
 def load(path, counter):
@@ -36,7 +36,10 @@ def load(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
-        out.append((r.get("Dispatch_Id") or r.get("Correlation_Id"), name.split("<")[0], float(r["Counter_Value"])))
+        base = name.split("<")[0]
+        out.append((r.get("Dispatch_Id") or r.get("Correlation_Id"), base, float(r["Counter_Value"])))
+        if base == "cl6_kernel" and name.replace(" ", "").endswith(",false>"):
+            out.append((None, "cl6_rows", 0.0))  # one split-bf16 InfoNCE call = one rows pass (marker)
     return out
 
 
