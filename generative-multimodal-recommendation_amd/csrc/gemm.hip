@@ -515,6 +515,16 @@ bool default_x6() {
   return x;
 }
 
+// GMR_GEMM_X6_64=1: NT products planned on 64^2 tiles also take the split-bf16 kernel (64^2 split tiles;
+// off by default: measured per shape first, scripts/gemm_bench.py --tiles 64 --mfma 32,6)
+bool default_x6_64() {
+  static bool x = [] {
+    const char* e = getenv("GMR_GEMM_X6_64");
+    return e && atoi(e) == 1;
+  }();
+  return x;
+}
+
 bool default_glds() {
   static bool g = [] {
     const char* e = getenv("GMR_GEMM_GLDS");
@@ -556,6 +566,7 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
   // (the staging and MFMA-shape flags name fp32-kernel variants, so they select the fp32 kernel too)
   const bool x6 = allow_x6 && ((tile & GMR_GEMM_X6) || default_x6()) &&
                   !(tile & (GMR_GEMM_F32 | GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32 | GMR_GEMM_GLDS | GMR_GEMM_REGSTAGE));
+  const bool x6_64 = x6 && ((tile & GMR_GEMM_X6) || default_x6_64());
   tile &= ~(GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32 | GMR_GEMM_GLDS | GMR_GEMM_REGSTAGE | GMR_GEMM_X6 | GMR_GEMM_F32);
   if (tile == 0) {
     // measured on MI355X (scripts/gemm_bench.py): 256^2 tiles win the long-K products of the
@@ -594,7 +605,7 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
   if (x6 && tile == 64 && M * N >= ((int64_t)4 << 20) && K >= 256) tile = 128;
   // the split-bf16 kernel (gemm_x6.hip): NT products on 128^2, 256 x 128, 128 x 256 and 256^2 tiles
   // (the 256^2 tile maps to 256 x 128: a 2-wave-per-SIMD 256^2 block spills its prefetch registers)
-  if (x6 && tile != 64 && !ta && tb) {
+  if (x6 && (tile != 64 || x6_64) && !ta && tb) {
     mf = 6;
     // products with >= 768 128^2 tiles run three 128^2 blocks per CU (gemm_x6.hip), which beat
     // 256 x 128 there (19445 x 1000 x 7050: 1852 -> 1605 us); smaller ones keep 256 x 128
@@ -614,7 +625,7 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
     // fill < 80 % of the resident slots (256 x 128: one block per CU; 128^2: two) and slabs stay >= 512
     // deep (measured: the 7050 x 1000 x 2048 weight gradients 253 -> 222 us unsplit, the 2048-row
     // diffusion products best at 4 slabs; profiles/r02x6_study.txt)
-    const int64_t slots = p.bm * p.bn == 128 * 128 ? 512 : 256;
+    const int64_t slots = p.bm == 64 ? 768 : p.bm * p.bn == 128 * 128 ? 512 : 256;
     splits = 1;
     while (p.tm * p.tn * splits * 5 < slots * 4 && K / (splits * 2) >= 512 && splits < 16) splits *= 2;
   }

@@ -398,6 +398,8 @@ int x6_launch(int bm, int bn, dim3 grid, hipStream_t st, int64_t M, int64_t N, i
   // 4-wave blocks per CU, single-buffered (48 KiB each), so one block's split / barrier phase overlaps
   // the others' MFMA steps (GMR_GEMM_X6_NB128 = 1 / 3: always two / three single-buffered blocks,
   // = 2: one double-buffered block per CU; for A/B runs)
+  // 64^2 (4 waves of 32^2, LDS double-buffered, 48 KiB: three blocks per CU) for the small products
+  if (bm == 64 && bn == 64) GMR_X6(64, 64, 2, 2, 2, 3)
   if (bm == 256 && bn == 128) GMR_X6(256, 128, 4, 2, 2, 1)
   if (bm == 128 && bn == 256) GMR_X6(128, 256, 2, 4, 2, 1)
   if (bm == 128 && bn == 128) {

@@ -35,6 +35,9 @@ SPMM_FUSE = int(os.environ.get("GMR_SPMM_FUSE", str(FUSE_FWD | FUSE_UI_T)))
 # (−1.5 ms per rebuild vs 8,192-user chunks: fewer, fuller GEMM waves; 1.3 GB of buffers per
 # denoiser, profiles/r02m_knobs_ab.txt); GMR_REBUILD_CHUNK overrides, for tuning
 REBUILD_CHUNK = int(os.environ.get("GMR_REBUILD_CHUNK", "32768"))
+# data parallel: all-reduce E0's gradient from inside rec_step, overlapped with the projection-weight
+# GEMMs (GMR_DP_EARLY_REDUCE=0: one all-reduce of the whole slab after the step)
+EARLY_REDUCE = os.environ.get("GMR_DP_EARLY_REDUCE", "1") != "0"
 
 
 def diffmm_tables(noise_scale, noise_min, noise_max, steps):
@@ -360,6 +363,10 @@ class DiffMM(GeneralRecommender):
         E0 = s.view("E0")
         _lib.call("gmr_dmm_assemble", N, U, ptr(w["T2"]), ptr(w["T3"]), ptr(w["OutI"]), ptr(w["OutT"]), ptr(E0),
                   2.0 * self.reg_weight * reg_share, ptr(s.gview("E0")), ptr(w["dNF"]), stream())
+        if dist.is_dist() and EARLY_REDUCE:
+            # data parallel: E0's gradient (6.8 MB of the 7.9 MB slab) is final here; its RCCL all-reduce
+            # runs beside the projection-weight GEMMs below (the Trainer reduces the rest and waits)
+            self._early = dist.all_reduce_start(s.grad[:self.early_reduce_cut(s)])
         # modality projections: normalize + leaky-relu backward, then W grads (text beside image)
         dNF = w["dNF"]
         with st.on(1):
@@ -370,6 +377,17 @@ class DiffMM(GeneralRecommender):
         st.join(1)
         self._step += 1
         return loss[0]
+
+    def early_reduce_cut(self, slab):
+        """Gradient words of `slab` that rec_step all-reduces itself (E0, issued as soon as it is final);
+        the Trainer reduces [cut:) and waits (idle ranks issue the same two reduces).  None: whole slab."""
+        if slab is not self.rec_slab or not EARLY_REDUCE:
+            return None
+        return slab.offsets["image_trans"]
+
+    def take_early_reduce(self):
+        h, self._early = getattr(self, "_early", None), None
+        return h
 
     def _transpose_of(self, g):
         """A^T for the backward of a UI-graph product: A itself at keep_rate 1 (the normalised graph

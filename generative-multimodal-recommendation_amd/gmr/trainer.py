@@ -30,6 +30,25 @@ from .utils import dict2str, early_stopping
 FUSED_EVAL = os.environ.get("GMR_EVAL_FUSED", "1") != "0"
 
 
+def reduce_slab_grads(model, slabs):
+    """SUM all-reduce of the gradient slabs after one data-parallel step.  A model may have started
+    the first `early_reduce_cut(slab)` words itself inside rec_step (DiffMM: E0, overlapped with its
+    last GEMMs); then only the rest is reduced here and the early one is waited for.  A rank that ran
+    no rec_step (idle in a short last batch) issues the same two reduces, so collectives match."""
+    if not dist.is_dist():
+        return
+    early = model.take_early_reduce() if hasattr(model, "take_early_reduce") else None
+    for s_ in slabs:
+        cut = model.early_reduce_cut(s_) if hasattr(model, "early_reduce_cut") else None
+        if cut is None:
+            dist.all_reduce_(s_.grad)
+        else:
+            if early is None:
+                dist.all_reduce_(s_.grad[:cut])
+            dist.all_reduce_(s_.grad[cut:])
+    dist.wait(early)
+
+
 class Trainer:
     def __init__(self, config, model, mg=False):
         self.config = config
@@ -106,8 +125,7 @@ class Trainer:
                 for s_ in slabs:
                     s_.zero_grad()
             if W > 1:
-                for s_ in slabs:
-                    dist.all_reduce_(s_.grad)
+                reduce_slab_grads(self.model, slabs)
             if hook is not None:
                 hook()
             self.optimizer.step()

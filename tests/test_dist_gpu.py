@@ -43,7 +43,7 @@ def _case():
     from gmr import dist
     from gmr.dataloader import TrainDataLoader
     from gmr.dataset import RecDataset
-    from gmr.trainer import DiffMMTrainer, Trainer
+    from gmr.trainer import DiffMMTrainer, Trainer, reduce_slab_grads
 
     g = _golden()
     dev = "cuda"
@@ -58,7 +58,7 @@ def _case():
     norm, share = dist.dp_scales(dist.shard_sizes(B))
     loss = m.rec_step(u[a:b], p[a:b], n[a:b], norm_rows=norm, reg_share=share).view(1).double()
     dist.all_reduce_(loss)
-    dist.all_reduce_(m.rec_slab.grad)
+    reduce_slab_grads(m, [m.rec_slab])
     out["rec_loss"] = loss.cpu().numpy()
     out["rec_grad"] = m.rec_slab.grad.cpu().numpy().copy()
     # --- one diffusion step, Philox draws keyed by the global row
@@ -273,7 +273,7 @@ def _case_genrec():
     from gmr import dist
     from gmr.dataloader import TrainDataLoader
     from gmr.dataset import RecDataset
-    from gmr.trainer import Trainer
+    from gmr.trainer import Trainer, reduce_slab_grads
     g = dict(np.load(os.path.join(ROOT, "tests", "golden", "genrecv1_tiny.npz"), allow_pickle=False))
     m = sub(g, "m_")
     out = {}
@@ -286,7 +286,7 @@ def _case_genrec():
     gb = (u, p, a) if dist.is_dist() else None
     loss = model.rec_step(u[a:b], p[a:b], n[a:b], norm_rows=norm, reg_share=share, gbatch=gb).view(1).double()
     dist.all_reduce_(loss)
-    dist.all_reduce_(model.rec_slab.grad)
+    reduce_slab_grads(model, [model.rec_slab])
     out["loss"] = loss.cpu().numpy()
     out["grad"] = model.rec_slab.grad.cpu().numpy().copy()
     # one BPR epoch through the Trainer (global batch 24 split over the ranks)

@@ -145,6 +145,7 @@ def _dp_case():
     """One BPR global step (calculate_loss + backward) at the sports shape on the first 2,048-row
     batch of the epoch draw, this rank's share of it; loss and rec gradient after the all-reduce."""
     from gmr import dist
+    from gmr.trainer import reduce_slab_grads
     _, tl, _, m, _ = _build(with_eval=False)
     _ref_graphs(m, dict(np.load(FIX, allow_pickle=False)))
     d = tl.epoch(with_plans=False)
@@ -154,7 +155,7 @@ def _dp_case():
     norm, share = dist.dp_scales(dist.shard_sizes(B))
     loss = m.rec_step(u[a:b], p[a:b], n[a:b], norm_rows=norm, reg_share=share).view(1).double()
     dist.all_reduce_(loss)
-    dist.all_reduce_(m.rec_slab.grad)
+    reduce_slab_grads(m, [m.rec_slab])
     return {"loss": loss.cpu().numpy(), "grad": m.rec_slab.grad.cpu().numpy().copy()}
 
 
