@@ -515,12 +515,14 @@ bool default_x6() {
   return x;
 }
 
-// GMR_GEMM_X6_64=1: NT products planned on 64^2 tiles also take the split-bf16 kernel (64^2 split tiles;
-// off by default: measured per shape first, scripts/gemm_bench.py --tiles 64 --mfma 32,6)
+// NT products planned on 64^2 tiles also take the split-bf16 kernel (64^2 split tiles, three blocks per CU):
+// measured (profiles/r03j_gemm64.txt) 2048 x 512 x 512 19.7 -> 17.1 us, 2048 x 6710 x 256 86.5 -> 68.5,
+// 2048 x 7050 x 64 43.6 -> 34.1; the TN / NN forms lose to their operand transposes there (4096 x 64 x
+// 7050 TN 49 -> 86 us), so only plain NT calls use it (make_plan).  GMR_GEMM_X6_64=0 turns it off.
 bool default_x6_64() {
   static bool x = [] {
     const char* e = getenv("GMR_GEMM_X6_64");
-    return e && atoi(e) == 1;
+    return !(e && atoi(e) == 0);
   }();
   return x;
 }
@@ -644,7 +646,7 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
 Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, int split_k) {
   if (ta || !tb) {
     Plan q = make_plan_core(0, 1, M, N, K, tile, split_k, true);
-    if (q.mf == 6) {
+    if (q.mf == 6 && q.bm != 64) {  // 64^2 split tiles: plain NT calls only (the copies cost more there)
       q.xpose = (ta ? 1 : 0) | (tb ? 0 : 2);
       return q;
     }

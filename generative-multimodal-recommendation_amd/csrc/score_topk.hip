@@ -28,6 +28,7 @@ constexpr int ST_ROWS = 16;     // rows per wave (one 16 x 16 MFMA tile height)
 constexpr int ST_CAP = 256;     // candidate slots per row
 constexpr int ST_TILES = 4;     // 16-item tiles per step
 constexpr int ST_STEP = 16 * ST_TILES;
+constexpr int ST_MSTAGE = 1024;  // masked items of a wave's 16 rows staged in LDS
 
 __device__ __forceinline__ uint32_t okey(float f) {  // order-preserving uint32 key
   const uint32_t u = __float_as_uint(f);
@@ -99,35 +100,18 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long x,
   return ((unsigned long long)hi << 32) | lo;
 }
 
-// DK = D / 64 (embedding width 64 or 128)
-template <int DK>
-__global__ void __launch_bounds__(64 * ST_WAVES, 1) score_topk_kernel(
-    int64_t n_rows, const int* __restrict__ users, const float* __restrict__ U, int64_t ldu, int64_t n_items,
-    const float* __restrict__ I, int64_t ldi, const int64_t* __restrict__ mptr, const int* __restrict__ mcols,
-    float fill, int K, int* __restrict__ out_idx, int64_t ld_idx, float* __restrict__ out_val) {
-  __shared__ unsigned long long cand[ST_WAVES][ST_ROWS][ST_CAP];
-  __shared__ int cnt[ST_WAVES][ST_ROWS];
-  constexpr int KS = 16 * DK;  // k values per lane: lane group g holds k in [KS g, KS (g + 1))
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 15, grp = lane >> 4;
-  const int64_t row0 = ((int64_t)blockIdx.x * ST_WAVES + w) * ST_ROWS;
-  if (row0 >= n_rows) return;
-  unsigned long long(*cb)[ST_CAP] = cand[w];
-  int* cn = cnt[w];
-
-  float a[KS];  // A[row col][k = KS grp + s]
-  {
-    const int64_t r = min(row0 + col, n_rows - 1);
-    const int64_t u = users ? (int64_t)users[r] : r;
-    const float4* p = reinterpret_cast<const float4*>(U + u * ldu + KS * grp);
-#pragma unroll
-    for (int q = 0; q < KS / 4; ++q) {
-      const float4 x = p[q];
-      a[4 * q] = x.x;
-      a[4 * q + 1] = x.y;
-      a[4 * q + 2] = x.z;
-      a[4 * q + 3] = x.w;
-    }
-  }
+// One wave's 16 rows (DK = D / 64: embedding width 64 or 128).  STAGED: the rows' masked items sit in
+// the wave's LDS slice (a mask lookup is an LDS read); otherwise (more than ST_MSTAGE masked items in
+// the 16 rows) they are read from global memory, which also waits for the item prefetch in flight.
+template <int DK, bool STAGED>
+__device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, int lane, const float (&a)[16 * DK],
+                                                int64_t n_items, const float* __restrict__ I, int64_t ldi,
+                                                const int64_t* __restrict__ mptr, const int* __restrict__ mcols,
+                                                const int* ms, int64_t mbase, float fill, int K,
+                                                unsigned long long (*cb)[ST_CAP], int* cn) {
+  constexpr int KS = 16 * DK;
+  const int col = lane & 15, grp = lane >> 4;
+  auto mask_at = [&](int64_t i) -> int { return STAGED ? ms[i - mbase] : mcols[i]; };
   // the lane's output rows are row0 + 4 grp + e (MFMA C/D map: row = 4 (lane >> 4) + reg, col = lane & 15)
   int64_t mc[4], me[4];
   int nm[4];
@@ -137,12 +121,11 @@ __global__ void __launch_bounds__(64 * ST_WAVES, 1) score_topk_kernel(
     const int64_t r = row0 + 4 * grp + e;
     mc[e] = r < n_rows ? mptr[r] : 0;
     me[e] = r < n_rows ? mptr[r + 1] : 0;
-    nm[e] = mc[e] < me[e] ? mcols[mc[e]] : 0x7fffffff;
+    nm[e] = mc[e] < me[e] ? mask_at(mc[e]) : 0x7fffffff;
     tau[e] = 0;
   }
-  if (lane < ST_ROWS) cn[lane] = 0;
-
-  float b[ST_TILES][KS], nb[ST_TILES][KS];
+  // items [c0, c0 + 64): this lane's 16 consecutive k of item c0 + 16 t + col (clamped: the loads of
+  // a step past the end are issued anyway, so no branch splits the prefetch from its use)
   auto load_b = [&](int64_t c0, float (&bb)[ST_TILES][KS]) {
 #pragma unroll
     for (int t = 0; t < ST_TILES; ++t) {
@@ -158,11 +141,7 @@ __global__ void __launch_bounds__(64 * ST_WAVES, 1) score_topk_kernel(
       }
     }
   };
-  load_b(0, b);
-#pragma unroll 1
-  for (int64_t c0 = 0; c0 < n_items; c0 += ST_STEP) {
-    const bool more = c0 + ST_STEP < n_items;
-    if (more) load_b(c0 + ST_STEP, nb);
+  auto step = [&](int64_t c0, const float (&b)[ST_TILES][KS]) {
     f32x4 acc[ST_TILES];
 #pragma unroll
     for (int t = 0; t < ST_TILES; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -181,7 +160,7 @@ __global__ void __launch_bounds__(64 * ST_WAVES, 1) score_topk_kernel(
             if (t == (d >> 4)) acc[t][e] = fill;
         }
         ++mc[e];
-        nm[e] = mc[e] < me[e] ? mcols[mc[e]] : 0x7fffffff;
+        nm[e] = mc[e] < me[e] ? mask_at(mc[e]) : 0x7fffffff;
       }
     }
 #pragma unroll
@@ -213,12 +192,58 @@ __global__ void __launch_bounds__(64 * ST_WAVES, 1) score_topk_kernel(
           if (e == (r & 3)) tau[e] = nt;
       }
     }
-    if (more) {
+  };
+  // two register sets, ping-pong: step j computes on one while the other's loads are in flight
+  float b0[ST_TILES][KS], b1[ST_TILES][KS];
+  load_b(0, b0);
+#pragma unroll 1
+  for (int64_t c0 = 0; c0 < n_items; c0 += 2 * ST_STEP) {
+    load_b(c0 + ST_STEP, b1);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs (the scheduler sinks it)
+    step(c0, b0);
+    if (c0 + ST_STEP >= n_items) break;
+    load_b(c0 + 2 * ST_STEP, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    step(c0 + ST_STEP, b1);
+  }
+}
+
+template <int DK>
+__global__ void __launch_bounds__(64 * ST_WAVES, 1) score_topk_kernel(
+    int64_t n_rows, const int* __restrict__ users, const float* __restrict__ U, int64_t ldu, int64_t n_items,
+    const float* __restrict__ I, int64_t ldi, const int64_t* __restrict__ mptr, const int* __restrict__ mcols,
+    float fill, int K, int* __restrict__ out_idx, int64_t ld_idx, float* __restrict__ out_val) {
+  __shared__ unsigned long long cand[ST_WAVES][ST_ROWS][ST_CAP];
+  __shared__ int cnt[ST_WAVES][ST_ROWS];
+  __shared__ int mstage[ST_WAVES][ST_MSTAGE];
+  constexpr int KS = 16 * DK;  // k values per lane: lane group g holds k in [KS g, KS (g + 1))
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 15, grp = lane >> 4;
+  const int64_t row0 = ((int64_t)blockIdx.x * ST_WAVES + w) * ST_ROWS;
+  if (row0 >= n_rows) return;
+  unsigned long long(*cb)[ST_CAP] = cand[w];
+  int* cn = cnt[w];
+
+  float a[KS];  // A[row col][k = KS grp + s]
+  {
+    const int64_t r = min(row0 + col, n_rows - 1);
+    const int64_t u = users ? (int64_t)users[r] : r;
+    const float4* p = reinterpret_cast<const float4*>(U + u * ldu + KS * grp);
 #pragma unroll
-      for (int t = 0; t < ST_TILES; ++t)
-#pragma unroll
-        for (int s = 0; s < KS; ++s) b[t][s] = nb[t][s];
+    for (int q = 0; q < KS / 4; ++q) {
+      const float4 x = p[q];
+      a[4 * q] = x.x;
+      a[4 * q + 1] = x.y;
+      a[4 * q + 2] = x.z;
+      a[4 * q + 3] = x.w;
     }
+  }
+  if (lane < ST_ROWS) cn[lane] = 0;
+  const int64_t mbase = mptr[row0], mend = mptr[min(row0 + ST_ROWS, n_rows)];
+  if (mend - mbase <= ST_MSTAGE) {
+    for (int64_t i = mbase + lane; i < mend; i += 64) mstage[w][i - mbase] = mcols[i];
+    score_topk_wave<DK, true>(n_rows, row0, lane, a, n_items, I, ldi, mptr, mcols, mstage[w], mbase, fill, K, cb, cn);
+  } else {
+    score_topk_wave<DK, false>(n_rows, row0, lane, a, n_items, I, ldi, mptr, mcols, mstage[w], mbase, fill, K, cb, cn);
   }
   // final: the k best of each row, sorted ascending on the 64-bit key (score desc, item asc)
 #pragma unroll 1

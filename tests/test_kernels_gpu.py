@@ -610,7 +610,7 @@ X6, F32 = 1 << 26, 1 << 27  # GMR_GEMM_X6 / GMR_GEMM_F32 tile flags (include/gmr
 X6_RATIO, X6_FLOOR, X6_ABS = 1.25, 2.0 ** -24, 6e-7
 
 
-@pytest.mark.parametrize("tile", [0, 128, 256128, 128256])
+@pytest.mark.parametrize("tile", [0, 64, 128, 256128, 128256])
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
 def test_gemm_x6_fp32_accuracy(K, tile, ta, tb):
     """Split-bf16 products (GMR_GEMM_X6: x = hi + mid + lo exactly, six bf16 MFMA products) carry fp32
@@ -637,8 +637,12 @@ def test_gemm_x6_fp32_accuracy(K, tile, ta, tb):
             err[flag] = ((C.double() - ref).abs() / scale).max().item()
         assert err[X6] <= X6_RATIO * err[F32] + X6_FLOOR, (M, N, Kd, split, err)
         assert err[X6] <= X6_ABS, (M, N, Kd, split, err)
-    if tile:  # an explicit >= 128^2 tile with GMR_GEMM_X6 takes the split kernel in every layout
+    if tile and (tile != 64 or (ta, tb) == (0, 1)):
+        # an explicit >= 128^2 tile with GMR_GEMM_X6 takes the split kernel in every layout, a 64^2 one
+        # for plain NT calls (the other layouts keep the fp32 kernel: their operand copies cost more)
         assert _lib_kind(ta, tb, 1000, 700, 7050, tile | X6) == 6
+    if tile == 64 and (ta, tb) != (0, 1):
+        assert _lib_kind(ta, tb, 1000, 700, 7050, tile | X6) == 32
 
 
 def _lib_kind(ta, tb, M, N, Kd, tile):
@@ -660,12 +664,13 @@ def test_gemm_x6_epilogues(K):
     eb = _dev(rng.standard_normal((T, N)).astype(np.float32))
     t = _dev(rng.integers(0, T, size=M), torch.int32)
     want = torch.tanh(acc + eb.double()[t.long()])
-    err = {}
-    for flag in (X6, F32):
-        C = torch.empty(M, N, device=DEV)
-        K.gemm(A, B, C, trans_b=True, epi=K.EPI_BIAS_TANH, bias=eb, bias_row=t, ld_bias=N, tile=128 | flag)
-        err[flag] = ((C.double() - want).abs() / (scale + 1.0)).max().item()
-    assert err[X6] <= X6_RATIO * err[F32] + X6_FLOOR and err[X6] <= X6_ABS, err
+    for tile in (128, 64):
+        err = {}
+        for flag in (X6, F32):
+            C = torch.empty(M, N, device=DEV)
+            K.gemm(A, B, C, trans_b=True, epi=K.EPI_BIAS_TANH, bias=eb, bias_row=t, ld_bias=N, tile=tile | flag)
+            err[flag] = ((C.double() - want).abs() / (scale + 1.0)).max().item()
+        assert err[X6] <= X6_RATIO * err[F32] + X6_FLOOR and err[X6] <= X6_ABS, (tile, err)
     aux = _dev(rng.standard_normal((M, N)).astype(np.float32))
     bias = _dev(rng.standard_normal(N).astype(np.float32))
     want = 0.25 * (acc + bias.double()) + 0.75 * aux.double()
