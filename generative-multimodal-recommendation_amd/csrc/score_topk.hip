@@ -108,7 +108,8 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
                                                 int64_t n_items, const float* __restrict__ I, int64_t ldi,
                                                 const int64_t* __restrict__ mptr, const int* __restrict__ mcols,
                                                 const int* ms, int64_t mbase, float fill, int K,
-                                                unsigned long long (*cb)[ST_CAP], int* cn) {
+                                                unsigned long long (*cb)[ST_CAP], int* cn,
+                                                unsigned long long* trash) {
   constexpr int KS = 16 * DK;
   const int col = lane & 15, grp = lane >> 4;
   auto mask_at = [&](int64_t i) -> int { return STAGED ? ms[i - mbase] : mcols[i]; };
@@ -116,6 +117,7 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
   int64_t mc[4], me[4];
   int nm[4];
   uint32_t tau[4];
+  int cnt[4];  // entries in the buffers of the lane's rows (the same in the 16 lanes of a row group)
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int64_t r = row0 + 4 * grp + e;
@@ -123,14 +125,17 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
     me[e] = r < n_rows ? mptr[r + 1] : 0;
     nm[e] = mc[e] < me[e] ? mask_at(mc[e]) : 0x7fffffff;
     tau[e] = 0;
+    cnt[e] = 0;
   }
   // items [c0, c0 + 64): this lane's 16 consecutive k of item c0 + 16 t + col (clamped: the loads of
-  // a step past the end are issued anyway, so no branch splits the prefetch from its use)
-  auto load_b = [&](int64_t c0, float (&bb)[ST_TILES][KS]) {
+  // a step past the end are issued anyway, so no branch splits the prefetch from its use; 32-bit
+  // offsets, n_items * ldi < 2^31 is checked by the host)
+  const int nlast = (int)n_items - 1, ld32 = (int)ldi;
+  const float* __restrict__ ig = I + KS * grp;
+  auto load_b = [&](int c0, float (&bb)[ST_TILES][KS]) {
 #pragma unroll
     for (int t = 0; t < ST_TILES; ++t) {
-      const int64_t c = min(c0 + 16 * t + col, n_items - 1);
-      const float4* p = reinterpret_cast<const float4*>(I + c * ldi + KS * grp);
+      const float4* p = reinterpret_cast<const float4*>(ig + min(c0 + 16 * t + col, nlast) * ld32);
 #pragma unroll
       for (int q = 0; q < KS / 4; ++q) {
         const float4 x = p[q];
@@ -141,19 +146,25 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
       }
     }
   };
-  auto step = [&](int64_t c0, const float (&b)[ST_TILES][KS]) {
-    f32x4 acc[ST_TILES];
+  auto mfma = [&](const float (&b)[ST_TILES][KS], f32x4 (&acc)[ST_TILES]) {
 #pragma unroll
     for (int t = 0; t < ST_TILES; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int t = 0; t < ST_TILES; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[t][s], acc[t], 0, 0, 0);
-    // train positives of the lane's rows inside [c0, c0 + 64) -> fill
+  };
+  // train positives of the lane's rows inside [c0, c0 + 64) -> fill (a wave-uniform test; the loop
+  // runs only in the rare steps that hold one)
+  auto mask_fix = [&](int c0, f32x4 (&acc)[ST_TILES]) {
+    bool hit = false;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hit |= nm[e] < c0 + ST_STEP;
+    if (!__ballot(hit)) return;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       while (nm[e] < c0 + ST_STEP) {
-        const int d = nm[e] - (int)c0;
+        const int d = nm[e] - c0;
         if (d >= 0 && (d & 15) == col) {
 #pragma unroll
           for (int t = 0; t < ST_TILES; ++t)
@@ -163,48 +174,88 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
         nm[e] = mc[e] < me[e] ? mask_at(mc[e]) : 0x7fffffff;
       }
     }
+  };
+  // candidates of one step, branch-free: a row's slots come from a ballot over the 16 lanes of its group
+  // (tile by tile); a lane with nothing to insert writes its own trash slot
+  const uint32_t below = (1u << col) - 1u;
+  auto filter = [&](int c0, const f32x4 (&acc)[ST_TILES]) {
 #pragma unroll
     for (int t = 0; t < ST_TILES; ++t) {
-      const int64_t c = c0 + 16 * t + col;
-      if (c < n_items) {
+      const int c = c0 + 16 * t + col;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t k = okey(acc[t][e]);
-          if (k > tau[e]) {
-            const int r = 4 * grp + e;
-            const int slot = atomicAdd(&cn[r], 1);
-            cb[r][slot] = ((unsigned long long)(~k) << 32) | (uint32_t)c;
-          }
-        }
-      }
-    }
-    // a row near its capacity (one step adds at most 64): keep its k best, raise its tau
-    const int mine = cn[col];
-    unsigned long long full = __ballot(lane < ST_ROWS && mine > ST_CAP - ST_STEP);
-    while (full) {
-      const int r = __ffsll((long long)full) - 1;
-      full &= full - 1;
-      const uint32_t nt = st_compact(cb[r], cn[r], K, lane);
-      if (lane == 0) cn[r] = K;
-      if (grp == (r >> 2)) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (e == (r & 3)) tau[e] = nt;
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t k = okey(acc[t][e]);
+        const bool in = c < n_items && k > tau[e];
+        const uint32_t g = (uint32_t)(__ballot(in) >> (16 * grp)) & 0xffffu;
+        unsigned long long* dst = in ? &cb[4 * grp + e][cnt[e] + __popc(g & below)] : trash;
+        *dst = ((unsigned long long)(~k) << 32) | (uint32_t)c;
+        cnt[e] += __popc(g);
       }
     }
   };
-  // two register sets, ping-pong: step j computes on one while the other's loads are in flight
+  // a row near its capacity (one step adds at most 64): keep its k best, raise its tau
+  auto compact_check = [&]() {
+    bool near = false;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) near |= cnt[e] > ST_CAP - ST_STEP;
+    if (!__ballot(near)) return;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      unsigned long long full = __ballot(col == 0 && cnt[e] > ST_CAP - ST_STEP);  // one bit per row group
+      while (full) {
+        const int g = (__ffsll((long long)full) - 1) >> 4;
+        full &= full - 1;
+        const int r = 4 * g + e;
+        const int n = __shfl(cnt[e], 16 * g);
+        const uint32_t nt = st_compact(cb[r], n, K, lane);
+        if (grp == g) {
+          tau[e] = nt;
+          cnt[e] = K;
+        }
+      }
+    }
+  };
+  // software pipeline: the MFMAs of step j + 1 are issued between the filter instructions of step j
+  // (independent registers, so the matrix and vector pipes co-execute); two item register sets and two
+  // accumulator sets, the loads of step j + 2 in flight meanwhile
+  auto interleave = [&]() {
+#pragma unroll
+    for (int i = 0; i < ST_TILES * KS; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // four VALU
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // one LDS write
+    }
+  };
   float b0[ST_TILES][KS], b1[ST_TILES][KS];
+  f32x4 acc0[ST_TILES], acc1[ST_TILES];
   load_b(0, b0);
+  load_b(ST_STEP, b1);
+  mfma(b0, acc0);
+  const int ni = (int)n_items;
 #pragma unroll 1
-  for (int64_t c0 = 0; c0 < n_items; c0 += 2 * ST_STEP) {
-    load_b(c0 + ST_STEP, b1);
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs (the scheduler sinks it)
-    step(c0, b0);
-    if (c0 + ST_STEP >= n_items) break;
+  for (int c0 = 0;; c0 += 2 * ST_STEP) {
+    mask_fix(c0, acc0);
     load_b(c0 + 2 * ST_STEP, b0);
     __builtin_amdgcn_sched_barrier(0);
-    step(c0 + ST_STEP, b1);
+    mfma(b1, acc1);
+    filter(c0, acc0);
+    interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    compact_check();
+    if (c0 + ST_STEP >= ni) break;
+    mask_fix(c0 + ST_STEP, acc1);
+    load_b(c0 + 3 * ST_STEP, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma(b0, acc0);
+    filter(c0 + ST_STEP, acc1);
+    interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    compact_check();
+    if (c0 + 2 * ST_STEP >= ni) break;
+  }
+  if (col == 0) {  // the final pass reads the counts from LDS
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cn[4 * grp + e] = cnt[e];
   }
 }
 
@@ -216,6 +267,7 @@ __global__ void __launch_bounds__(64 * ST_WAVES, 1) score_topk_kernel(
   __shared__ unsigned long long cand[ST_WAVES][ST_ROWS][ST_CAP];
   __shared__ int cnt[ST_WAVES][ST_ROWS];
   __shared__ int mstage[ST_WAVES][ST_MSTAGE];
+  __shared__ unsigned long long trash[ST_WAVES][64];  // per-lane sink of the branch-free candidate writes
   constexpr int KS = 16 * DK;  // k values per lane: lane group g holds k in [KS g, KS (g + 1))
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 15, grp = lane >> 4;
   const int64_t row0 = ((int64_t)blockIdx.x * ST_WAVES + w) * ST_ROWS;
@@ -241,9 +293,11 @@ __global__ void __launch_bounds__(64 * ST_WAVES, 1) score_topk_kernel(
   const int64_t mbase = mptr[row0], mend = mptr[min(row0 + ST_ROWS, n_rows)];
   if (mend - mbase <= ST_MSTAGE) {
     for (int64_t i = mbase + lane; i < mend; i += 64) mstage[w][i - mbase] = mcols[i];
-    score_topk_wave<DK, true>(n_rows, row0, lane, a, n_items, I, ldi, mptr, mcols, mstage[w], mbase, fill, K, cb, cn);
+    score_topk_wave<DK, true>(n_rows, row0, lane, a, n_items, I, ldi, mptr, mcols, mstage[w], mbase, fill, K, cb, cn,
+                              &trash[w][lane]);
   } else {
-    score_topk_wave<DK, false>(n_rows, row0, lane, a, n_items, I, ldi, mptr, mcols, mstage[w], mbase, fill, K, cb, cn);
+    score_topk_wave<DK, false>(n_rows, row0, lane, a, n_items, I, ldi, mptr, mcols, mstage[w], mbase, fill, K, cb, cn,
+                              &trash[w][lane]);
   }
   // final: the k best of each row, sorted ascending on the 64-bit key (score desc, item asc)
 #pragma unroll 1
@@ -282,6 +336,7 @@ extern "C" int gmr_score_topk_f32(int64_t n_rows, const int32_t* users, const fl
   GMR_ARG(dim == 64 || dim == 128, "embedding width must be 64 or 128");
   GMR_ARG(k >= 1 && k <= 64 && k <= n_items, "k must be in [1, min(64, n_items)]");
   GMR_ARG(n_items < (1ll << 31) - ST_STEP && ld_idx >= k, "bad sizes");
+  GMR_ARG(n_items * ld_item < (1ll << 31), "item table too large for 32-bit offsets");
   GMR_ARG(ld_user % 4 == 0 && ld_item % 4 == 0 && ld_user >= dim && ld_item >= dim, "leading dims: multiples of 4, >= dim");
   GMR_ARG(((uintptr_t)user_table | (uintptr_t)item_table) % 16 == 0, "tables must be 16-byte aligned");
   const int64_t waves = (n_rows + ST_ROWS - 1) / ST_ROWS;
