@@ -75,6 +75,28 @@ __device__ __forceinline__ float4 wave_groups_sum(float4 a) {
   return gmr::f4_add(a, shx(a, 32));
 }
 
+// lane J of each 8-lane group to the whole group, in registers: DPP row_newbcast (gfx950) broadcasts lane
+// n of each 16-lane row, so two of them (lanes J and 8 + J) and a select by half-row give each group its
+// own lane J (a __shfl is an LDS round trip: the gathers of a round waited on 16 of them in a chain)
+template <int J>
+__device__ __forceinline__ int grp_bcast_t(int x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, x, 0x150 + J, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, x, 0x158 + J, 0xf, 0xf, false);
+  return (threadIdx.x & 8) ? hi : lo;
+}
+__device__ __forceinline__ int grp_bcast(int x, int j) {  // j is a constant after unrolling
+  switch (j) {
+    case 0: return grp_bcast_t<0>(x);
+    case 1: return grp_bcast_t<1>(x);
+    case 2: return grp_bcast_t<2>(x);
+    case 3: return grp_bcast_t<3>(x);
+    case 4: return grp_bcast_t<4>(x);
+    case 5: return grp_bcast_t<5>(x);
+    case 6: return grp_bcast_t<6>(x);
+    default: return grp_bcast_t<7>(x);
+  }
+}
+
 // NS = 32-column slices of the product (d = 32 NS), EB = entries in flight per lane group
 template <int EB, int NS>
 __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __restrict__ plan, SideSrc src,
@@ -149,7 +171,7 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
           int2 cur[EPL];  // this round's entries: their values are shuffled out again at the FMAs
 #pragma unroll
           for (int u = 0; u < EB; ++u) {
-            const int c = __shfl(rec[u / 8].x, gbase + u % 8) & 0x7fffffff;
+            const int c = grp_bcast(rec[u / 8].x, u % 8) & 0x7fffffff;
             xs[u] = f4_zero();
             if (e + u < end) xs[u] = gather(c);
           }
@@ -161,7 +183,7 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
           }
 #pragma unroll
           for (int u = 0; u < EB; ++u)
-            if (e + u < end) acc = gmr::f4_fma(__int_as_float(__shfl(cur[u / 8].y, gbase + u % 8)), xs[u], acc);
+            if (e + u < end) acc = gmr::f4_fma(__int_as_float(grp_bcast(cur[u / 8].y, u % 8)), xs[u], acc);
         }
         acc = wave_groups_sum(acc);
         if (tk.w < 0) {
@@ -223,7 +245,7 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
           xs[u] = f4_zero();
-          if (e + u < end) xs[u] = gather(__shfl(rec[u / 8].x, gbase + u % 8) & 0x7fffffff);
+          if (e + u < end) xs[u] = gather(grp_bcast(rec[u / 8].x, u % 8) & 0x7fffffff);
         }
         // the next round's entries (the next task's first ones after the last round) travel while
         // these gathers land
@@ -238,8 +260,8 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
           if (e + u < end) {
-            acc = gmr::f4_fma(__int_as_float(__shfl(cur[u / 8].y, gbase + u % 8)), xs[u], acc);
-            if (__shfl(cur[u / 8].x, gbase + u % 8) < 0) {  // row end
+            acc = gmr::f4_fma(__int_as_float(grp_bcast(cur[u / 8].y, u % 8)), xs[u], acc);
+            if (grp_bcast(cur[u / 8].x, u % 8) < 0) {  // row end
               store(row, acc);
               ++row;
               acc = f4_zero();

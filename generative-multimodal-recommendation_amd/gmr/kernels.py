@@ -263,8 +263,8 @@ SPMM_CHUNK = 1 << 18  # chunk plan: whole-row tasks of <= 128 entries, one gathe
 # adjacencies): each XCD serves one (side, 32-column slice), lane groups stream <= SPMM_SIDE_T-entry
 # tasks, hub rows combine in-launch.  GMR_SPMM_SIDE=0 keeps every product on the lane plans (A/B)
 SPMM_SIDE = os.environ.get("GMR_SPMM_SIDE", "1") == "1"
-# short-row task entries: 16 for the rebuilt UI graphs (average degree ~2.5: many small tasks), 32 for
-# norm_adj (average degree ~9); GMR_SPMM_SIDE_T overrides (profiles/r03b_sweep.txt)
+# short-row task entries: 16 for every graph (round-3 sweeps with 8 / 12 / 16 / 32 / 64-entry tasks,
+# profiles/r03o_sweep.txt, r03p_sweep.txt: 16 is best or tied at d <= 128); GMR_SPMM_SIDE_T overrides
 SPMM_SIDE_T = int(os.environ.get("GMR_SPMM_SIDE_T", "0"))
 SPMM_SIDE_TW = int(os.environ.get("GMR_SPMM_SIDE_TW", "32"))
 
@@ -310,7 +310,7 @@ class CSR:
         import numpy as np
         lib = _lib.load()
         if T is None:
-            T = SPMM_SIDE_T or (16 if self.nnz < 4 * self.n_rows else 32)
+            T = SPMM_SIDE_T or 16  # 16-entry tasks: norm_adj d = 64 / 128 -10 % vs 32 (profiles/r03o_sweep.txt)
         T = int(T)
         if not T >> 16:
             T |= SPMM_SIDE_TW << 16
@@ -331,7 +331,7 @@ class CSR:
         # workgroups per XCD by product width (profiles/r03b_sweep.txt): the short-task UI graphs and
         # the 64-column products fill the XCDs with 128, the wider norm_adj products with 256
         short = self.nnz < 4 * self.n_rows
-        self.side_wpx = {1: 128, 2: 128 if short else 256, 4: 128 if short else 256}
+        self.side_wpx = {1: 128, 2: 128, 4: 128 if short else 256}
         self.side_hdr = tuple(int(x) for x in host[:16])
         self.partial = torch.zeros(max(nsc, self.partial.numel()), dtype=torch.float32, device=dev)
 
