@@ -331,6 +331,23 @@ __global__ void __launch_bounds__(1024) time_bwd_e_kernel(int T, int E, int H, c
                                                           float* __restrict__ dembB, int accumulate) {
   extern __shared__ __attribute__((aligned(16))) float demb[];  // T * E
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (T * E >= 256) {  // many outputs (DiffRec: T = 100): one thread per output, a serial h loop in 4 chains
+    for (int o = threadIdx.x; o < T * E; o += 1024) {
+      const int t = o / E, i = o % E;
+      const float* srow = S + (int64_t)t * H;
+      const float* wcol = W1 + off + i;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int h = 0;
+      for (; h + 4 <= H; h += 4) {
+        a0 = fmaf(srow[h], wcol[(int64_t)h * ldw], a0);
+        a1 = fmaf(srow[h + 1], wcol[(int64_t)(h + 1) * ldw], a1);
+        a2 = fmaf(srow[h + 2], wcol[(int64_t)(h + 2) * ldw], a2);
+        a3 = fmaf(srow[h + 3], wcol[(int64_t)(h + 3) * ldw], a3);
+      }
+      for (; h < H; ++h) a0 = fmaf(srow[h], wcol[(int64_t)h * ldw], a0);
+      demb[o] = (a0 + a1) + (a2 + a3);
+    }
+  } else  // few outputs (DiffMM: T x E = 50, H = 1000): a wave per output
   for (int o = wv; o < T * E; o += 16) {
     const int t = o / E, i = o % E;
     const float* srow = S + (int64_t)t * H;

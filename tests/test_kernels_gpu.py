@@ -764,7 +764,7 @@ def _side_graph(self_loops, U=3000, I=500, seed=41):
 @pytest.mark.parametrize("self_loops", [0, 1])
 def test_spmm_side_vs_fp64_and_lane(K, nb, self_loops):
     """Side-split plan (csrc/spmm_side.hip): every row within fp32 tolerance of an fp64 product with
-    split sources, alpha / beta; rows of degree <= 32 bit-identical to the lane plan (both sum a
+    split sources, alpha / beta; rows of degree <= T (the plan's task size) bit-identical to the lane plan (both sum a
     short row's entries in CSR order from zero); hub rows (pieces added in order by the last arriving
     piece) identical across repeated launches (the counters re-arm) and with a second scratch."""
     rp, col, val = _side_graph(self_loops)
@@ -794,7 +794,8 @@ def test_spmm_side_vs_fp64_and_lane(K, nb, self_loops):
     scale = 0.7 * (np.abs(a) @ np.abs(src)) + 0.3 * np.abs(Y0) + 1e-6
     err = np.abs(ys.cpu().numpy() - want) / scale
     assert err.max() <= 1e-6, err.max()
-    short = torch.as_tensor(deg <= 32, device=DEV)
+    T = gs.side_hdr[3]  # the plan's short-row bound (H_T): longer rows are hub rows (wave blocks)
+    short = torch.as_tensor(deg <= T, device=DEV)
     assert torch.equal(ys[short].view(torch.int32), yl[short].view(torch.int32))
     for y in outs[2:]:
         assert torch.equal(y.view(torch.int32), ys.view(torch.int32))
