@@ -388,16 +388,20 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const flo
   C[m * ldc + n] = epi_apply(epi, s, m, n, C, ldc);
 }
 
-// tile order inside each XCD's contiguous range: GMR_GEMM_GROUP = G > 1 walks G tile rows per
-// column (the workgroups resident on one XCD then share G A-panels and ~resident/G B-panels of
-// each k slab in its L2 instead of one A-panel and ~resident B-panels); 0/1 = row-major
-int tile_group() {
+// tile order inside each XCD's contiguous range: G > 1 walks G tile rows per column (the workgroups
+// resident on one XCD then share G A-panels and ~resident/G B-panels of each k slab in its L2 instead
+// of one A-panel and ~resident B-panels); 0/1 = row-major.  Default: G = 8 for products at least 32
+// tiles wide, row-major below (measured, profiles/r03t_*: 19445 x 7050 x 1000 fetches 4.8 -> 1.7 GB per
+// launch, the 2048-row diffusion product 457 -> 136 MB, time unchanged; the 8-tile-wide p_sample hidden
+// layer fetches more grouped, 1.9 -> 2.4 GB).  GMR_GEMM_GROUP = G forces G for every product.
+int tile_group(int64_t tn) {
   static const int g = [] {
     const char* e = getenv("GMR_GEMM_GROUP");
-    const int v = e ? atoi(e) : 0;
-    return v < 0 ? 0 : (v > 64 ? 64 : v);
+    const int v = e ? atoi(e) : -1;
+    return v < 0 ? -1 : (v > 64 ? 64 : v);
   }();
-  return g;
+  if (g >= 0) return g;
+  return tn >= 32 ? 8 : 0;
 }
 
 bool inkernel_fixup() {
@@ -775,7 +779,7 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   }
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)(tm * tn), 1, (unsigned)splits);
-  const int tnp = (int)tn | (tile_group() << 20);
+  const int tnp = (int)tn | (tile_group(tn) << 20);
   switch (tile) {
     case 256:
       launch_tile<256, 256, 4, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);

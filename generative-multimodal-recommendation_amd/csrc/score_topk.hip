@@ -9,10 +9,10 @@
 //     item row (B, four float4 per 16-item tile, straight from L2: the table is 1.8 MB at baby);
 //   * the mask: each row's train positives are sorted, so a lane only compares the row's next masked
 //     item with the step's range (a load only when one falls inside);
-//   * selection: per row a candidate buffer of 256 (score key, item) pairs in LDS and a threshold tau =
+//   * selection: per row a candidate buffer of 128 (score key, item) pairs in LDS and a threshold tau =
 //     the k-th best score among the items seen so far.  An item enters only if its score beats tau
 //     STRICTLY (items arrive in increasing index order, so an equal score loses the tie); when a buffer
-//     passes 192 entries the wave selects its k smallest 64-bit keys ((~okey(score)) << 32 | item: unique,
+//     passes 112 entries (checked per 16-item tile) the wave selects its k smallest 64-bit keys ((~okey(score)) << 32 | item: unique,
 //     so there are no ties to break) by a bitwise radix select on ballots, keeps exactly those and raises
 //     tau.  After the last step the k survivors are sorted by a 64-lane bitonic network.
 // The selection is exact (the same k items, in the same order, as a full radix top-k over the masked
@@ -25,10 +25,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int ST_WAVES = 4;     // waves per workgroup (independent: no block barrier)
 constexpr int ST_ROWS = 16;     // rows per wave (one 16 x 16 MFMA tile height)
-constexpr int ST_CAP = 256;     // candidate slots per row
+constexpr int ST_CAP = 128;     // candidate slots per row (two 4-wave workgroups per CU fit the LDS)
 constexpr int ST_TILES = 4;     // 16-item tiles per step
 constexpr int ST_STEP = 16 * ST_TILES;
-constexpr int ST_MSTAGE = 1024;  // masked items of a wave's 16 rows staged in LDS
+constexpr int ST_MSTAGE = 512;   // masked items of a wave's 16 rows staged in LDS
 
 __device__ __forceinline__ uint32_t okey(float f) {  // order-preserving uint32 key
   const uint32_t u = __float_as_uint(f);
@@ -41,10 +41,11 @@ __device__ __forceinline__ float okey_inv(uint32_t k) {
 // Keep the K smallest of the row's n (<= ST_CAP) unique 64-bit entries in slots [0, K) (any order);
 // returns tau = okey of the K-th best score.  Wave-uniform call.
 __device__ uint32_t st_compact(unsigned long long* buf, int n, int K, int lane) {
-  unsigned long long e[4];
-  bool v[4];
+  constexpr int NE = ST_CAP / 64;
+  unsigned long long e[NE];
+  bool v[NE];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NE; ++j) {
     const int i = lane + 64 * j;
     v[j] = i < n;
     e[j] = v[j] ? buf[i] : ~0ull;
@@ -57,7 +58,7 @@ __device__ uint32_t st_compact(unsigned long long* buf, int n, int K, int lane) 
     const uint32_t m = ~0u << b;
     int c = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) c += __popcll(__ballot(v[j] && ((((uint32_t)(e[j] >> 32)) ^ H) & m) == 0));
+    for (int j = 0; j < NE; ++j) c += __popcll(__ballot(v[j] && ((((uint32_t)(e[j] >> 32)) ^ H) & m) == 0));
     if (c < need) {
       need -= c;
       H |= 1u << b;
@@ -65,7 +66,7 @@ __device__ uint32_t st_compact(unsigned long long* buf, int n, int K, int lane) 
   }
   int eq = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) eq += __popcll(__ballot(v[j] && (uint32_t)(e[j] >> 32) == H));
+  for (int j = 0; j < NE; ++j) eq += __popcll(__ballot(v[j] && (uint32_t)(e[j] >> 32) == H));
   uint32_t L = 0xffffffffu;
   if (eq > need) {  // equal scores straddle the cut: the lowest items among them stay
     L = 0;
@@ -74,7 +75,7 @@ __device__ uint32_t st_compact(unsigned long long* buf, int n, int K, int lane) 
       const uint32_t m = ~0u << b;
       int c = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NE; ++j)
         c += __popcll(__ballot(v[j] && (uint32_t)(e[j] >> 32) == H && ((((uint32_t)e[j]) ^ L) & m) == 0));
       if (c < need) {
         need -= c;
@@ -86,7 +87,7 @@ __device__ uint32_t st_compact(unsigned long long* buf, int n, int K, int lane) 
   const unsigned long long lt = (1ull << lane) - 1ull;
   int pos = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NE; ++j) {
     const bool keep = v[j] && e[j] <= T;
     const unsigned long long bal = __ballot(keep);
     if (keep) buf[pos + __popcll(bal & lt)] = e[j];
@@ -178,30 +179,15 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
   // candidates of one step, branch-free: a row's slots come from a ballot over the 16 lanes of its group
   // (tile by tile); a lane with nothing to insert writes its own trash slot
   const uint32_t below = (1u << col) - 1u;
-  auto filter = [&](int c0, const f32x4 (&acc)[ST_TILES]) {
-#pragma unroll
-    for (int t = 0; t < ST_TILES; ++t) {
-      const int c = c0 + 16 * t + col;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t k = okey(acc[t][e]);
-        const bool in = c < n_items && k > tau[e];
-        const uint32_t g = (uint32_t)(__ballot(in) >> (16 * grp)) & 0xffffu;
-        unsigned long long* dst = in ? &cb[4 * grp + e][cnt[e] + __popc(g & below)] : trash;
-        *dst = ((unsigned long long)(~k) << 32) | (uint32_t)c;
-        cnt[e] += __popc(g);
-      }
-    }
-  };
-  // a row near its capacity (one step adds at most 64): keep its k best, raise its tau
+  // a row near its capacity (one tile adds at most 16): keep its k best, raise its tau
   auto compact_check = [&]() {
     bool near = false;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) near |= cnt[e] > ST_CAP - ST_STEP;
+    for (int e = 0; e < 4; ++e) near |= cnt[e] > ST_CAP - 16;
     if (!__ballot(near)) return;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      unsigned long long full = __ballot(col == 0 && cnt[e] > ST_CAP - ST_STEP);  // one bit per row group
+      unsigned long long full = __ballot(col == 0 && cnt[e] > ST_CAP - 16);  // one bit per row group
       while (full) {
         const int g = (__ffsll((long long)full) - 1) >> 4;
         full &= full - 1;
@@ -215,17 +201,25 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
       }
     }
   };
-  // software pipeline: the MFMAs of step j + 1 are issued between the filter instructions of step j
-  // (independent registers, so the matrix and vector pipes co-execute); two item register sets and two
-  // accumulator sets, the loads of step j + 2 in flight meanwhile
-  auto interleave = [&]() {
+  auto filter = [&](int c0, const f32x4 (&acc)[ST_TILES]) {
 #pragma unroll
-    for (int i = 0; i < ST_TILES * KS; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // four VALU
-      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // one LDS write
+    for (int t = 0; t < ST_TILES; ++t) {
+      const int c = c0 + 16 * t + col;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t k = okey(acc[t][e]);
+        const bool in = c < n_items && k > tau[e];
+        const uint32_t g = (uint32_t)(__ballot(in) >> (16 * grp)) & 0xffffu;
+        unsigned long long* dst = in ? &cb[4 * grp + e][cnt[e] + __popc(g & below)] : trash;
+        *dst = ((unsigned long long)(~k) << 32) | (uint32_t)c;
+        cnt[e] += __popc(g);
+      }
+      compact_check();
     }
   };
+  // software pipeline: the MFMAs of step j + 1 are issued before the filter of step j (independent
+  // registers: the matrix pipe runs while the vector pipe filters); two item register sets and two
+  // accumulator sets, the loads of step j + 2 in flight meanwhile
   float b0[ST_TILES][KS], b1[ST_TILES][KS];
   f32x4 acc0[ST_TILES], acc1[ST_TILES];
   load_b(0, b0);
@@ -239,18 +233,12 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
     __builtin_amdgcn_sched_barrier(0);
     mfma(b1, acc1);
     filter(c0, acc0);
-    interleave();
-    __builtin_amdgcn_sched_barrier(0);
-    compact_check();
     if (c0 + ST_STEP >= ni) break;
     mask_fix(c0 + ST_STEP, acc1);
     load_b(c0 + 3 * ST_STEP, b1);
     __builtin_amdgcn_sched_barrier(0);
     mfma(b0, acc0);
     filter(c0 + ST_STEP, acc1);
-    interleave();
-    __builtin_amdgcn_sched_barrier(0);
-    compact_check();
     if (c0 + 2 * ST_STEP >= ni) break;
   }
   if (col == 0) {  // the final pass reads the counts from LDS
@@ -260,7 +248,7 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
 }
 
 template <int DK>
-__global__ void __launch_bounds__(64 * ST_WAVES, 1) score_topk_kernel(
+__global__ void __launch_bounds__(64 * ST_WAVES, DK == 1 ? 2 : 1) score_topk_kernel(
     int64_t n_rows, const int* __restrict__ users, const float* __restrict__ U, int64_t ldu, int64_t n_items,
     const float* __restrict__ I, int64_t ldi, const int64_t* __restrict__ mptr, const int* __restrict__ mcols,
     float fill, int K, int* __restrict__ out_idx, int64_t ld_idx, float* __restrict__ out_val) {
