@@ -268,6 +268,42 @@ __global__ void __launch_bounds__(256) colsum_split_kernel(int64_t rows, int64_t
   if (w == 0 && c < cols) part[(int64_t)blockIdx.y * cols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
+// rows <= 4096, cols % 4 == 0, 16-byte rows: one 1024-thread workgroup per 64 columns; a lane group of 16
+// lanes reads one row's 64 columns as float4, so a wave covers 4 rows and the workgroup 64 rows per pass,
+// eight passes unrolled (their loads in flight together); the 64 partial rows meet in a fixed LDS order.
+// One launch (the split + finish pair cost 15 + 10 us at 2048 x 512).
+__global__ void __launch_bounds__(1024) colsum_wide_kernel(int64_t rows, int64_t cols, const float* __restrict__ x,
+                                                           int64_t ld, float* __restrict__ out, int accumulate) {
+  __shared__ float4 red[64][16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = lane & 15, rr = 4 * w + (lane >> 4);  // column quad, row slot (0..63)
+  const int64_t c = (int64_t)blockIdx.x * 64 + 4 * q;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < cols) {
+    int64_t r = rr;
+    for (; r + 7 * 64 < rows; r += 8 * 64) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(x + (r + 64 * u) * ld + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s = gmr::f4_add(s, v[u]);
+    }
+    for (; r < rows; r += 64) s = gmr::f4_add(s, *reinterpret_cast<const float4*>(x + r * ld + c));
+  }
+  red[rr][q] = s;
+  __syncthreads();
+  if (threadIdx.x < 64) {  // column blockIdx.x * 64 + threadIdx.x: its 64 row-slot partials in order
+    const int cq = threadIdx.x >> 2, ce = threadIdx.x & 3;
+    const int64_t cc = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    float t = 0.f;
+    for (int j = 0; j < 64; ++j) {
+      const float4 p = red[j][cq];
+      t += ce == 0 ? p.x : ce == 1 ? p.y : ce == 2 ? p.z : p.w;
+    }
+    if (cc < cols) out[cc] = accumulate ? out[cc] + t : t;
+  }
+}
+
 __global__ void colsum_split_fin_kernel(int64_t cols, int S, const float* __restrict__ part, float* __restrict__ out,
                                         int accumulate) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -672,6 +708,11 @@ extern "C" int gmr_colsum_split_f32(int64_t rows, int64_t cols, const float* x, 
   GMR_ARG(workspace_floats >= (int64_t)kColSplits * cols, "workspace too small (gmr_colsum_split_floats)");
   hipStream_t st = (hipStream_t)stream;
   const unsigned gx = (unsigned)((cols + 63) / 64);
+  if (rows <= 4096 && cols % 4 == 0 && ld % 4 == 0 && ((uintptr_t)x & 15) == 0) {
+    hipLaunchKernelGGL(colsum_wide_kernel, dim3(gx), dim3(1024), 0, st, rows, cols, x, ld, out, (int)accumulate);
+    GMR_LAUNCHED();
+    return GMR_OK;
+  }
   hipLaunchKernelGGL(colsum_split_kernel, dim3(gx, kColSplits), dim3(256), 0, st, rows, cols, x, ld, workspace);
   GMR_LAUNCHED();
   hipLaunchKernelGGL(colsum_split_fin_kernel, dim3(gmr::grid_for(cols, 256)), dim3(256), 0, st, cols, kColSplits,
