@@ -361,14 +361,17 @@ __global__ void __launch_bounds__(256) time_bwd_h_kernel(int T, int E, int H, co
 // h = l, l + 64, ... in four chains, then a fixed xor butterfly: deterministic); one thread per (t, i)
 // with a serial h loop took 115 us at T x E = 50, H = 1000.  Then
 // d emb_W[i][j] = sum_t demb[t][i] temb[t][j], d emb_b[i] = sum_t demb[t][i]
-__global__ void __launch_bounds__(1024) time_bwd_e_kernel(int T, int E, int H, const float* __restrict__ S,
+// FEW (T x E <= 64): 512 threads (8 waves: 256 VGPRs each for the 64 register accumulators); else 1024
+template <bool FEW>
+__global__ void __launch_bounds__(FEW ? 512 : 1024) time_bwd_e_kernel(int T, int E, int H, const float* __restrict__ S,
                                                           const float* __restrict__ W1, int64_t ldw, int64_t off,
                                                           const float* __restrict__ temb, float* __restrict__ dembW,
                                                           float* __restrict__ dembB, int accumulate) {
   extern __shared__ __attribute__((aligned(16))) float demb[];  // T * E
+  constexpr int kTbeThreads = FEW ? 512 : 1024;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (T * E >= 256) {  // many outputs (DiffRec: T = 100): one thread per output, a serial h loop in 4 chains
-    for (int o = threadIdx.x; o < T * E; o += 1024) {
+  if constexpr (!FEW) {  // many outputs (DiffRec: T = 100): one thread per output, a serial h loop in 4 chains
+    for (int o = threadIdx.x; o < T * E; o += kTbeThreads) {
       const int t = o / E, i = o % E;
       const float* srow = S + (int64_t)t * H;
       const float* wcol = W1 + off + i;
@@ -383,31 +386,48 @@ __global__ void __launch_bounds__(1024) time_bwd_e_kernel(int T, int E, int H, c
       for (; h < H; ++h) a0 = fmaf(srow[h], wcol[(int64_t)h * ldw], a0);
       demb[o] = (a0 + a1) + (a2 + a3);
     }
-  } else  // few outputs (DiffMM: T x E = 50, H = 1000): a wave per output
-  for (int o = wv; o < T * E; o += 16) {
-    const int t = o / E, i = o % E;
-    const float* srow = S + (int64_t)t * H;
-    const float* wcol = W1 + off + i;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int h = lane;
-    for (; h + 192 < H; h += 256) {
-      a0 = fmaf(srow[h], wcol[(int64_t)h * ldw], a0);
-      a1 = fmaf(srow[h + 64], wcol[(int64_t)(h + 64) * ldw], a1);
-      a2 = fmaf(srow[h + 128], wcol[(int64_t)(h + 128) * ldw], a2);
-      a3 = fmaf(srow[h + 192], wcol[(int64_t)(h + 192) * ldw], a3);
+  } else {  // few outputs (DiffMM: T x E = 50, H = 1000): lane = h, every output at once
+    // lane h reads its W1 row's E columns (one line) and S[t][h], accumulates all T x E products of its
+    // h in registers; the partials meet in a fixed order: xor butterfly in each wave, then waves in order
+    constexpr int kMaxTE = 64;
+    __shared__ float wpart[kTbeThreads / 64][kMaxTE];
+    float acc[kMaxTE];
+#pragma unroll
+    for (int o = 0; o < kMaxTE; ++o) acc[o] = 0.f;
+    for (int h = threadIdx.x; h < H; h += kTbeThreads) {
+      const float* wrow = W1 + (int64_t)h * ldw + off;
+      int t = 0, i = 0;  // (t, i) of output o, stepped instead of divided
+#pragma unroll
+      for (int o = 0; o < kMaxTE; ++o) {
+        if (o < T * E) acc[o] = fmaf(S[(int64_t)t * H + h], wrow[i], acc[o]);
+        if (++i == E) {
+          i = 0;
+          ++t;
+        }
+      }
     }
-    for (; h < H; h += 64) a0 = fmaf(srow[h], wcol[(int64_t)h * ldw], a0);
-    const float v = gmr::wave_sum((a0 + a1) + (a2 + a3));
-    if (lane == 0) demb[o] = v;
+#pragma unroll
+    for (int o = 0; o < kMaxTE; ++o) {
+      if (o < T * E) {
+        const float v = gmr::wave_sum(acc[o]);
+        if (lane == 0) wpart[wv][o] = v;
+      }
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < T * E; o += kTbeThreads) {
+      float v = 0.f;
+      for (int j = 0; j < kTbeThreads / 64; ++j) v += wpart[j][o];
+      demb[o] = v;
+    }
   }
   __syncthreads();
-  for (int o = threadIdx.x; o < E * E; o += 1024) {
+  for (int o = threadIdx.x; o < E * E; o += kTbeThreads) {
     const int i = o / E, j = o % E;
     float a = 0.f;
     for (int t = 0; t < T; ++t) a = fmaf(demb[t * E + i], temb[t * E + j], a);
     dembW[o] = accumulate ? dembW[o] + a : a;
   }
-  for (int i = threadIdx.x; i < E; i += 1024) {
+  for (int i = threadIdx.x; i < E; i += kTbeThreads) {
     float a = 0.f;
     for (int t = 0; t < T; ++t) a += demb[t * E + i];
     dembB[i] = accumulate ? dembB[i] + a : a;
@@ -694,8 +714,12 @@ extern "C" int gmr_diff_time_bwd(int32_t T, int32_t E, int32_t H, const float* S
                      col_off, db1, accumulate);
   GMR_LAUNCHED();
   GMR_ARG((size_t)T * E * sizeof(float) <= 60000, "T * E too large for the LDS staging");
-  hipLaunchKernelGGL(time_bwd_e_kernel, dim3(1), dim3(1024), sizeof(float) * (size_t)T * E, st, T, E, H, S, W1, ld_w1,
-                     col_off, temb, d_emb_W, d_emb_b, accumulate);
+  if (T * E <= 64)
+    hipLaunchKernelGGL(time_bwd_e_kernel<true>, dim3(1), dim3(512), sizeof(float) * (size_t)T * E, st, T, E, H, S, W1,
+                       ld_w1, col_off, temb, d_emb_W, d_emb_b, accumulate);
+  else
+    hipLaunchKernelGGL(time_bwd_e_kernel<false>, dim3(1), dim3(1024), sizeof(float) * (size_t)T * E, st, T, E, H, S, W1,
+                       ld_w1, col_off, temb, d_emb_W, d_emb_b, accumulate);
   GMR_LAUNCHED();
   return GMR_OK;
 }
