@@ -361,14 +361,14 @@ __global__ void __launch_bounds__(256) time_bwd_h_kernel(int T, int E, int H, co
 // h = l, l + 64, ... in four chains, then a fixed xor butterfly: deterministic); one thread per (t, i)
 // with a serial h loop took 115 us at T x E = 50, H = 1000.  Then
 // d emb_W[i][j] = sum_t demb[t][i] temb[t][j], d emb_b[i] = sum_t demb[t][i]
-// FEW (T x E <= 64): 512 threads (8 waves: 256 VGPRs each for the 64 register accumulators); else 1024
+// FEW (T x E <= 64): a wave per output; else a thread per output
 template <bool FEW>
-__global__ void __launch_bounds__(FEW ? 512 : 1024) time_bwd_e_kernel(int T, int E, int H, const float* __restrict__ S,
+__global__ void __launch_bounds__(1024) time_bwd_e_kernel(int T, int E, int H, const float* __restrict__ S,
                                                           const float* __restrict__ W1, int64_t ldw, int64_t off,
                                                           const float* __restrict__ temb, float* __restrict__ dembW,
                                                           float* __restrict__ dembB, int accumulate) {
   extern __shared__ __attribute__((aligned(16))) float demb[];  // T * E
-  constexpr int kTbeThreads = FEW ? 512 : 1024;
+  constexpr int kTbeThreads = 1024;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if constexpr (!FEW) {  // many outputs (DiffRec: T = 100): one thread per output, a serial h loop in 4 chains
     for (int o = threadIdx.x; o < T * E; o += kTbeThreads) {
@@ -386,38 +386,24 @@ __global__ void __launch_bounds__(FEW ? 512 : 1024) time_bwd_e_kernel(int T, int
       for (; h < H; ++h) a0 = fmaf(srow[h], wcol[(int64_t)h * ldw], a0);
       demb[o] = (a0 + a1) + (a2 + a3);
     }
-  } else {  // few outputs (DiffMM: T x E = 50, H = 1000): lane = h, every output at once
-    // lane h reads its W1 row's E columns (one line) and S[t][h], accumulates all T x E products of its
-    // h in registers; the partials meet in a fixed order: xor butterfly in each wave, then waves in order
-    constexpr int kMaxTE = 64;
-    __shared__ float wpart[kTbeThreads / 64][kMaxTE];
-    float acc[kMaxTE];
-#pragma unroll
-    for (int o = 0; o < kMaxTE; ++o) acc[o] = 0.f;
-    for (int h = threadIdx.x; h < H; h += kTbeThreads) {
-      const float* wrow = W1 + (int64_t)h * ldw + off;
-      int t = 0, i = 0;  // (t, i) of output o, stepped instead of divided
-#pragma unroll
-      for (int o = 0; o < kMaxTE; ++o) {
-        if (o < T * E) acc[o] = fmaf(S[(int64_t)t * H + h], wrow[i], acc[o]);
-        if (++i == E) {
-          i = 0;
-          ++t;
-        }
+  } else {  // few outputs (DiffMM: T x E = 50, H = 1000): a wave per output, its lanes splitting h
+    // (lane l sums h = l, l + 64, ... in four chains, then a fixed xor butterfly: deterministic).  A lane
+    // per h holding all T x E sums in registers measured slower (52.8 vs 32.5 us: 100 loads per h)
+    for (int o = wv; o < T * E; o += kTbeThreads / 64) {
+      const int t = o / E, i = o % E;
+      const float* srow = S + (int64_t)t * H;
+      const float* wcol = W1 + off + i;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int h = lane;
+      for (; h + 192 < H; h += 256) {
+        a0 = fmaf(srow[h], wcol[(int64_t)h * ldw], a0);
+        a1 = fmaf(srow[h + 64], wcol[(int64_t)(h + 64) * ldw], a1);
+        a2 = fmaf(srow[h + 128], wcol[(int64_t)(h + 128) * ldw], a2);
+        a3 = fmaf(srow[h + 192], wcol[(int64_t)(h + 192) * ldw], a3);
       }
-    }
-#pragma unroll
-    for (int o = 0; o < kMaxTE; ++o) {
-      if (o < T * E) {
-        const float v = gmr::wave_sum(acc[o]);
-        if (lane == 0) wpart[wv][o] = v;
-      }
-    }
-    __syncthreads();
-    for (int o = threadIdx.x; o < T * E; o += kTbeThreads) {
-      float v = 0.f;
-      for (int j = 0; j < kTbeThreads / 64; ++j) v += wpart[j][o];
-      demb[o] = v;
+      for (; h < H; h += 64) a0 = fmaf(srow[h], wcol[(int64_t)h * ldw], a0);
+      const float v = gmr::wave_sum((a0 + a1) + (a2 + a3));
+      if (lane == 0) demb[o] = v;
     }
   }
   __syncthreads();
@@ -715,7 +701,7 @@ extern "C" int gmr_diff_time_bwd(int32_t T, int32_t E, int32_t H, const float* S
   GMR_LAUNCHED();
   GMR_ARG((size_t)T * E * sizeof(float) <= 60000, "T * E too large for the LDS staging");
   if (T * E <= 64)
-    hipLaunchKernelGGL(time_bwd_e_kernel<true>, dim3(1), dim3(512), sizeof(float) * (size_t)T * E, st, T, E, H, S, W1,
+    hipLaunchKernelGGL(time_bwd_e_kernel<true>, dim3(1), dim3(1024), sizeof(float) * (size_t)T * E, st, T, E, H, S, W1,
                        ld_w1, col_off, temb, d_emb_W, d_emb_b, accumulate);
   else
     hipLaunchKernelGGL(time_bwd_e_kernel<false>, dim3(1), dim3(1024), sizeof(float) * (size_t)T * E, st, T, E, H, S, W1,
