@@ -153,3 +153,51 @@ def test_step_slices_cover_every_row_once(monkeypatch, mode, n, B, w):
     assert (seen == 1).all()
     nb = -(-n // B)
     assert steps == (nb if mode == "global" else -(-nb // w))
+
+
+def _early_reduce_main(rank, world, port, out_q):
+    """gmr.trainer.reduce_slab_grads with a model that all-reduces the head of one slab from inside its
+    step (DiffMM's E0 gradient): rank 0 ran the step (head already in flight), rank 1 was idle in a short
+    last batch and issues both reduces itself; the collectives must match and the sums be exact."""
+    import sys
+    from types import SimpleNamespace
+    for p in (ROOT, os.path.join(ROOT, "generative-multimodal-recommendation_amd")):
+        sys.path.insert(0, p)
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    from gmr import dist
+    from gmr.trainer import reduce_slab_grads
+    s0 = SimpleNamespace(grad=torch.arange(10, dtype=torch.float32) * (rank + 1))
+    s1 = SimpleNamespace(grad=torch.full((4,), float(rank + 7)))
+
+    class Model:
+        early = dist.all_reduce_start(s0.grad[:3]) if rank == 0 else None
+
+        def early_reduce_cut(self, slab):
+            return 3 if slab is s0 else None
+
+        def take_early_reduce(self):
+            h, Model.early = Model.early, None
+            return h
+
+    reduce_slab_grads(Model(), [s0, s1])
+    out_q.put((rank, s0.grad.numpy().copy(), s1.grad.numpy().copy()))
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_reduce_slab_grads_early_head_and_idle_rank():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_early_reduce_main, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for _, g0, g1 in res:
+        np.testing.assert_array_equal(g0, np.arange(10, dtype=np.float32) * 3)
+        np.testing.assert_array_equal(g1, np.full(4, 15.0, np.float32))
