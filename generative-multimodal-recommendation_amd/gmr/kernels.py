@@ -534,6 +534,8 @@ def score_topk(usr, itm, users, mask_ptr, mask_cols, k, out_idx, out_val=None, f
     n = users.numel() if users is not None else out_idx.shape[0]
     if out_idx.shape[0] < n or mask_ptr.numel() < n + 1 or mask_ptr.dtype != torch.int64:
         raise ValueError("score_topk: out_idx / mask_ptr (int64, n + 1) too small for the rows")
+    if n == 0:  # an empty rank shard: nothing to score (the C-ABI rejects n_rows < 1)
+        return out_idx
     _lib.call("gmr_score_topk_f32", n, ptr(users), ptr(usr), _ld(usr), itm.shape[0], ptr(itm), _ld(itm), itm.shape[1],
               ptr(mask_ptr), ptr(mask_cols), float(fill), int(k), ptr(out_idx), _ld(out_idx), ptr(out_val), stream())
     return out_idx

@@ -76,6 +76,48 @@ def test_users_none_and_empty_masks():
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("D,n_items,k", [(64, 5000, 50), (128, 3001, 64), (64, 700, 1)])
+def test_all_scores_tied(D, n_items, k):
+    """Zero embeddings: every item scores 0, so every tile fills the candidate buffer with ties and
+    the compaction must keep the lowest indices (masked items excluded)."""
+    rng = np.random.default_rng(D + k)
+    n_rows = 40
+    U = np.zeros((n_rows, D), np.float32)
+    I = np.zeros((n_items, D), np.float32)
+    rows, ptr, cols = _mask(rng, n_rows, n_items, 60)
+    want, _ = _expected(np.zeros((n_rows, n_items)), rows, k)
+    got, val = _run(U, I, None, ptr, cols, k, want_val=True)
+    np.testing.assert_array_equal(got, want)
+    assert (val == 0).all()
+
+
+@pytest.mark.parametrize("D,sign", [(64, 1), (64, -1), (128, 1)])
+def test_monotone_scores(D, sign):
+    """Scores strictly increasing (sign 1: every tile beats the running top-k, the most compactions)
+    or decreasing (sign -1: the threshold rejects everything after the first tiles) with item index."""
+    rng = np.random.default_rng(D)
+    n_rows, n_items, k = 24, 6000, 50
+    U = np.zeros((n_rows, D), np.float32)
+    U[:, 0] = sign * (1 + np.arange(n_rows))  # integer-valued: exact fp32 dots
+    I = np.zeros((n_items, D), np.float32)
+    I[:, 0] = np.arange(n_items)
+    rows, ptr, cols = _mask(rng, n_rows, n_items, 30)
+    want, s = _expected(U.astype(np.int64) @ I.T.astype(np.int64), rows, k)
+    got, val = _run(U, I, None, ptr, cols, k, want_val=True)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(val, np.take_along_axis(s, want, 1).astype(np.float32))
+
+
+def test_zero_rows_is_a_no_op():
+    from gmr import kernels as K
+    out = torch.full((1, 20), -7, dtype=torch.int32, device=DEV)
+    K.score_topk(torch.zeros((4, 64), device=DEV), torch.zeros((100, 64), device=DEV),
+                 torch.zeros(0, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int64, device=DEV),
+                 torch.zeros(1, dtype=torch.int32, device=DEV), 20, out)
+    torch.cuda.synchronize()
+    assert (out.cpu() == -7).all()
+
+
 def test_float_embeddings_vs_unfused_path():
     """Real-valued embeddings: the fused result equals the unfused GEMM + mask + radix top-k wherever
     the fp64 scores are not within 1e-5 (relative) of a tie."""
