@@ -20,6 +20,27 @@ def test_header_and_binding_agree():
     assert _header_symbols() == sorted(_lib.SIGNATURES)
 
 
+def test_binding_arity_matches_header():
+    """Every ctypes argtypes list matches the header declaration parameter by parameter (a missing,
+    extra or mistyped argument would shift or truncate every later one silently)."""
+    from gmr import _lib
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "gmr.h")).read(), flags=re.S)
+    txt = re.sub(r"//[^\n]*", "", txt)
+    decls = dict(re.findall(r"\b(gmr_\w+)\s*\(([^)]*)\)\s*;", txt))
+    assert set(decls) == set(_lib.SIGNATURES)
+    ctype = {"int64_t": _lib.I64, "int32_t": _lib.I32, "uint64_t": _lib.U64, "float": _lib.F32,
+             "double": _lib.F64}
+    bad = {}
+    for name, params in decls.items():
+        params = [p.strip() for p in params.split(",") if p.strip() not in ("", "void")]
+        want = [(_lib.P, _lib.CP) if "*" in p else (ctype[re.sub(r"^const\s+|\s+\w+$", "", p)],)
+                for p in params]
+        got = _lib.SIGNATURES[name][1]
+        if len(want) != len(got) or any(g not in w for g, w in zip(got, want)):
+            bad[name] = (params, got)
+    assert not bad, bad
+
+
 def test_library_exports_every_symbol():
     import ctypes
 
