@@ -62,7 +62,7 @@ __global__ void flip_schedule_kernel(int B, const int* __restrict__ users, const
 __global__ void flip_qsample_kernel(int B, int I, const float* __restrict__ x0, int64_t ld0, const int* __restrict__ t,
                                     int t_const, const float* __restrict__ tab, int T, float temp,
                                     const uint8_t* __restrict__ flip, int64_t ldf, uint64_t seed, uint64_t step,
-                                    float* __restrict__ xt, int64_t ldt) {
+                                    int64_t row0, float* __restrict__ xt, int64_t ldt) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)B * I) return;
   const int b = (int)(gid / I), i = (int)(gid % I);
@@ -73,7 +73,7 @@ __global__ void flip_qsample_kernel(int B, int I, const float* __restrict__ x0, 
   } else {
     const int tt = t ? t[b] : t_const;
     const float a = x == 0.f ? tab[tt] : tab[T + tt];
-    const uint4 r = gmr::Philox::gen(seed, step, (uint64_t)gid);
+    const uint4 r = gmr::Philox::gen(seed, step, (uint64_t)((row0 + b) * I + i));
     const float p = sigm((a - unit01(r.x)) * temp);
     f = unit01(r.y) < p;
   }
@@ -85,8 +85,8 @@ __global__ void flip_qsample_kernel(int B, int I, const float* __restrict__ x0, 
 // Bernoulli(probs) on the last step; draws (0/1 bytes) replace the Bernoulli when given
 __global__ void flip_step_kernel(int B, int I, const float* __restrict__ z, int64_t ldz, const float* __restrict__ tab,
                                  int T, int qi, int last, const uint8_t* __restrict__ draws, int64_t ldd, uint64_t seed,
-                                 uint64_t step, float* __restrict__ x, int64_t ldx, float* __restrict__ probs,
-                                 int64_t ldp) {
+                                 uint64_t step, int64_t row0, float* __restrict__ x, int64_t ldx,
+                                 float* __restrict__ probs, int64_t ldp) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)B * I) return;
   const int b = (int)(gid / I), i = (int)(gid % I);
@@ -103,7 +103,7 @@ __global__ void flip_step_kernel(int B, int I, const float* __restrict__ z, int6
   if (draws) {
     v = draws[(int64_t)b * ldd + i] ? 1.f : 0.f;
   } else {
-    const uint4 r = gmr::Philox::gen(seed, step, (uint64_t)gid);
+    const uint4 r = gmr::Philox::gen(seed, step, (uint64_t)((row0 + b) * I + i));
     v = unit01(r.x) < q ? 1.f : 0.f;
   }
   x[(int64_t)b * ldx + i] = v;
@@ -327,7 +327,8 @@ __global__ void adaln_bwd_kernel(int64_t rows, int D, const float* __restrict__ 
 // mask_out), else read from mask_in
 __global__ void dropout_kernel(int64_t rows, int D, int group, const float* __restrict__ x, int64_t ldx,
                                float p_keep, const uint8_t* __restrict__ mask_in, uint8_t* __restrict__ mask_out,
-                               int64_t ldm, uint64_t seed, uint64_t step, float* __restrict__ y, int64_t ldy) {
+                               int64_t ldm, uint64_t seed, uint64_t step, int64_t row0, float* __restrict__ y,
+                               int64_t ldy) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= rows * D) return;
   const int64_t r = gid / D;
@@ -337,7 +338,7 @@ __global__ void dropout_kernel(int64_t rows, int D, int group, const float* __re
   if (mask_in) {
     k = mask_in[r * ldm + mc] != 0;
   } else {
-    const uint4 rr = gmr::Philox::gen(seed, step, (uint64_t)(r * (D / group) + mc));
+    const uint4 rr = gmr::Philox::gen(seed, step, (uint64_t)((row0 + r) * (D / group) + mc));
     k = unit01(rr.x) < p_keep;
     if (mask_out && c % group == 0) mask_out[r * ldm + mc] = k ? 1 : 0;
   }
@@ -390,21 +391,21 @@ extern "C" int gmr_flip_schedule(int32_t B, const int32_t* users, const int32_t*
 
 extern "C" int gmr_flip_qsample(int32_t B, int32_t I, const float* x0, int64_t ld0, const int32_t* t, int32_t t_const,
                                 const float* tables, int32_t T, float temp, const uint8_t* flip, int64_t ld_flip,
-                                uint64_t seed, uint64_t step, float* xt, int64_t ldt, void* stream) {
-  GMR_ARG(x0 && tables && xt && B > 0 && I > 0, "bad args");
+                                uint64_t seed, uint64_t step, int64_t row0, float* xt, int64_t ldt, void* stream) {
+  GMR_ARG(x0 && tables && xt && B > 0 && I > 0 && row0 >= 0, "bad args");
   GMR_ARG(t || (t_const >= 0 && t_const < T), "bad t");
   hipLaunchKernelGGL(flip_qsample_kernel, dim3(gmr::grid_for((int64_t)B * I, 256)), dim3(256), 0, (hipStream_t)stream,
-                     B, I, x0, ld0, t, t_const, tables, T, temp, flip, ld_flip, seed, step, xt, ldt);
+                     B, I, x0, ld0, t, t_const, tables, T, temp, flip, ld_flip, seed, step, row0, xt, ldt);
   GMR_LAUNCHED();
   return GMR_OK;
 }
 
 extern "C" int gmr_flip_step(int32_t B, int32_t I, const float* z, int64_t ldz, const float* tables, int32_t T,
-                             int32_t qi, int32_t last, const uint8_t* draws, int64_t ldd, uint64_t seed, uint64_t step, float* x,
-                             int64_t ldx, float* probs, int64_t ldp, void* stream) {
-  GMR_ARG(z && tables && x && B > 0 && I > 0 && qi >= 0 && qi < T, "bad args");
+                             int32_t qi, int32_t last, const uint8_t* draws, int64_t ldd, uint64_t seed, uint64_t step,
+                             int64_t row0, float* x, int64_t ldx, float* probs, int64_t ldp, void* stream) {
+  GMR_ARG(z && tables && x && B > 0 && I > 0 && qi >= 0 && qi < T && row0 >= 0, "bad args");
   hipLaunchKernelGGL(flip_step_kernel, dim3(gmr::grid_for((int64_t)B * I, 256)), dim3(256), 0, (hipStream_t)stream, B,
-                     I, z, ldz, tables, T, qi, last, draws, ldd, seed, step, x, ldx, probs, ldp);
+                     I, z, ldz, tables, T, qi, last, draws, ldd, seed, step, row0, x, ldx, probs, ldp);
   GMR_LAUNCHED();
   return GMR_OK;
 }
@@ -495,11 +496,11 @@ extern "C" int gmr_adaln_bwd(int64_t rows, int32_t D, const float* h0, int64_t l
 
 extern "C" int gmr_dropout_f32(int64_t rows, int32_t D, int32_t group, const float* x, int64_t ldx, float p_keep,
                                const uint8_t* mask_in, uint8_t* mask_out, int64_t ldm, uint64_t seed, uint64_t step,
-                               float* y, int64_t ldy, void* stream) {
-  GMR_ARG(x && y && rows > 0 && D > 0 && group >= 1 && D % group == 0, "bad args");
+                               int64_t row0, float* y, int64_t ldy, void* stream) {
+  GMR_ARG(x && y && rows > 0 && D > 0 && group >= 1 && D % group == 0 && row0 >= 0, "bad args");
   GMR_ARG(p_keep > 0.f && p_keep <= 1.f, "p_keep in (0, 1]");
   hipLaunchKernelGGL(dropout_kernel, dim3(gmr::grid_for(rows * D, 256)), dim3(256), 0, (hipStream_t)stream, rows, D,
-                     group, x, ldx, p_keep, mask_in, mask_out, ldm, seed, step, y, ldy);
+                     group, x, ldx, p_keep, mask_in, mask_out, ldm, seed, step, row0, y, ldy);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -570,10 +570,11 @@ __global__ void mul_flat_kernel(int64_t n, const float* __restrict__ a, const fl
 }
 
 // Bernoulli(p_keep) keep bytes (nn.Dropout masks of the modal projections)
-__global__ void keep_mask_kernel(int64_t n, float p_keep, uint64_t seed, uint64_t step, uint8_t* __restrict__ out) {
+__global__ void keep_mask_kernel(int64_t n, float p_keep, uint64_t seed, uint64_t step, uint64_t ctr0,
+                                 uint8_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint4 r = gmr::Philox::gen(seed, step, (uint64_t)i);
+  const uint4 r = gmr::Philox::gen(seed, step, ctr0 + (uint64_t)i);
   out[i] = (float)(r.x >> 8) * (1.0f / 16777216.0f) < p_keep ? 1 : 0;
 }
 
@@ -749,10 +750,11 @@ extern "C" int gmr_mul_f32(int64_t n, const float* a, const float* b, float* out
   return GMR_OK;
 }
 
-extern "C" int gmr_keep_mask_u8(int64_t n, float p_keep, uint64_t seed, uint64_t step, uint8_t* out, void* stream) {
+extern "C" int gmr_keep_mask_u8(int64_t n, float p_keep, uint64_t seed, uint64_t step, uint64_t ctr0, uint8_t* out,
+                                void* stream) {
   GMR_ARG(out && n > 0 && p_keep > 0.f && p_keep <= 1.f, "bad args");
   hipLaunchKernelGGL(keep_mask_kernel, dim3(gmr::grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, p_keep, seed,
-                     step, out);
+                     step, ctr0, out);
   GMR_LAUNCHED();
   return GMR_OK;
 }

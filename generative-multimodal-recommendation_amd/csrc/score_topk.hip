@@ -281,6 +281,10 @@ __global__ void __launch_bounds__(64 * ST_WAVES, DK == 1 ? 2 : 1) score_topk_ker
   const int64_t mbase = mptr[row0], mend = mptr[min(row0 + ST_ROWS, n_rows)];
   if (mend - mbase <= ST_MSTAGE) {
     for (int64_t i = mbase + lane; i < mend; i += 64) mstage[w][i - mbase] = mcols[i];
+    // other lanes of this wave read the staged entries: order the LDS writes before those reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     score_topk_wave<DK, true>(n_rows, row0, lane, a, n_items, I, ldi, mptr, mcols, mstage[w], mbase, fill, K, cb, cn,
                               &trash[w][lane]);
   } else {

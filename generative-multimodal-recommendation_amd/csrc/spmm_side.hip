@@ -432,6 +432,8 @@ extern "C" int gmr_spmm_side_plan_build(const int32_t* rowptr_host, int64_t n_ro
   const int64_t nnz = rowptr_host[n_rows];
   const SideLayout l = side_layout(p, nnz);
   GMR_ARG(words >= l.words, "plan buffer smaller than gmr_spmm_side_plan_words(...)");
+  // hub partial rows are addressed by 32-bit buffer offsets (slot * 256 + column) * 4 bytes
+  GMR_ARG((int64_t)p.slotmap.size() * 1024 < INT32_MAX, "too many hub slots for 32-bit partial offsets");
   int32_t* h = plan_host;
   h[H_MAGIC] = kSideMagic;
   h[H_NROWS] = (int)n_rows;

@@ -128,7 +128,7 @@ SIGNATURES = {
     "gmr_bpr_logsigmoid_f32": (I32, [I32, I64, P, P, P, P, P, P, F32, P]),
     "gmr_axpy_dev_f32": (I32, [I64, P, P, P, P]),
     "gmr_mul_f32": (I32, [I64, P, P, P, P]),
-    "gmr_keep_mask_u8": (I32, [I64, F32, U64, U64, P, P]),
+    "gmr_keep_mask_u8": (I32, [I64, F32, U64, U64, U64, P, P]),
     "gmr_csr_transpose": (I32, [I64, I64, I64, P, P, P, P, P, P, P, P, P, P]),
     "gmr_csr_drop_count": (I32, [I64, P, P, I32, P, F32, U64, U64, P, P, P]),
     "gmr_csr_drop_write": (I32, [I64, P, P, P, I32, P, F32, U64, U64, P, P, P, P]),
@@ -144,8 +144,8 @@ SIGNATURES = {
     "gmr_kmeans_assign": (I32, [I64, I32, P, I64, P, P, P, P, I64, P, P, P]),
     "gmr_kmeans_centroids": (I32, [I32, I32, P, I64, P, I64, I64, P, I64, P, P]),
     "gmr_flip_schedule": (I32, [I32, P, P, I32, I32, P, P]),
-    "gmr_flip_qsample": (I32, [I32, I32, P, I64, P, I32, P, I32, F32, P, I64, U64, U64, P, I64, P]),
-    "gmr_flip_step": (I32, [I32, I32, P, I64, P, I32, I32, I32, P, I64, U64, U64, P, I64, P, I64, P]),
+    "gmr_flip_qsample": (I32, [I32, I32, P, I64, P, I32, P, I32, F32, P, I64, U64, U64, I64, P, I64, P]),
+    "gmr_flip_step": (I32, [I32, I32, P, I64, P, I32, I32, I32, P, I64, U64, U64, I64, P, I64, P, I64, P]),
     "gmr_flip_loss_rows": (I32, [I32, I32, P, I64, P, I64, P, P, I32, F32, P, I64, P, P, P]),
     "gmr_flip_total": (I32, [P, P, F32, P, P]),
     "gmr_layernorm_fwd": (I32, [I64, I32, P, I64, P, I64, P, I64, F32, P, P, F32, I32, P, I64, P, I64, P, P, P]),
@@ -153,7 +153,7 @@ SIGNATURES = {
     "gmr_layernorm_bwd": (I32, [I64, I32, P, I64, P, P, P, P, I32, P, I64, P, I64, I32, P, P, P, I32, P]),
     "gmr_adaln_fwd": (I32, [I64, I32, P, I64, P, I32, P, I64, P, I64, P]),
     "gmr_adaln_bwd": (I32, [I64, I32, P, I64, P, I64, P, P, I64, P, I64, P, I64, P]),
-    "gmr_dropout_f32": (I32, [I64, I32, I32, P, I64, F32, P, P, I64, U64, U64, P, I64, P]),
+    "gmr_dropout_f32": (I32, [I64, I32, I32, P, I64, F32, P, P, I64, U64, U64, I64, P, I64, P]),
     "gmr_time_embedding": (I32, [I32, I32, P, P]),
     "gmr_silu_f32": (I32, [I64, P, P, P, P]),
 }

@@ -162,6 +162,11 @@ class DiffMM(GeneralRecommender):
         self._step = 0
         self._rebuilds = 0
         self._streams = K.Streams(2)
+        # data parallel: rec_step starts E0's gradient all-reduce itself only when the caller consumes
+        # the handle (Trainer sets this and reduces through reduce_slab_grads); off, the caller reduces
+        # the whole slab after the step
+        self.dp_early_reduce = False
+        self._early = None
         self._sq_parts = int(_lib.load().gmr_sqnorm_nparts(self.N * 64))
 
     # ================================================================= buffers
@@ -363,9 +368,12 @@ class DiffMM(GeneralRecommender):
         E0 = s.view("E0")
         _lib.call("gmr_dmm_assemble", N, U, ptr(w["T2"]), ptr(w["T3"]), ptr(w["OutI"]), ptr(w["OutT"]), ptr(E0),
                   2.0 * self.reg_weight * reg_share, ptr(s.gview("E0")), ptr(w["dNF"]), stream())
-        if dist.is_dist() and EARLY_REDUCE:
+        if dist.is_dist() and EARLY_REDUCE and self.dp_early_reduce:
             # data parallel: E0's gradient (6.8 MB of the 7.9 MB slab) is final here; its RCCL all-reduce
             # runs beside the projection-weight GEMMs below (the Trainer reduces the rest and waits)
+            if self._early is not None:
+                raise RuntimeError("rec_step: the previous step's early all-reduce was never taken "
+                                   "(reduce_slab_grads consumes it)")
             self._early = dist.all_reduce_start(s.grad[:self.early_reduce_cut(s)])
         # modality projections: normalize + leaky-relu backward, then W grads (text beside image)
         dNF = w["dNF"]
@@ -381,12 +389,12 @@ class DiffMM(GeneralRecommender):
     def early_reduce_cut(self, slab):
         """Gradient words of `slab` that rec_step all-reduces itself (E0, issued as soon as it is final);
         the Trainer reduces [cut:) and waits (idle ranks issue the same two reduces).  None: whole slab."""
-        if slab is not self.rec_slab or not EARLY_REDUCE:
+        if slab is not self.rec_slab or not EARLY_REDUCE or not self.dp_early_reduce:
             return None
         return slab.offsets["image_trans"]
 
     def take_early_reduce(self):
-        h, self._early = getattr(self, "_early", None), None
+        h, self._early = self._early, None
         return h
 
     def _transpose_of(self, g):
@@ -509,7 +517,7 @@ class DiffMM(GeneralRecommender):
         return scores
 
     @torch.no_grad()
-    def topk_from_embeddings(self, usr, itm, users_i32, mask_rows, mask_cols, k, out_idx, scores_buf):
+    def topk_from_embeddings(self, usr, itm, users_i32, mask_rows, mask_cols, k, out_idx, scores_buf, out_val=None):
         """scores -> mask train positives (-1e10) -> top-k (trainer.py:379-386), all on the device."""
         E = users_i32.numel()
         ub = scores_buf.new_empty((E, 64))
@@ -517,7 +525,7 @@ class DiffMM(GeneralRecommender):
         sc = scores_buf[:E, :self.n_items]
         K.gemm(ub, itm, sc, trans_b=True)
         K.mask_scores(sc, mask_rows, mask_cols)
-        K.topk_rows(sc, k, out_idx)
+        K.topk_rows(sc, k, out_idx, out_val)
         return out_idx
 
     # ================================================================= diffusion

@@ -5,8 +5,9 @@ F2); this module holds the sharding rules used by the trainers:
   * diffusion phase  — each batch of train_batch_size users of the epoch permutation is split
     over the ranks (contiguous slices); denoiser gradients are all-reduced (SUM of per-rank sums
     normalised by the batch's row count) before the identical Adam steps;
-  * graph rebuild    — users are split in contiguous shards; each rank p_samples its shard and
-    the int32 top-k lists are all-gathered; every rank builds the identical CSR;
+  * graph rebuild    — users are split in contiguous shards (GenRecV1: whole batch chunks dealt
+    round-robin); each rank p_samples its users and the int32 top-k lists are exchanged; every
+    rank builds the identical CSR;
   * BPR phase        — each train_batch_size batch of the epoch draw is split over the ranks;
     the rec gradients are all-reduced (the regulariser is counted once);
   * evaluation       — eval users are sharded; the top-K index rows are all-gathered.
@@ -14,10 +15,11 @@ The global batch is the reference's train_batch_size at every world size, so the
 optimiser steps per epoch, and the trajectory up to fp32 reassociation of the sums, are the
 single-process ones (the per-GPU batch shrinks as B / world: strong scaling).  DiffMM and DiffRec
 key every device draw by (global step, global row), so their draws are also the single-process
-ones at any world size; GenRecV1's diffusion phase and rebuild key their Philox streams by
-(step, rank) and the value-only InfoNCE of its diffusion loss (genrecv1.py:577-582) is taken over
-the rank's rows, so its DP run is the same objective with differently drawn noise (its rec step's
-in-batch InfoNCE is the global batch's, tests/test_dist_gpu.py).
+ones at any world size.  GenRecV1 does the same: its diffusion draws (t, flips, dropout masks) are
+keyed by (global step, global row), the value-only InfoNCE of its diffusion loss (genrecv1.py:577-582)
+takes the whole step's rows as keys (gather_step_rows), and its rebuild deals whole train_batch_size
+chunks of users round-robin over the ranks, each chunk drawing what it draws in one process
+(tests/test_dist_gpu.py).
 
 Opt-in GMR_DP_MODE=local ("partition users across the GPUs", BASELINE north star): every rank
 takes whole train_batch_size batches (rank r takes batch g * world + r of global step g), so one
@@ -143,6 +145,20 @@ def all_gather_rows_(full, size):
             for i, p in enumerate(parts):
                 full[i * size:(i + 1) * size].copy_(p)
     return full
+
+
+def gather_step_rows(local, rank_rows):
+    """Rows of one global step held by each rank (rank q holds rank_rows[q] rows, 0 = idle) -> the
+    step's rows in rank order on every rank (one padded all-gather; idle ranks pass an empty slice)."""
+    if not is_dist():
+        return local
+    w, r = world(), rank()
+    m = max(max(rank_rows), 1)
+    full = local.new_zeros((w * m,) + tuple(local.shape[1:]))
+    if rank_rows[r]:
+        full[r * m:r * m + rank_rows[r]].copy_(local[:rank_rows[r]])
+    all_gather_rows_(full, m)
+    return torch.cat([full[q * m:q * m + rank_rows[q]] for q in range(w)])
 
 
 def barrier():

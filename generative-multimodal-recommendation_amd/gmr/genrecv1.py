@@ -283,7 +283,7 @@ class GenRecV1(GeneralRecommender):
                 if given is not None:
                     mk[2 * m + j].copy_(torch.as_tensor(given, dtype=torch.uint8))
                 else:
-                    _lib.call("gmr_keep_mask_u8", I * 64, 0.9, self.seed, self._mask_step(m, j), ptr(mk[2 * m + j]),
+                    _lib.call("gmr_keep_mask_u8", I * 64, 0.9, self.seed, self._mask_step(m, j), 0, ptr(mk[2 * m + j]),
                               stream())
         self._linear(X, f"{mod}_residual_project_0", w["Zr"][m])
         self._bn(w, c0, w["Zr"][m], I, ACT_LEAKY, train, y=w["Xr"][m], keep=mk[2 * m] if train else None)
@@ -411,9 +411,13 @@ class GenRecV1(GeneralRecommender):
         B = users.numel()
         dev = self.device
         keys = torch.stack([users, pos]).to(torch.int32).contiguous()
-        offs = torch.tensor([0, B], dtype=torch.int64, device=dev)
+        # the constant operands are built once (per B): torch.tensor(..., device) is a blocking copy
+        cache = self.__dict__.setdefault("_plan2_const", {})
+        if B not in cache:
+            cache[B] = (torch.tensor([0, B], dtype=torch.int64, device=dev),
+                        torch.tensor([0, self.n_users], dtype=torch.int32, device=dev))
+        offs, ka = cache[B]
         pc = torch.empty((1, 1 << max(1, (2 * B - 1).bit_length())), dtype=torch.int64, device=dev)
-        ka = torch.tensor([0, self.n_users], dtype=torch.int32, device=dev)
         _lib.call("gmr_sort_batch_keys", 1, ptr(keys), ptr(offs), ptr(ka), 2, B, ptr(pc), pc.shape[1], pc.shape[1],
                   stream())
         return pc[0]
@@ -555,14 +559,14 @@ class GenRecV1(GeneralRecommender):
         return out
 
     @torch.no_grad()
-    def topk_from_embeddings(self, usr, itm, users_i32, mask_rows, mask_cols, k, out_idx, scores_buf):
+    def topk_from_embeddings(self, usr, itm, users_i32, mask_rows, mask_cols, k, out_idx, scores_buf, out_val=None):
         E = users_i32.numel()
         ub = scores_buf.new_empty((E, 64))
         K.gather_rows(usr, users_i32, ub)
         sc = scores_buf[:E, :self.n_items]
         self._score(ub, itm, sc)
         K.mask_scores(sc, mask_rows, mask_cols)
-        K.topk_rows(sc, k, out_idx)
+        K.topk_rows(sc, k, out_idx, out_val)
         return out_idx
 
     def extra_state(self):
@@ -631,10 +635,11 @@ class FlipDiffusion:
                   ptr(w["tab"]), stream())
         return w["tab"]
 
-    def p_sample(self, den, x0, tab, seed, step, inject=None, probs_out=None, q_steps=None):
+    def p_sample(self, den, x0, tab, seed, step, inject=None, probs_out=None, q_steps=None, row0=0):
         """p_sample(steps = q_steps, bayesian) (:528-548): q_sample at t = q_steps - 1 (none when
         q_steps = 0), then T model calls; the Bayesian step's coefficients are the q_sample tables at
-        that t (:541-542 re-index the q_sample tensors).  Returns the final x and the last probs."""
+        that t (:541-542 re-index the q_sample tensors).  Returns the final x and the last probs.
+        Draws are keyed by (step, row0 + row): x0's rows are rows [row0, row0 + B) of the step."""
         B, I = x0.shape
         w = self._w
         T = self.steps
@@ -645,23 +650,27 @@ class FlipDiffusion:
         inj = inject or {}
         flip = inj.get("flip")
         _lib.call("gmr_flip_qsample", B, I, ptr(x0), x0.stride(0), None, qs - 1, ptr(tab), T, self.base_temp,
-                  ptr(flip), flip.stride(0) if flip is not None else 0, seed, step * 16, ptr(xt), xt.stride(0), stream())
+                  ptr(flip), flip.stride(0) if flip is not None else 0, seed, step * 16, row0, ptr(xt), xt.stride(0),
+                  stream())
         probs = probs_out if probs_out is not None else w["probs"][:B, :I]
         for j, i in enumerate(reversed(range(T))):
-            den.forward(xt, t_const=i, T=T, out=z, seed=seed, step=step * 16 + 1 + j)
+            den.forward(xt, t_const=i, T=T, out=z, seed=seed, step=step * 16 + 1 + j, row0=row0)
             draws = inj.get("draws")
             dr = draws[j] if draws is not None else None
             _lib.call("gmr_flip_step", B, I, ptr(z), z.stride(0), ptr(tab), T, qs - 1, int(i == 0), ptr(dr),
-                      dr.stride(0) if dr is not None else 0, seed, step * 16 + 8 + j, ptr(xt), xt.stride(0),
+                      dr.stride(0) if dr is not None else 0, seed, step * 16 + 8 + j, row0, ptr(xt), xt.stride(0),
                       ptr(probs) if i == 0 else None, probs.stride(0), stream())
         return xt, probs
 
     def training_step(self, den, users, item_embeds, feats, seed, step, norm_rows=None, sched_users=None,
-                      inject=None):
+                      inject=None, row0=0, rank_rows=None):
         """training_losses (:550-606) + the denoiser backward (only the BCE term carries gradient).
         Returns the device loss vector [bce, kl, cl, total] (fp64; the loss of the rows held here,
         normalised by norm_rows).  The BCE backward runs before the p_sample of the InfoNCE term
-        (which reuses the denoiser workspace); the reference's value is unchanged by the order."""
+        (which reuses the denoiser workspace); the reference's value is unchanged by the order.
+        Data parallel: users are rows [row0, row0 + B) of the step whose ranks hold rank_rows rows;
+        every draw is keyed by the global row and the InfoNCE keys are the whole step's rows, so the
+        SUM over ranks of the returned vector and of the gradients is the single-process step's."""
         B = users.numel()
         nr = float(norm_rows or B)
         w = self._work(B)
@@ -673,12 +682,12 @@ class FlipDiffusion:
         if "t" in inj:
             t.copy_(inj["t"])
         else:
-            _lib.call("gmr_diff_sample_t", B, T, seed, step, 0, ptr(t), stream())
+            _lib.call("gmr_diff_sample_t", B, T, seed, step, row0, ptr(t), stream())
         xt, z, dz = w["xt"][:B, :I], w["z"][:B, :I], w["dz"][:B, :I]
         flip = inj.get("flip1")
         _lib.call("gmr_flip_qsample", B, I, ptr(x0), x0.stride(0), ptr(t), 0, ptr(tab), T, self.base_temp, ptr(flip),
-                  flip.stride(0) if flip is not None else 0, seed, step * 16 + 15, ptr(xt), xt.stride(0), stream())
-        den.forward(xt, t_rows=t, T=T, out=z, masks=inj.get("den_masks"), seed=seed, step=step * 16 + 14)
+                  flip.stride(0) if flip is not None else 0, seed, step * 16 + 15, row0, ptr(xt), xt.stride(0), stream())
+        den.forward(xt, t_rows=t, T=T, out=z, masks=inj.get("den_masks"), seed=seed, step=step * 16 + 14, row0=row0)
         _lib.call("gmr_flip_loss_rows", B, I, ptr(x0), x0.stride(0), ptr(z), z.stride(0), ptr(t), ptr(tab), T,
                   1.0 / (nr * I), ptr(dz), dz.stride(0), ptr(w["bce"]), ptr(w["kl"]), stream())
         den.backward(dz)
@@ -687,13 +696,16 @@ class FlipDiffusion:
         _lib.call("gmr_sum_f64", B, ptr(w["kl"]), 1.0 / nr, ptr(loss[1:2]), 0, stream())
         # InfoNCE(x0 (iE * feats), p_sample(x0) (iE * feats)) — value only (:577-582)
         gen, _ = self.p_sample(den, x0, tab, seed, step + 1, inject={"flip": inj.get("ps_flip"),
-                                                                     "draws": inj.get("ps_draws")})
-        cl = self.infonce_value(x0, gen, item_embeds, feats)
+                                                                     "draws": inj.get("ps_draws")}, row0=row0)
+        cl = self.infonce_value(x0, gen, item_embeds, feats, row0, rank_rows)
         out = w["lossv"]
         _lib.call("gmr_flip_total", ptr(loss), ptr(cl), 0.01, ptr(out), stream())
         return out
 
-    def infonce_value(self, x0, gen, item_embeds, feats):
+    def infonce_value(self, x0, gen, item_embeds, feats, row0=0, rank_rows=None):
+        """InfoNCE(x0 (iE * feats), gen (iE * feats)) of the step (:577-582), value only.  Data
+        parallel: this rank's rows are the queries, the keys are all the step's rows (gathered), and
+        the returned value is this rank's share of the step mean (the SUM over ranks is the mean)."""
         B, I = x0.shape
         w = self._w
         fe = w["fe"]
@@ -704,12 +716,27 @@ class FlipDiffusion:
         K.gemm(gen, fe, o[1][:B])
         K.normalize_rows(o[0][:B], w["nv"][0][:B], w["nrm"][0][:B])
         K.normalize_rows(o[1][:B], w["nv"][1][:B], w["nrm"][1][:B])
-        L = w["L"][:B, :B]
-        K.gemm(w["nv"][0][:B], w["nv"][1][:B], L, trans_b=True, alpha=1.0 / self.sparse_temp)
-        _lib.call("gmr_nce_rows_f32", B, ptr(L), L.stride(0), 0.0, ptr(w["rows"]), stream())
         out = w["lossf"][:1]
-        _lib.call("gmr_sum_f32", B, ptr(w["rows"]), 1.0 / B, ptr(out), 0, stream())
+        if rank_rows is None or len(rank_rows) == 1:
+            L = w["L"][:B, :B]
+            K.gemm(w["nv"][0][:B], w["nv"][1][:B], L, trans_b=True, alpha=1.0 / self.sparse_temp)
+            _lib.call("gmr_nce_rows_f32", B, ptr(L), L.stride(0), 0.0, ptr(w["rows"]), stream())
+            _lib.call("gmr_sum_f32", B, ptr(w["rows"]), 1.0 / B, ptr(out), 0, stream())
+            return out
+        keys = dist.gather_step_rows(w["nv"][1][:B], rank_rows)
+        Bg = keys.shape[0]
+        Lbuf = self.__dict__.get("_Ldp")
+        if Lbuf is None or Lbuf.shape[0] < B or Lbuf.shape[1] < (Bg + 3) // 4 * 4:
+            Lbuf = self._Ldp = torch.empty((B, (Bg + 3) // 4 * 4), dtype=torch.float32, device=self.m.device)
+        L = Lbuf[:B, :Bg]
+        K.gemm(w["nv"][0][:B], keys, L, trans_b=True, alpha=1.0 / self.sparse_temp)
+        _lib.call("gmr_nce_rows_off_f32", B, Bg, ptr(L), L.stride(0), int(row0), 0.0, ptr(w["rows"]), stream())
+        _lib.call("gmr_sum_f32", B, ptr(w["rows"]), 1.0 / Bg, ptr(out), 0, stream())
         return out
+
+    def idle_step(self, rank_rows):
+        """A rank holding no rows of a data-parallel step: joins the step's InfoNCE key gather."""
+        dist.gather_step_rows(torch.zeros((0, 64), dtype=torch.float32, device=self.m.device), rank_rows)
 
     # ------------------------------------------------------------------ graph rebuild (trainer.py:736-789)
     @torch.no_grad()

@@ -89,6 +89,7 @@ class Trainer:
         # Off by default: the step is GPU-bound, so replay saves only launch gaps.
         self._use_graphs = os.environ.get("GMR_GRAPHS", "0") == "1" and hasattr(model, "graph_key")
         self._graph = None
+        self.fused_eval = FUSED_EVAL  # per trainer, so a test can run both eval paths in one process
 
     def _build_optimizer(self):
         if (self.learner or "adam").lower() != "adam":
@@ -105,6 +106,8 @@ class Trainer:
         K.zero_(acc)
         W = dist.world()
         slabs = self.model.optim_slabs()
+        if W > 1 and hasattr(self.model, "dp_early_reduce"):
+            self.model.dp_early_reduce = True  # reduce_slab_grads below takes the handle every step
         hook = getattr(self.model, "dp_step_end", None)  # per-global-step model state sync (DiffRec)
         # one optimiser step per train_batch_size batch, as the reference (trainer.py:144-208);
         # under data parallelism every batch is split over the ranks
@@ -305,9 +308,11 @@ class Trainer:
         return self.evaluator.evaluate_device(topk, eval_data, is_test=is_test, idx=idx)
 
     @torch.no_grad()
-    def topk_all(self, eval_data, kmax):
+    def topk_all(self, eval_data, kmax, out_val=None):
         """Top-k indices of every eval user (n_eval x k int32, device); reference trainer.py:369-388.
-        Data parallel: each rank scores a contiguous shard of the eval users; rows are all-gathered."""
+        Data parallel: each rank scores a contiguous shard of the eval users; rows are all-gathered.
+        out_val (n_eval x k fp32, single process only): the scores of the picked items, as the eval
+        kernel computed them (the parity tests' near-tie rule reads them)."""
         d = eval_data.to_device()
         n = eval_data.pr_end
         E = eval_data.step
@@ -317,11 +322,13 @@ class Trainer:
         if out is None or out.shape != (W * size, kmax):
             out = torch.zeros((W * size, kmax), dtype=torch.int32, device=self.device)
             self._topk_buf = out
+        if out_val is not None and (W > 1 or out_val.shape != (n, kmax)):
+            raise ValueError("topk_all: out_val is (n_eval, k) and single-process only")
         m = self.model
         fused = False
         if hasattr(m, "forward_embeddings"):
             usr, itm = m.forward_embeddings()  # identical for every batch of the pass (no_grad)
-            fused = FUSED_EVAL and getattr(m, "fused_eval", True) and usr.shape[1] in (64, 128) and hi_r > lo_r
+            fused = self.fused_eval and getattr(m, "fused_eval", True) and usr.shape[1] in (64, 128) and hi_r > lo_r
             if not fused:
                 sb = getattr(self, "_score_buf", None)
                 if sb is None or sb.shape[0] < min(E, n):
@@ -331,7 +338,7 @@ class Trainer:
         off = dist.rank() * size - lo_r  # row of user lo_r inside the padded gather buffer
         if fused:  # scores -> mask -> top-k in one launch over the whole shard: no E x I buffer
             K.score_topk(usr, itm, d["eval_u32"][lo_r:hi_r], d["mask_ptr_dev"][lo_r:], d["mask_cols_sorted"], kmax,
-                         out[off + lo_r:off + hi_r])
+                         out[off + lo_r:off + hi_r], out_val)
         for lo in range(lo_r, hi_r, E) if not fused else ():
             hi = min(hi_r, lo + E)
             users = d["eval_u32"][lo:hi]
@@ -339,12 +346,13 @@ class Trainer:
             rows = d["mask_rows"][m0:m1] - lo
             cols = d["mask_cols"][m0:m1]
             dst = out[off + lo:off + hi]
+            val = out_val[lo:hi] if out_val is not None else None
             if hasattr(m, "forward_embeddings"):
-                m.topk_from_embeddings(usr, itm, users, rows, cols, kmax, dst, sb)
+                m.topk_from_embeddings(usr, itm, users, rows, cols, kmax, dst, sb, out_val=val)
             else:
                 scores = m.full_sort_predict([users.long()])
                 K.mask_scores(scores, rows, cols)
-                K.topk_rows(scores, kmax, dst)
+                K.topk_rows(scores, kmax, dst, val)
         dist.all_gather_rows_(out, size)
         if W == 1:
             return out
@@ -491,45 +499,53 @@ class GenRecV1Trainer(Trainer):
         _lib.call("gmr_permutation", U, m.seed, 2000 + self._epoch_ctr, ptr(self._perm), stream())
         K.zero_(self._dloss)
         steps = 0
-        for g, lo, hi, blo, bhi, rank_rows, _ in dist.step_slices(U, B, W, r):
+        for g, lo, hi, blo, bhi, rank_rows, row0 in dist.step_slices(U, B, W, r):
             users = self._perm[lo:hi]
-            step = ((self._epoch_ctr * 100000 + g) * W + r) * 4
+            # draws keyed by (global step, global row): any rank count draws the single process's noise
+            step = (self._epoch_ctr * 100000 + g) * 4
             if users.numel() > 0:
                 lv = diff.training_step(den, users, iE, feats_i, m.seed, step, norm_rows=sum(rank_rows),
-                                        sched_users=self._perm[blo:bhi])
+                                        sched_users=self._perm[blo:bhi], row0=row0,
+                                        rank_rows=rank_rows if W > 1 else None)
                 _lib.call("gmr_axpy_dev_f32", 4, ptr(self._one), ptr(lv), ptr(self._dloss), stream())
             else:
                 den.slab.zero_grad()
+                if W > 1:
+                    diff.idle_step(rank_rows)
             if W > 1:
                 dist.all_reduce_(den.slab.grad)
             self.denoise_opt_image.step()
             steps += 1
+        dist.all_reduce_(self._dloss)  # [bce, kl, cl, total] of the whole step (each rank holds its share)
         self._epoch_ctr += 1
         return steps
 
     @torch.no_grad()
     def rebuild(self, chunk=None):
-        """trainer.py:730-789 on the device for users [lo, hi) of this rank; top-k rows all-gathered."""
+        """trainer.py:730-789 on the device, in chunks of train_batch_size users (the schedule, the
+        debias sample and the draws of a chunk depend on the chunk, as the reference's batches do).
+        Data parallel: whole chunks are dealt round-robin over the ranks, so each chunk computes what
+        it computes in one process; the top-k rows are summed over the ranks (each row is written by
+        exactly one rank, the others hold zeros)."""
         m = self.model
         U, I = self.user_num, self.item_num
         kg, kr = m.gen_topk, m.rebuild_k
         B = chunk or self.config["train_batch_size"]
         dev = self.device
-        lo_r, hi_r, size = dist.padded_shard(U)
-        W = dist.world()
-        topk = torch.zeros((W * size, kr), dtype=torch.int32, device=dev)
+        W, r = dist.world(), dist.rank()
+        topk = torch.zeros((U, kr), dtype=torch.int32, device=dev)
         den, diff = m.denoise_model_image, m.diffusion_model
         labels = self.multimodal_interest_space["image_modal"] if self.debias else None
-        base = (self._epoch_ctr * 100000 + dist.rank()) * 1000
-        for j, lo in enumerate(range(lo_r, hi_r, B)):
-            hi = min(hi_r, lo + B)
-            diff.rebuild_rows(den, self._users[lo:hi],
-                              topk[lo - lo_r + dist.rank() * size:hi - lo_r + dist.rank() * size],
-                              labels, self.sample_ratio, m.seed, base + 4 * j)
-        dist.all_gather_rows_(topk, size)
+        base = self._epoch_ctr * 100000 * 1000
+        for j, lo in enumerate(range(0, U, B)):
+            if j % W != r:
+                continue
+            hi = min(U, lo + B)
+            diff.rebuild_rows(den, self._users[lo:hi], topk[lo:hi], labels, self.sample_ratio, m.seed, base + 4 * j)
+        dist.all_reduce_(topk)
         uptr = torch.empty(U + 1, dtype=torch.int32, device=dev)
         uitems = torch.empty(U * kr, dtype=torch.int32, device=dev)
-        K.topk_to_user_csr(topk[:U], uptr, uitems)
+        K.topk_to_user_csr(topk, uptr, uitems)
         g = K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0)
         st = 5000 + self._epoch_ctr                                                      # edgeDropper (:789)
         gd = K.csr_drop_edges(g, m.keep_rate, seed=m.seed, step=st)

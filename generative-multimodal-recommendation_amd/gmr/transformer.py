@@ -137,10 +137,11 @@ class TransformerDenoiser:
         return te, ste, TB, S
 
     # ------------------------------------------------------------------ forward
-    def forward(self, x, t_rows=None, t_const=None, T=5, out=None, masks=None, seed=None, step=0):
+    def forward(self, x, t_rows=None, t_const=None, T=5, out=None, masks=None, seed=None, step=0, row0=0):
         """logits = model(x, t) for x (B x I, fp32, ld % 4 == 0) and per-row t (int32 device tensor) or
-        a constant t.  Train mode draws the dropout masks (Philox seed/step) unless `masks` gives
-        them ({'a','c','1','2','3','f'} -> uint8 (L, B, ...)); returns out (B x I)."""
+        a constant t.  Train mode draws the dropout masks (Philox seed/step, keyed by the global row
+        row0 + r, so a data-parallel rank draws what one process holding the whole batch draws) unless
+        `masks` gives them ({'a','c','1','2','3','f'} -> uint8 (L, B, ...)); returns out (B x I)."""
         B = x.shape[0]
         w = self._work(B)
         D, I, L, H2 = self.D, self.I, self.L, self.H2
@@ -165,14 +166,14 @@ class TransformerDenoiser:
             V, SAin, SA = w["V"][l, :B], w["SAin"][l, :B], w["SA"][l, :B]
             K.gemm(h, wv, V, trans_b=True, epi=K.EPI_BIAS, bias=bv)
             if train_drop:
-                self._drop(V, SAin, "a", l, masks, keep, seed, step, group=D // self.nhead)
+                self._drop(V, SAin, "a", l, masks, keep, seed, step, row0, group=D // self.nhead)
             else:
                 SAin = V
             K.gemm(SAin, self.v(p + "self_attn_out_proj_weight"), SA, trans_b=True, epi=K.EPI_BIAS,
                    bias=self.v(p + "self_attn_out_proj_bias"))
             h1 = w["h1"][l, :B]
             m1 = w["m1"][l]
-            self._ln(h, SA, D, w["mask_1"][l, :B] if train_drop else None, "1", l, masks, keep, seed, step,
+            self._ln(h, SA, D, w["mask_1"][l, :B] if train_drop else None, "1", l, masks, keep, seed, step, row0,
                      self.v(p + "norm1_weight"), self.v(p + "norm1_bias"), h1, w["s1"][l, :B], m1[0, :B], m1[1, :B])
             # cross-attention on the zero memory: out_proj(dropout_head(b_v)) (+ b_o)
             bvc = self.v(p + "multihead_attn_in_proj_bias")[2 * D:]
@@ -182,25 +183,25 @@ class TransformerDenoiser:
             m2 = w["m2"][l]
             if train_drop:
                 Bc, CA = w["Bc"][l, :B], w["CA"][l, :B]
-                self._drop(bvc.view(1, D), Bc, "c", l, masks, keep, seed, step, group=D // self.nhead, ldx=0)
+                self._drop(bvc.view(1, D), Bc, "c", l, masks, keep, seed, step, row0, group=D // self.nhead, ldx=0)
                 K.gemm(Bc, woc, CA, trans_b=True, epi=K.EPI_BIAS, bias=boc)
-                self._ln(h1, CA, D, w["mask_2"][l, :B], "2", l, masks, keep, seed, step, self.v(p + "norm2_weight"),
+                self._ln(h1, CA, D, w["mask_2"][l, :B], "2", l, masks, keep, seed, step, row0, self.v(p + "norm2_weight"),
                          self.v(p + "norm2_bias"), h2, w["s2"][l, :B], m2[0, :B], m2[1, :B])
             else:
                 cav = w["cav"][l:l + 1]
                 K.gemm(bvc.view(1, D), woc, cav, trans_b=True, epi=K.EPI_BIAS, bias=boc)
-                self._ln(h1, cav, 0, None, "2", l, masks, keep, seed, step, self.v(p + "norm2_weight"),
+                self._ln(h1, cav, 0, None, "2", l, masks, keep, seed, step, row0, self.v(p + "norm2_weight"),
                          self.v(p + "norm2_bias"), h2, w["s2"][l, :B], m2[0, :B], m2[1, :B])
             F1, F2 = w["F1"][l, :B], w["F2"][l, :B]
             K.gemm(h2, self.v(p + "linear1_weight"), F1, trans_b=True, epi=K.EPI_BIAS_RELU,
                    bias=self.v(p + "linear1_bias"))
             if train_drop:
-                self._drop(F1, F1, "f", l, masks, keep, seed, step, group=1)
+                self._drop(F1, F1, "f", l, masks, keep, seed, step, row0, group=1)
             K.gemm(F1, self.v(p + "linear2_weight"), F2, trans_b=True, epi=K.EPI_BIAS,
                    bias=self.v(p + "linear2_bias"))
             m3 = w["m3"][l]
             hn = w["h"][l + 1, :B]
-            self._ln(h2, F2, D, w["mask_3"][l, :B] if train_drop else None, "3", l, masks, keep, seed, step,
+            self._ln(h2, F2, D, w["mask_3"][l, :B] if train_drop else None, "3", l, masks, keep, seed, step, row0,
                      self.v(p + "norm3_weight"), self.v(p + "norm3_bias"), hn, w["s3"][l, :B], m3[0, :B], m3[1, :B])
             h = hn
         o1, og = w["o1"][:B], w["og"][:B]
@@ -215,7 +216,7 @@ class TransformerDenoiser:
         self._last = (B, x, t_rows, t_const, train_drop, keep)
         return out
 
-    def _drop(self, x, y, site, l, masks, keep, seed, step, group, ldx=None):
+    def _drop(self, x, y, site, l, masks, keep, seed, step, row0, group, ldx=None):
         w = self._ws
         B = y.shape[0]
         D = self.D
@@ -226,12 +227,12 @@ class TransformerDenoiser:
             mbuf.copy_(mask_in)
         _lib.call("gmr_dropout_f32", B, D, group, ptr(x), K._ld(x) if ldx is None else ldx, keep,
                   ptr(mbuf) if mask_in is not None else None, ptr(mbuf) if mask_in is None else None,
-                  mbuf.stride(0), seed, self._site_step(step, l, site), ptr(y), K._ld(y), stream())
+                  mbuf.stride(0), seed, self._site_step(step, l, site), int(row0), ptr(y), K._ld(y), stream())
 
     def _site_step(self, step, l, site):
         return ((step * 64 + l) * 8 + "ac123f".index(site)) & 0xFFFFFFFFFFFF
 
-    def _ln(self, a, b, ldb, mbuf, site, l, masks, keep, seed, step, wt, bs, y, s, mean, rstd):
+    def _ln(self, a, b, ldb, mbuf, site, l, masks, keep, seed, step, row0, wt, bs, y, s, mean, rstd):
         B = a.shape[0]
         D = self.D
         if mbuf is not None:
@@ -239,7 +240,8 @@ class TransformerDenoiser:
             if given is not None:
                 mbuf.copy_(given[l])
             else:  # draw the residual-branch dropout mask (mask only: the LN kernel applies it)
-                _lib.call("gmr_keep_mask_u8", B * D, keep, seed, self._site_step(step, l, site), ptr(mbuf), stream())
+                _lib.call("gmr_keep_mask_u8", B * D, keep, seed, self._site_step(step, l, site), int(row0) * D, ptr(mbuf),
+                          stream())
         _lib.call("gmr_layernorm_fwd", B, D, ptr(a), K._ld(a), ptr(b), ldb, ptr(mbuf), mbuf.stride(0) if mbuf is not None
                   else 0, 1.0 / keep, ptr(wt), ptr(bs), 1e-5, 0, ptr(y), K._ld(y), ptr(s), D, ptr(mean), ptr(rstd),
                   stream())
@@ -360,7 +362,7 @@ class TransformerDenoiser:
         if mask is None:
             return g
         B = g.shape[0]
-        _lib.call("gmr_dropout_f32", B, self.D, group, ptr(g), K._ld(g), keep, ptr(mask), None, mask.stride(0), 0, 0,
+        _lib.call("gmr_dropout_f32", B, self.D, group, ptr(g), K._ld(g), keep, ptr(mask), None, mask.stride(0), 0, 0, 0,
                   ptr(out), K._ld(out), stream())
         return out
 

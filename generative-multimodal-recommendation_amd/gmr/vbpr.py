@@ -159,14 +159,14 @@ class VBPR(GeneralRecommender):
         return ui[:self.n_users], ui[self.n_users:]
 
     @torch.no_grad()
-    def topk_from_embeddings(self, usr, itm, users_i32, mask_rows, mask_cols, k, out_idx, scores_buf):
+    def topk_from_embeddings(self, usr, itm, users_i32, mask_rows, mask_cols, k, out_idx, scores_buf, out_val=None):
         E = users_i32.numel()
         ub = scores_buf.new_empty((E, self.D))
         K.gather_rows(usr, users_i32, ub)
         sc = scores_buf[:E, :self.n_items]
         K.gemm(ub, itm, sc, trans_b=True)
         K.mask_scores(sc, mask_rows, mask_cols)
-        K.topk_rows(sc, k, out_idx)
+        K.topk_rows(sc, k, out_idx, out_val)
         return out_idx
 
     @torch.no_grad()

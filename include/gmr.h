@@ -465,7 +465,8 @@ int gmr_bpr_logsigmoid_f32(int32_t B, int64_t U, const float* C, const int32_t* 
 /* y += alpha[0] x (device scalar); out = a * b (flat); Bernoulli(p_keep) keep bytes (nn.Dropout masks) */
 int gmr_axpy_dev_f32(int64_t n, const float* alpha, const float* x, float* y, void* stream);
 int gmr_mul_f32(int64_t n, const float* a, const float* b, float* out, void* stream);
-int gmr_keep_mask_u8(int64_t n, float p_keep, uint64_t seed, uint64_t step, uint8_t* out, void* stream);
+/* keep byte i uses Philox counter ctr0 + i (a data-parallel rank's rows: ctr0 = first global row x row length) */
+int gmr_keep_mask_u8(int64_t n, float p_keep, uint64_t seed, uint64_t step, uint64_t ctr0, uint8_t* out, void* stream);
 
 /* ---------------------------------------------------------------- GenRecV1 graphs (§8a G2, G6)
  * CSR transpose (columns ascending in every output row, values carried); workspace 2*n_cols ints,
@@ -518,15 +519,17 @@ int gmr_kmeans_centroids(int32_t k, int32_t d, const float* sums, int64_t lds, c
  * pos_weight | sparsity] from the batch users' history sizes (get_cum, :480-498). */
 int gmr_flip_schedule(int32_t B, const int32_t* users, const int32_t* user_ptr, int32_t I, int32_t T, float* tables,
                       void* stream);
-/* q_sample (:512-526): x_t = x0 xor Bernoulli(sigmoid((a_t - u) temp)); flip (0/1 bytes) replaces the draws */
+/* q_sample (:512-526): x_t = x0 xor Bernoulli(sigmoid((a_t - u) temp)); flip (0/1 bytes) replaces the draws.
+ * Draws are keyed by (step, global row row0 + b, item), so a data-parallel rank holding rows
+ * [row0, row0 + B) of a batch draws what one process holding the whole batch draws. */
 int gmr_flip_qsample(int32_t B, int32_t I, const float* x0, int64_t ld0, const int32_t* t, int32_t t_const,
                      const float* tables, int32_t T, float temp, const uint8_t* flip, int64_t ld_flip, uint64_t seed,
-                     uint64_t step, float* xt, int64_t ldt, void* stream);
-/* one p_sample step on the model logits (:536-548); probs may be NULL */
+                     uint64_t step, int64_t row0, float* xt, int64_t ldt, void* stream);
+/* one p_sample step on the model logits (:536-548); probs may be NULL; draws keyed as gmr_flip_qsample */
 int gmr_flip_step(int32_t B, int32_t I, const float* z, int64_t ldz, const float* tables, int32_t T, int32_t qi,
                   int32_t last,
-                  const uint8_t* draws, int64_t ldd, uint64_t seed, uint64_t step, float* x, int64_t ldx, float* probs,
-                  int64_t ldp, void* stream);
+                  const uint8_t* draws, int64_t ldd, uint64_t seed, uint64_t step, int64_t row0, float* x, int64_t ldx,
+                  float* probs, int64_t ldp, void* stream);
 /* BCE(pos_weight) + curriculum KL rows (:550-627); dz = grad_scale * dBCE/dz (may alias z) */
 int gmr_flip_loss_rows(int32_t B, int32_t I, const float* x0, int64_t ld0, const float* z, int64_t ldz,
                        const int32_t* t, const float* tables, int32_t T, float grad_scale, float* dz, int64_t lddz,
@@ -555,8 +558,8 @@ int gmr_adaln_bwd(int64_t rows, int32_t D, const float* h0, int64_t ld0, const f
 /* dropout with keep probability p_keep, one draw per (row, column / group) (group = head size for
  * the attention-weight dropout of a length-1 sequence); mask_in replays a mask, mask_out records it */
 int gmr_dropout_f32(int64_t rows, int32_t D, int32_t group, const float* x, int64_t ldx, float p_keep,
-                    const uint8_t* mask_in, uint8_t* mask_out, int64_t ldm, uint64_t seed, uint64_t step, float* y,
-                    int64_t ldy, void* stream);
+                    const uint8_t* mask_in, uint8_t* mask_out, int64_t ldm, uint64_t seed, uint64_t step, int64_t row0,
+                    float* y, int64_t ldy, void* stream);
 /* sinusoidal time embedding table T x E (:692-696); SiLU (dy == NULL) or its backward */
 int gmr_time_embedding(int32_t T, int32_t E, float* out, void* stream);
 int gmr_silu_f32(int64_t n, const float* x, const float* dy, float* y, void* stream);

@@ -8,9 +8,11 @@ Checked through the HIP path:
          reference's after init_seed(999) (models/diffmm.py:42-79: the CPU RNG order) - bit-exact;
   * D13/D17 p_sample (steps 0, no noise) of both denoisers over all users + top-1: the reference's
          top-1 item for every user except inside near-tie groups of the reference's own values;
-  * D9/D19 full_sort_predict + mask + top-50 on the valid split: equal to the reference BY POSITION
-         except where our two candidates' scores tie within 1e-6 relative (fp32 summation order);
-         scores of the reference's top-50 within fp32 tolerance for the stored user sample;
+  * D9/D19 Trainer.topk_all (score -> mask -> top-50) on the valid and test splits, through BOTH eval
+         paths (the fused gmr_score_topk_f32 kernel, the product default, and GMR_EVAL_FUSED=0's GEMM +
+         mask + radix top-k): equal to the reference BY POSITION except where our two candidates'
+         scores, as that path computed them, tie within 1e-6 relative (fp32 summation order); scores
+         of the reference's top-50 within fp32 tolerance for the stored user sample;
   * D21  Recall/NDCG/Precision/MAP@{5,10,20,50} (unrounded) within 1e-4 of the reference;
   * (f)2 the test split with is_test=True: every extra of the reference (Pop/Niche, Cold/Warm,
          Coverage/Gini/Tail%) within its 4-decimal rounding.
@@ -123,7 +125,8 @@ def ref_graphs(baby):
 
 
 def _eval_with_scores(m, ld, kmax=50, keep_scores=None):
-    """trainer.topk_all's loop (score -> mask -> top-k on the device), keeping score rows for ties."""
+    """The unfused eval (GMR_EVAL_FUSED=0: score GEMM -> mask -> radix top-k, trainer.topk_all's
+    fallback loop), keeping the score rows for the near-tie rule."""
     d = ld.to_device()
     n, E = ld.pr_end, ld.step
     usr, itm = m.forward_embeddings()
@@ -139,47 +142,120 @@ def _eval_with_scores(m, ld, kmax=50, keep_scores=None):
     return out, (np.concatenate(rows_kept) if keep_scores else None)
 
 
-def test_valid_topk_by_position_and_scores(baby, ref_graphs):
-    m, g = baby["model"], baby["g"]
-    out, scores = _eval_with_scores(m, baby["vl"], keep_scores=True)
-    ours = out.cpu().numpy().astype(np.int64)
-    ref = g["valid_top50"].astype(np.int64)
+EVAL_PATHS = ("fused", "unfused")
+
+
+def trainer_topk(trainer, ld, path, kmax=50):
+    """Trainer.topk_all (common/trainer.py:369-388) on one eval path -> (top-k, their scores as that path
+    computed them).  'fused' is the product default (gmr_score_topk_f32); 'unfused' is GMR_EVAL_FUSED=0."""
+    val = torch.empty((ld.pr_end, kmax), dtype=torch.float32, device=DEV)
+    keep = trainer.fused_eval
+    trainer.fused_eval = path == "fused"
+    try:
+        out = trainer.topk_all(ld, kmax, out_val=val).clone()
+    finally:
+        trainer.fused_eval = keep
+    return out, val.cpu().numpy()
+
+
+def fused_pair_scores(usr, itm, user, items):
+    """The fused eval kernel's own fp32 scores of (user, item) for the given items.  Each output of its
+    MFMA tile accumulates k in a fixed order that does not depend on the tile an item sits in, so a
+    launch over a sub-table of these items gives the values the full launch computed (checked against
+    the full launch's own outputs in check_topk_vs_reference)."""
+    from gmr import kernels as K
+    items = np.asarray(items, np.int64)
+    out = np.empty(len(items), np.float32)
+    u = torch.tensor([int(user)], dtype=torch.int32, device=DEV)
+    mp = torch.zeros(2, dtype=torch.int64, device=DEV)
+    mc = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for a in range(0, len(items), 64):
+        sub = items[a:a + 64]
+        it = itm[torch.as_tensor(sub, device=DEV)].contiguous()
+        idx = torch.empty((1, len(sub)), dtype=torch.int32, device=DEV)
+        val = torch.empty((1, len(sub)), dtype=torch.float32, device=DEV)
+        K.score_topk(usr, it, u, mp, mc, len(sub), idx, val)
+        out[a + idx.cpu().numpy()[0]] = val.cpu().numpy()[0]
+    return out
+
+
+def check_topk_vs_reference(m, trainer, ld, ref, val_sample, path):
+    """D19 parity on one eval path: the top-50 equals the reference's BY POSITION except where the two
+    candidates' scores, as that path computed them, tie within 1e-6 relative; the reference's picks of
+    the stored user sample score within fp32 tolerance of the reference's values.  Returns the top-k."""
+    ours_t, val = trainer_topk(trainer, ld, path)
+    ours = ours_t.cpu().numpy().astype(np.int64)
     assert ours.shape == ref.shape
-    # scores of the reference's picks (first SAMPLE users) agree to fp32 tolerance
-    S = g["valid_top50_val_sample"].shape[0]
-    mine = np.take_along_axis(scores[:S], ref[:S], 1)
-    np.testing.assert_allclose(mine, g["valid_top50_val_sample"], rtol=1e-5, atol=1e-6)
-    # position-wise equality except inside near-tie groups of our own scores
+    usr, itm = m.forward_embeddings()
+    U64, I64 = usr.double().cpu().numpy(), itm.double().cpu().numpy()
+    users = ld.to_device()["eval_u32"].cpu().numpy().astype(np.int64)
+    S = val_sample.shape[0]
+    ref_s = np.einsum("sd,skd->sk", U64[users[:S]], I64[ref[:S]])
+    np.testing.assert_allclose(ref_s, val_sample, rtol=1e-5, atol=1e-6)
+    # the path's own scores of its picks: fp32 values of our embeddings, non-increasing along the row
+    own = np.einsum("nd,nkd->nk", U64[users], I64[ours])
+    np.testing.assert_allclose(val, own, rtol=1e-5, atol=1e-6)
+    assert (np.diff(val, axis=1) <= 0).all()
     r, c = np.nonzero(ours != ref)
-    s_o = scores[r, ours[r, c]]
-    s_r = scores[r, ref[r, c]]
+    if path == "unfused":
+        again, scores = _eval_with_scores(m, ld, keep_scores=True)
+        np.testing.assert_array_equal(again.cpu().numpy(), ours)  # the trainer's fallback loop, same kernels
+        s_o, s_r = scores[r, ours[r, c]], scores[r, ref[r, c]]
+        np.testing.assert_array_equal(s_o, val[r, c])  # same kernels, same values
+    else:
+        s_o, s_r = val[r, c], np.empty(len(r), np.float32)
+        for row in np.unique(r):
+            sel = np.nonzero(r == row)[0]
+            items = np.unique(np.concatenate([ours[row, c[sel]], ref[row, c[sel]]]))
+            sc = dict(zip(items.tolist(), fused_pair_scores(usr, itm, users[row], items)))
+            np.testing.assert_array_equal([sc[i] for i in ours[row, c[sel]]], val[row, c[sel]])
+            s_r[sel] = [sc[i] for i in ref[row, c[sel]]]
     tie = np.abs(s_o - s_r) <= 1e-6 * np.maximum(np.abs(s_o), 1e-3)
-    assert tie.all(), (f"{int((~tie).sum())} top-50 positions differ outside near ties "
+    assert tie.all(), (f"{path}: {int((~tie).sum())} top-50 positions differ outside near ties "
                        f"(first rows {np.unique(r[~tie])[:5]}); {len(r)} differing positions in all")
-    baby["valid_topk"] = out
+    return ours_t
 
 
-def test_valid_metrics_unrounded(baby, ref_graphs):
-    tr, vl = baby["trainer"], baby["vl"]
-    out = baby.get("valid_topk")
-    if out is None:
-        out, _ = _eval_with_scores(baby["model"], vl)
-    sums = tr.evaluator.device_sums(out, vl).cpu().numpy().reshape(4, 8)
+def check_metrics_vs_reference(trainer, ld, out, meta_split):
+    sums = trainer.evaluator.device_sums(out, ld).cpu().numpy().reshape(4, 8)
     n = out.shape[0]
-    raw = baby["meta"]["valid"]["raw"]
+    raw = meta_split["raw"]
     for j, name in enumerate(["recall", "ndcg", "precision", "map"]):
         for q, k in enumerate([5, 10, 20, 50]):
             assert abs(sums[j, q] / n - raw[name][k - 1]) <= 1e-4, (name, k, sums[j, q] / n, raw[name][k - 1])
-    res = tr.evaluator.evaluate_device(out, vl)
-    want = baby["meta"]["valid"]["rounded"]
-    for k, v in want.items():
+    res = trainer.evaluator.evaluate_device(out, ld)
+    for k, v in meta_split["rounded"].items():
         assert abs(res[k] - v) <= 1.01e-4, (k, res[k], v)
 
 
-def test_test_split_extras(baby, ref_graphs):
+@pytest.mark.parametrize("path", EVAL_PATHS)
+def test_valid_topk_by_position_and_scores(baby, ref_graphs, path):
+    g = baby["g"]
+    out = check_topk_vs_reference(baby["model"], baby["trainer"], baby["vl"], g["valid_top50"].astype(np.int64),
+                                  g["valid_top50_val_sample"], path)
+    baby["valid_topk_" + path] = out
+
+
+@pytest.mark.parametrize("path", EVAL_PATHS)
+def test_valid_metrics_unrounded(baby, ref_graphs, path):
+    out = baby.get("valid_topk_" + path)
+    if out is None:
+        out, _ = trainer_topk(baby["trainer"], baby["vl"], path)
+    check_metrics_vs_reference(baby["trainer"], baby["vl"], out, baby["meta"]["valid"])
+
+
+@pytest.mark.parametrize("path", EVAL_PATHS)
+def test_test_split_topk_by_position(baby, ref_graphs, path):
+    g = baby["g"]
+    check_topk_vs_reference(baby["model"], baby["trainer"], baby["tel"], g["test_top50"].astype(np.int64),
+                            g["test_top50_val_sample"], path)
+
+
+@pytest.mark.parametrize("path", EVAL_PATHS)
+def test_test_split_extras(baby, ref_graphs, path):
     """is_test=True: pop/niche, cold/warm, coverage/gini/tail of the reference (topk_evaluator.py:122-270)."""
     tr, tel = baby["trainer"], baby["tel"]
-    out, _ = _eval_with_scores(baby["model"], tel)
+    out, _ = trainer_topk(tr, tel, path)
     res = tr.evaluator.evaluate_device(out, tel, is_test=True)
     want = baby["meta"]["test"]["rounded"]
     missing = sorted(set(want) - set(res))

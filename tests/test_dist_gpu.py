@@ -52,6 +52,7 @@ def _case():
     # --- one rec step (the text denoiser keeps its seeded init: same CPU RNG state in every process)
     torch.manual_seed(999)
     m = build_model(g)
+    m.dp_early_reduce = True  # E0's all-reduce from inside rec_step, as under the Trainer
     u, p, n = t("bpr_users"), t("bpr_pos"), t("bpr_neg")
     B = u.numel()
     a, b = dist.shard(B)
@@ -120,7 +121,7 @@ def test_dp2_step_equals_single_process():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for pr in procs:
         pr.start()
-    dp = q.get(timeout=200)
+    dp = q.get(timeout=380)
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
@@ -194,7 +195,7 @@ def test_dp2_local_batches_equal_double_batch_single_process():
     procs = [ctx.Process(target=_worker_local, args=(r, 2, port, q, 40)) for r in range(2)]
     for pr in procs:
         pr.start()
-    dp = q.get(timeout=200)
+    dp = q.get(timeout=380)
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
@@ -252,7 +253,7 @@ def test_dp2_local_batches_diffrec():
     procs = [ctx.Process(target=_worker_diffrec_local, args=(r, 2, port, q, 16)) for r in range(2)]
     for pr in procs:
         pr.start()
-    dp = q.get(timeout=200)
+    dp = q.get(timeout=380)
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
@@ -300,6 +301,60 @@ def _case_genrec():
     ep_loss, _ = tr._train_epoch(tl, 0)
     out["epoch_loss"] = np.array([ep_loss])
     out["params"] = model2.rec_slab.data.cpu().numpy().copy()
+    out.update(_case_genrec_diffusion())
+    return out
+
+
+def _case_genrec_diffusion():
+    """GenRecV1's diffusion phase and graph rebuild under the current world size (tiny synthetic
+    shape, 600 users): one global diffusion step (its [bce, kl, cl, total] and denoiser gradient
+    after the all-reduce), the whole diffusion phase (losses; denoiser after the Adam steps), and the
+    rebuilt image UI graph of a fresh model (CSR).  Draws are keyed by the global row and the rebuild
+    deals whole 256-user chunks over the ranks, so all of it is the single process's."""
+    from gmr import dist
+    from gmr.configurator import Config
+    from gmr.dataloader import TrainDataLoader
+    from gmr.genrecv1 import GenRecV1
+    from gmr.synthetic import make_dataset
+    from gmr.trainer import GenRecV1Trainer
+    from gmr.utils import init_seed
+
+    def fresh():
+        cfg = Config("GenRecV1", "tiktok", {"synthetic": "tiny", "train_batch_size": 256, "eval_batch_size": 256,
+                                             "epochs": 1, "save_recommended_topk": False, "num_layers": 2})
+        init_seed(999)
+        ds = make_dataset(cfg, "tiny", seed=0)
+        tr, _, _ = ds.split()
+        tl = TrainDataLoader(cfg, tr, batch_size=256, shuffle=True)
+        model = GenRecV1(cfg, tl)
+        return model, GenRecV1Trainer(cfg, model)
+
+    out = {}
+    # one global step on users 0..255 (this rank's share), loss vector + gradient summed over ranks
+    model, trainer = fresh()
+    model.train()
+    den, diff = model.denoise_model_image, model.diffusion_model
+    users = torch.arange(256, dtype=torch.int32, device="cuda")
+    a, b = dist.shard(256)
+    iE = model.rec_slab.view("E0")[model.n_users:]
+    feats = model.getImageFeats()
+    lv = diff.training_step(den, users[a:b], iE, feats, model.seed, 4, norm_rows=256, sched_users=users, row0=a,
+                            rank_rows=dist.shard_sizes(256) if dist.is_dist() else None).double()
+    dist.all_reduce_(lv)
+    dist.all_reduce_(den.slab.grad)
+    out["diff_step_loss"] = lv.cpu().numpy()
+    out["diff_step_grad"] = den.slab.grad.cpu().numpy().copy()
+    # the whole phase: 3 global steps (256 + 256 + 88 users; the last one uneven over the ranks)
+    model, trainer = fresh()
+    trainer.diffusion_phase(0)
+    out["diff_phase_loss"] = trainer._dloss.cpu().numpy().copy()
+    out["diff_phase_params"] = model.denoise_model_image.slab.data.cpu().numpy().copy()
+    # the rebuild of a fresh model: chunks 0, 2 on rank 0 and chunk 1 on rank 1 at two ranks
+    model, trainer = fresh()
+    trainer.rebuild()
+    g = model.image_UI_matrix
+    out["rebuild_rowptr"], out["rebuild_col"], out["rebuild_val"] = (x.cpu().numpy().copy()
+                                                                     for x in (g.rowptr, g.col, g.val))
     return out
 
 
@@ -319,12 +374,14 @@ def _worker_genrec(rank, world, port, q):
         tdist.destroy_process_group()
 
 
-@pytest.mark.timeout(240)
+@pytest.mark.timeout(420)
 def test_dp2_genrecv1_global_batch_infonce():
     """GenRecV1 data parallel (VERDICT r2 missing #3): with the global batch split over two ranks, each
     rank's queries meet ALL of the step's keys in the four in-batch InfoNCE terms
     (models/genrecv1.py:389-414), so the summed loss and the all-reduced gradient are the single
-    process's (the reference's objective) and a Trainer BPR epoch lands on the same parameters."""
+    process's (the reference's objective) and a Trainer BPR epoch lands on the same parameters.
+    The diffusion phase and the rebuild (common/trainer.py:689-789, models/genrecv1.py:550-606) are the
+    single process's as well (VERDICT r3 missing #5)."""
     import torch.multiprocessing as mp
     single = _case_genrec()
     ctx = mp.get_context("spawn")
@@ -333,7 +390,7 @@ def test_dp2_genrecv1_global_batch_infonce():
     procs = [ctx.Process(target=_worker_genrec, args=(r, 2, port, q)) for r in range(2)]
     for pr in procs:
         pr.start()
-    dp = q.get(timeout=200)
+    dp = q.get(timeout=380)
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
@@ -347,3 +404,13 @@ def test_dp2_genrecv1_global_batch_infonce():
     close = np.isclose(dp["params"], single["params"], rtol=1e-3, atol=2e-5)
     assert close.mean() >= 0.99, close.mean()
     np.testing.assert_allclose(dp["params"], single["params"], rtol=1e-3, atol=2e-3)
+    # diffusion phase (VERDICT r3 missing #5): draws keyed by the global row, InfoNCE keys = the step
+    np.testing.assert_allclose(dp["diff_step_loss"], single["diff_step_loss"], rtol=1e-5, atol=1e-7)
+    sc = float(np.abs(single["diff_step_grad"]).max())
+    np.testing.assert_allclose(dp["diff_step_grad"], single["diff_step_grad"], rtol=1e-4, atol=2e-6 * sc)
+    np.testing.assert_allclose(dp["diff_phase_loss"], single["diff_phase_loss"], rtol=1e-5, atol=1e-7)
+    close = np.isclose(dp["diff_phase_params"], single["diff_phase_params"], rtol=1e-3, atol=2e-5)
+    assert close.mean() >= 0.99, close.mean()
+    # rebuild: each chunk computes exactly what it computes in one process
+    for k in ("rebuild_rowptr", "rebuild_col", "rebuild_val"):
+        np.testing.assert_array_equal(dp[k], single[k], err_msg=k)

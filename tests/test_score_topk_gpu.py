@@ -120,7 +120,7 @@ def test_zero_rows_is_a_no_op():
 
 def test_float_embeddings_vs_unfused_path():
     """Real-valued embeddings: the fused result equals the unfused GEMM + mask + radix top-k wherever
-    the fp64 scores are not within 1e-5 (relative) of a tie."""
+    the fp64 scores are not within 1e-6 (relative) of a tie, and >= 99.9 % of the rows are identical."""
     from gmr import kernels as K
     rng = np.random.default_rng(11)
     n_users, n_items, k, n_rows = 2000, 7050, 50, 1500
@@ -144,14 +144,16 @@ def test_float_embeddings_vs_unfused_path():
     for r in range(n_rows):
         s64[r, rows[r]] = -1e10
     same = (got == ref).all(axis=1)
-    for r in np.nonzero(~same)[0]:  # any difference must be a near tie in fp64
+    for r in np.nonzero(~same)[0]:  # any difference must be a near tie in fp64 (1e-6 relative)
         a, b = s64[r, got[r]], s64[r, ref[r]]
-        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6, err_msg=f"row {r}")
-        assert np.abs(np.sort(a) - np.sort(b)).max() < 1e-5
-    assert same.mean() > 0.95
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-9, err_msg=f"row {r}")
+        assert np.abs(np.sort(a) - np.sort(b)).max() <= 1e-6 * np.abs(a).max()
+    n_diff = int((~same).sum())
+    print(f"fused vs unfused: {n_diff} of {n_rows} rows differ (all fp64 near ties)")
+    assert n_diff <= max(1, n_rows // 1000), n_diff  # >= 99.9 % of the rows identical
     # and every row is sorted by fp64 score up to the same tolerance
     g64 = np.take_along_axis(s64, got.astype(np.int64), 1)
-    assert (np.diff(g64, axis=1) <= 1e-6).all()
+    assert (np.diff(g64, axis=1) <= 1e-6 * np.abs(g64[:, :1])).all()
 
 
 def test_bad_arguments_raise():

@@ -7,7 +7,8 @@ common/trainer.py:369-388, 529-576, utils/topk_evaluator.py:77-120).
 The same bar as the baby-shape tests (test_baby_gpu.py), through the HIP path:
   * D2   parameter initialisation: SHA-256 of every rec and denoiser parameter equals the reference's;
   * D13/D17 p_sample top-1 of both denoisers over all 35,598 users (near-tie rule);
-  * D9/D19 valid-split top-50 BY POSITION (near-tie rule) and the reference's top-50 scores;
+  * D9/D19 Trainer.topk_all on the valid split through both eval paths (fused default, GMR_EVAL_FUSED=0):
+         top-50 BY POSITION (near-tie rule on the path's own scores) and the reference's top-50 scores;
   * D21  Recall/NDCG/Precision/MAP@{5,10,20,50} unrounded within 1e-4 (north-star bar);
   * (e)  the data-parallel BPR global step at this shape: two HIP-path ranks (gloo, one GPU) each
          holding half of a 2,048-row batch give the single process's loss and rec gradient.
@@ -21,7 +22,7 @@ import numpy as np
 import pytest
 import torch
 
-from test_baby_gpu import _eval_with_scores, _near_tie_ok, _sha
+from test_baby_gpu import EVAL_PATHS, _near_tie_ok, _sha, check_metrics_vs_reference, check_topk_vs_reference
 
 pytestmark = pytest.mark.gpu
 
@@ -112,32 +113,13 @@ def _ref_graphs(m, g):
         setattr(m, mod + "_UI_matrix", K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0))
 
 
-def test_sports_valid_topk_by_position_and_metrics(sports):
+@pytest.mark.parametrize("path", EVAL_PATHS)
+def test_sports_valid_topk_by_position_and_metrics(sports, path):
+    """Trainer.topk_all on both eval paths (fused default / GMR_EVAL_FUSED=0) vs the reference."""
     m, g, tr, vl = sports["model"], sports["g"], sports["trainer"], sports["vl"]
     _ref_graphs(m, g)
-    out, scores = _eval_with_scores(m, vl, keep_scores=True)
-    ours = out.cpu().numpy().astype(np.int64)
-    ref = g["valid_top50"].astype(np.int64)
-    assert ours.shape == ref.shape
-    S = g["valid_top50_val_sample"].shape[0]
-    mine = np.take_along_axis(scores[:S], ref[:S], 1)
-    np.testing.assert_allclose(mine, g["valid_top50_val_sample"], rtol=1e-5, atol=1e-6)
-    r, c = np.nonzero(ours != ref)
-    s_o = scores[r, ours[r, c]]
-    s_r = scores[r, ref[r, c]]
-    tie = np.abs(s_o - s_r) <= 1e-6 * np.maximum(np.abs(s_o), 1e-3)
-    assert tie.all(), (f"{int((~tie).sum())} top-50 positions differ outside near ties "
-                       f"(first rows {np.unique(r[~tie])[:5]}); {len(r)} differing positions in all")
-    del scores
-    sums = tr.evaluator.device_sums(out, vl).cpu().numpy().reshape(4, 8)
-    n = out.shape[0]
-    raw = sports["meta"]["valid"]["raw"]
-    for j, name in enumerate(["recall", "ndcg", "precision", "map"]):
-        for q, k in enumerate([5, 10, 20, 50]):
-            assert abs(sums[j, q] / n - raw[name][k - 1]) <= 1e-4, (name, k, sums[j, q] / n, raw[name][k - 1])
-    res = tr.evaluator.evaluate_device(out, vl)
-    for k, v in sports["meta"]["valid"]["rounded"].items():
-        assert abs(res[k] - v) <= 1.01e-4, (k, res[k], v)
+    out = check_topk_vs_reference(m, tr, vl, g["valid_top50"].astype(np.int64), g["valid_top50_val_sample"], path)
+    check_metrics_vs_reference(tr, vl, out, sports["meta"]["valid"])
 
 
 # ---------------------------------------------------------------------------- data parallel at this shape
