@@ -414,7 +414,126 @@ def gen_rebuild(ref, tmp):
     return out
 
 
+def main_tiktok():
+    """Config 5 eval fixture at the TikTok shape (9,319 users x 6,710 items, image 128-d, text 768-d:
+    gmr/synthetic.py 'tiktok', seed 0, N(0, 1) features), written as the reference's on-disk dataset
+    and read back by its own RecDataset / TrainDataLoader / EvalDataLoader.  The reference ships no
+    tiktok.yaml, so the data sits under the dataset name 'baby' (baby.yaml only names the id fields and
+    files; the GenRecV1.yaml model keys are the same either way).
+
+    Pinned (tests/test_genrec_tiktok_gpu.py):
+      models/genrecv1.py:16-125      seed-999 init (quick_start.py:171-176): SHA-256 of every rec parameter
+      common/trainer.py:673-687      the kNN item-item graphs (knn_k = 10): neighbour lists + values
+      common/trainer.py:464-485      buildUIMatrix of a fixed rebuild_k = 10 item list per user (injected)
+      models/genrecv1.py:330-353     forward in eval mode (BN running statistics = the init's): content
+                                     rows of a user / item sample
+      models/genrecv1.py:415-427     full_sort_predict -> common/trainer.py:379-386 mask -> top-50 (valid)
+      utils/topk_evaluator.py        unrounded Recall / NDCG / Precision / MAP @ {5, 10, 20, 50}
+    Writes tests/golden/genrecv1_tiktok.npz + genrecv1_tiktok_meta.json.  About a minute on 8 cores."""
+    import hashlib
+    import shutil
+    ref = _import_reference()
+    import torch
+    import utils.configurator as configurator
+    import utils.dataset as rdataset
+    import utils.dataloader as rdataloader
+    import utils.topk_evaluator as rtopk
+    import utils.utils as rutils
+    ROOT = os.path.dirname(os.path.dirname(HERE))
+    sys.path.insert(0, os.path.join(ROOT, "generative-multimodal-recommendation_amd"))
+    from gmr.synthetic import SHAPES, make_features, make_interactions as mk_inter
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    digest = lambda a: hashlib.sha256(np.ascontiguousarray(np.asarray(a, np.float32)).tobytes()).hexdigest()  # noqa
+    tmp = os.path.join(ROOT, ".golden_tmp")
+    if os.path.isdir(tmp):
+        shutil.rmtree(tmp)
+    U, I, n, dv, dt = SHAPES["tiktok"]
+    u, i, lb = mk_inter(U, I, n, 0)
+    v, t = make_features(I, dv, dt, 0, gaussian=True)
+    d = os.path.join(tmp, "baby")
+    os.makedirs(d)
+    with open(os.path.join(d, "baby.inter"), "w") as f:
+        f.write("userID\titemID\tx_label\trating\n")
+        for a, b, c in zip(u.tolist(), i.tolist(), lb.tolist()):
+            f.write(f"{a}\t{b}\t{c}\t5\n")
+    np.save(os.path.join(d, "image_feat.npy"), v)
+    np.save(os.path.join(d, "text_feat.npy"), t)
+    cwd = os.getcwd()
+    os.chdir(REF_SRC)
+    try:
+        cfg = configurator.Config("GenRecV1", "baby", {"use_gpu": False, "data_path": tmp + "/", "epochs": 1,
+                                                       "save_recommended_topk": False})
+    finally:
+        os.chdir(cwd)
+    ds = rdataset.RecDataset(cfg)
+    tr, va, te = ds.split()
+    for part in (tr, va, te):
+        str(part)
+    tl = rdataloader.TrainDataLoader(cfg, tr, batch_size=cfg["train_batch_size"], shuffle=True)
+    vl = rdataloader.EvalDataLoader(cfg, va, additional_dataset=tr, batch_size=cfg["eval_batch_size"])
+    rutils.init_seed(999)
+    tl.pretrain_setup()
+    model = ref["genrecv1"].GenRecV1(cfg, tl)
+    assert (model.n_users, model.n_items) == (U, I)
+    meta = {"U": U, "I": I, "n_train": len(tr), "torch": torch.__version__, "numpy": np.__version__,
+            "generator": "tests/golden/make_golden_genrec.py tiktok", "reference": REF_SRC,
+            "param_sha256": {nm: digest(p.detach().numpy()) for nm, p in model.named_parameters()
+                             if not nm.startswith("denoise_model")}}
+    out = {}
+    # kNN item-item graphs through the trainer's own builder (trainer.py:673-687)
+    trn = object.__new__(ref["trainer"].GenRecV1Trainer)
+    trn.config, trn.model, trn.device = cfg, model, torch.device("cpu")
+    trn.user_num, trn.item_num = U, I
+    trn._build_item_item_matrix()
+    for key, g in (("img", model.image_II_matrix), ("txt", model.text_II_matrix)):
+        idx, val = coo_of(g)
+        assert (np.bincount(idx[0], minlength=I) == 10).all()  # knn_k entries per row, row-major
+        out[f"ii_{key}_cols"] = idx[1].reshape(I, 10).astype(np.int16)
+        out[f"ii_{key}_vals"] = val.reshape(I, 10)
+    # injected rebuilt image UI graph: 10 distinct items per user (trainer.py:464-485, no edge drop)
+    rng = np.random.default_rng(31)
+    k10 = np.stack([rng.choice(I, size=10, replace=False) for _ in range(U)])
+    out["ui_k10_items"] = k10.astype(np.int16)
+    model.image_UI_matrix = trn.buildUIMatrix(np.repeat(np.arange(U), 10), k10.reshape(-1), np.ones(10 * U))
+    model.eval()
+    with torch.no_grad():
+        content, side = model.forward(model.R, model.norm_adj, model.image_UI_matrix, model.image_II_matrix,
+                                      model.text_II_matrix)
+    smp = np.concatenate([np.arange(0, U, 37), U + np.arange(0, I, 29)])
+    out["content_rows"], out["content_sample"] = smp, content.numpy()[smp]
+    out["side_sample"] = side.numpy()[smp]
+    ev = rtopk.TopKEvaluator(cfg)
+    kmax = max(cfg["topk"])
+    mats, vals = [], []
+    with torch.no_grad():
+        for batch in vl:
+            scores = model.full_sort_predict(batch)
+            m = batch[1]
+            scores[m[0], m[1]] = -1e10
+            vv, ix = torch.topk(scores, kmax, dim=-1)
+            mats.append(ix)
+            vals.append(vv)
+    topk = torch.cat(mats).numpy()
+    out["valid_top50"] = topk.astype(np.int16)
+    out["valid_top50_val_sample"] = torch.cat(vals)[:2048].numpy().astype(np.float32)
+    res = ev.evaluate([torch.as_tensor(topk)], vl, is_test=False)
+    pos = vl.get_eval_items()
+    bool_rec = np.asarray([[x in p for x in row] for p, row in zip(pos, topk)])
+    raw = ev._calculate_metrics(vl.get_eval_len_list(), bool_rec)
+    meta["valid"] = {"n_users": int(len(topk)), "rounded": res,
+                     "raw": {mname: np.asarray(raw[j], np.float64).tolist()
+                             for j, mname in enumerate(["recall", "ndcg", "precision", "map"])},
+                     "eval_users_head": np.asarray(vl.get_eval_users())[:16].tolist()}
+    np.savez_compressed(os.path.join(OUT, "genrecv1_tiktok.npz"), **out)
+    with open(os.path.join(OUT, "genrecv1_tiktok_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1, default=float)
+    shutil.rmtree(tmp)
+    print("wrote", os.path.join(OUT, "genrecv1_tiktok.npz"), meta["valid"]["rounded"])
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "tiktok":
+        return main_tiktok()
     ref = _import_reference()
     import torch
     import sklearn
