@@ -236,6 +236,24 @@ int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t
                  const float* rowvec1, const float* rowvec2, float slope, int32_t tile, int32_t split_k,
                  float* workspace, int64_t workspace_floats, void* stream);
 
+/* Pre-split operands (csrc/gemm_p3.hip; the graph rebuild's p_sample products, models/diffmm.py:352-358,
+ * 408-451, common/trainer.py:529-546).  A plane set is three bf16 matrices (uint16 storage) [3][rows][ld]
+ * with plane stride ps: x = hi + mid + lo exactly for every fp32 x (the split of GMR_GEMM_X6); ld is a
+ * multiple of 32 and the columns [cols, ld) are zero.  gmr_split3_planes writes one from an fp32 matrix.
+ * gmr_gemm_p3_f32: C[M,N] = epilogue(alpha * A B^T) with A (M x Kp) and B (N x Kp) given as plane sets
+ * (Kp = their padded k, a multiple of 32, 16-byte aligned planes, ld % 8 == 0), six bf16 MFMA products
+ * per 32x32x16 block (fp32-accurate, as GMR_GEMM_X6); output as fp32 C (ldc % 4 == 0, 16-byte aligned)
+ * and / or as a plane set C_planes (ldcp % 4 == 0: a later product's operand).  Epilogues NONE, BIAS,
+ * BIAS_TANH, POSTERIOR (c1 = slope, c2 = beta; aux as fp32 or as planes aux_planes — in place over
+ * C_planes is allowed).  tile: 0 = by shape, 1 = 256 x 128, 2 = 128^2 double-buffered, 3 = 128^2. */
+int gmr_split3_planes(int64_t rows, int64_t cols, const float* src, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
+                      int64_t plane_stride, void* stream);
+int gmr_gemm_p3_f32(int64_t M, int64_t N, int64_t Kp, float alpha, const uint16_t* A, int64_t lda, int64_t psa,
+                    const uint16_t* B, int64_t ldb, int64_t psb, float* C, int64_t ldc, uint16_t* C_planes,
+                    int64_t ldcp, int64_t pscp, int32_t epilogue, const float* bias, const float* aux, int64_t ld_aux,
+                    const uint16_t* aux_planes, int64_t ld_auxp, int64_t ps_auxp, float slope, float beta,
+                    int32_t tile, void* stream);
+
 /* ---------------------------------------------------------------- DiffMM rec step (diffmm.py:129-258)
  * Fused row kernels of forward_MM / forward_cl_MM / calculate_loss and their backward
  * (layouts in csrc/diffmm.hip). */
