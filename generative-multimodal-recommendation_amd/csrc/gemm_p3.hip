@@ -366,8 +366,10 @@ extern "C" int gmr_gemm_p3_f32(int64_t M, int64_t N, int64_t Kp, float alpha, co
   const __bf16* b = reinterpret_cast<const __bf16*>(B);
   const hipStream_t st = (hipStream_t)stream;
   int t = tile > 0 ? tile : p3_tile_env();
-  const int64_t tiles256 = ((M + 255) / 256) * ((N + 127) / 128);
-  if (t <= 0) t = tiles256 >= 512 ? 1 : 3;  // by shape: 256 x 128 once the grid fills two waves of CUs
+  // by shape (scripts/micro/p3_micro.hip at the rebuild products, profiles/r04c_p3_micro.txt): 256 x 128 for
+  // wide products (19445 x 7050 x 1000: 1.53 ms vs 1.79 / 1.69 on the 128^2 tiles), three single-buffered
+  // 128^2 blocks per CU for narrow ones (19445 x 1000 x 7050: 1.63 ms vs 1.71 on 256 x 128)
+  if (t <= 0) t = (N > 1024 && ((M + 255) / 256) * ((N + 127) / 128) >= 512) ? 1 : 3;
   const int tn = (int)((N + 127) / 128);
   const int group = tn >= 32 ? 8 : 0;  // gemm.hip tile_group: G tile rows per column on wide products
   if (t == 1) p3_launch<256, 128, 4, 2, 2, 1>(st, M, N, Kp, a, lda, psa, b, ldb, psb, e, o, group);

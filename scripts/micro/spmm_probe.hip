@@ -76,8 +76,13 @@ struct Args {
 __global__ void v0_empty(Args a) {}
 
 // MODE 1 = entries only, 2 = + gathers; CH chunks per pass; W16: one 16-B entry load per lane
-template <int MODE, int CH, bool W16>
+// SM (store mode, MODE 2): 0 one float4 per chunk; 1 a store at every simulated row end (every 6th entry,
+// offset per lane group: divergent across the wave's groups, like the side kernel's short rows);
+// 2 the same row ends uniform across the wave; 3 as 1 with non-temporal stores; 4 as 1 staged in LDS,
+// flushed once per chunk (one store per staged row, all groups together)
+template <int MODE, int CH, bool W16, int SM = 0>
 __global__ void __launch_bounds__(256) v_chunks(Args a) {
+  __shared__ float4 stage[4][8][4][8];  // [wave][group][slot][lane]
   const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
   const int lane = threadIdx.x & 63, grp = lane >> 3, sub = lane & 7;
   const int side = xcd >> 2, slice = xcd & 3;
@@ -128,14 +133,40 @@ __global__ void __launch_bounds__(256) v_chunks(Args a) {
           if (i < end - beg) xs[h][u] = *reinterpret_cast<const float4*>(Xs + (int64_t)c * a.ldx);
         }
 #pragma unroll
-      for (int h = 0; h < CH; ++h)
+      for (int h = 0; h < CH; ++h) {
+        int nst = 0;
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
           const int src = W16 ? (u >> 1) : (u & 7);
           const int which = W16 ? (u & 1) : (u >> 3);
           const float v = __int_as_float(__shfl(e[h][which].y, grp * 8 + src));
           acc[h] = f4_fma(v, xs[h][u], acc[h]);
+          if (SM != 0 && c0 + h < nch) {
+            const bool end = SM == 2 ? (u % 6 == 5) : ((u + 3 * grp) % 6 == 5);
+            if (end) {
+              float* o = a.out + (((int64_t)(side * 4 + slice) * nch + c0 + h) * 16 + u) * 32 + sub * 4;
+              if (SM == 4) {
+                stage[threadIdx.x >> 6][grp][nst & 3][sub] = acc[h];
+                ++nst;
+              } else if (SM == 3) {
+                typedef float f32x4v __attribute__((ext_vector_type(4)));
+                f32x4v ov = {acc[h].x, acc[h].y, acc[h].z, acc[h].w};
+                __builtin_nontemporal_store(ov, reinterpret_cast<f32x4v*>(o));
+              } else {
+                *reinterpret_cast<float4*>(o) = acc[h];
+              }
+              acc[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+          }
         }
+        if (SM == 4 && c0 + h < nch) {  // flush: slot j of every group in one store instruction
+          for (int j = 0; j < 3; ++j)
+            if (j < nst) {
+              float* o = a.out + (((int64_t)(side * 4 + slice) * nch + c0 + h) * 16 + j) * 32 + sub * 4;
+              *reinterpret_cast<float4*>(o) = stage[threadIdx.x >> 6][grp][j][sub];
+            }
+        }
+      }
     }
 #pragma unroll
     for (int h = 0; h < CH; ++h)
@@ -158,7 +189,7 @@ int main(int argc, char** argv) {
   const int64_t ldx = 128;
   CK(hipMalloc(&d_ent, ent.size() * 8 + 64));
   CK(hipMalloc(&d_X, (int64_t)n * ldx * 4));
-  CK(hipMalloc(&d_out, (int64_t)(g.nnz / 16 + 64) * 8 * 32 * 4));
+  CK(hipMalloc(&d_out, (int64_t)(g.nnz / 16 + 64) * 8 * 32 * 4 * 16));
   CK(hipMemcpy(d_ent, ent.data(), ent.size() * 8, hipMemcpyHostToDevice));
   std::vector<float> hX((int64_t)n * ldx);
   std::mt19937 rng(3);
@@ -205,6 +236,14 @@ int main(int argc, char** argv) {
     time(nm, [&] { hipLaunchKernelGGL((v_chunks<2, 2, false>), grid, blk, 0, 0, a); });
     snprintf(nm, 64, "V4 gathers CH1 w16  wpx %3d", wpx);
     time(nm, [&] { hipLaunchKernelGGL((v_chunks<2, 1, true>), grid, blk, 0, 0, a); });
+    snprintf(nm, 64, "V5 + rowend st div  wpx %3d", wpx);
+    time(nm, [&] { hipLaunchKernelGGL((v_chunks<2, 1, false, 1>), grid, blk, 0, 0, a); });
+    snprintf(nm, 64, "V6 + rowend st uni  wpx %3d", wpx);
+    time(nm, [&] { hipLaunchKernelGGL((v_chunks<2, 1, false, 2>), grid, blk, 0, 0, a); });
+    snprintf(nm, 64, "V7 + rowend NT div  wpx %3d", wpx);
+    time(nm, [&] { hipLaunchKernelGGL((v_chunks<2, 1, false, 3>), grid, blk, 0, 0, a); });
+    snprintf(nm, 64, "V8 + rowend LDS+fl  wpx %3d", wpx);
+    time(nm, [&] { hipLaunchKernelGGL((v_chunks<2, 1, false, 4>), grid, blk, 0, 0, a); });
   }
   return 0;
 }
