@@ -49,7 +49,10 @@ constexpr int kSideThreads = 256;
 constexpr int64_t kSideCounterWords = 8;  // counters per hub (one per 32-column slice, d <= 256)
 
 enum { H_MAGIC, H_NROWS, H_SPLIT, H_T, H_TASK, H_NT0, H_NT1, H_EMPTY, H_NE0, H_NE1, H_HUB, H_NHUB, H_SLOT, H_NSLOT,
-       H_PACKED, H_NNZ, H_WAVE, H_NW0, H_NW1, H_TW };
+       H_PACKED, H_NNZ, H_WAVE, H_NW0, H_NW1, H_TW,
+       // degree-class plan (Tw flag GMR_SIDE_CLASSES): short rows grouped by degree
+       H_DC, H_CLS, H_PERM, H_DSTO, H_NSR, H_PACKB, H_NSE };
+constexpr int kSideDcMax = 16;  // short rows of the degree-class plan: degree 1 .. 16 (one 16-entry round)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -153,49 +156,79 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
     {
       const int n_wv = P * wpx * NWV, wv = (part_i * wpx + k) * NWV + wid;
       const int w0 = side == 0 ? 0 : hdr[H_NW0], nwk = side == 0 ? hdr[H_NW0] : hdr[H_NW1];
-#pragma unroll 1
-      for (int wi = wv; wi < nwk; wi += n_wv) {
-        const int4 tk = wtasks[w0 + wi];
+      // the next task's descriptor is loaded at the top of a task and its first entries during the
+      // task's last gather round: one memory round trip per task instead of three
+      int wi = wv;
+      int4 tk = wi < nwk ? wtasks[w0 + wi] : make_int4(0, 0, 0, -1);
+      int b, end;
+      {
         const int pl = (tk.y - tk.x + 7) >> 3;
-        const int b = tk.x + grp * pl, end = min(tk.y, b + pl);
-        float4 acc = f4_zero();
-        int2 rec[EPL];
+        b = tk.x + grp * pl;
+        end = min(tk.y, b + pl);
+      }
+      int2 rec[EPL];
 #pragma unroll
-        for (int q = 0; q < EPL; ++q) {
-          const int i = b + q * 8 + sub;
-          rec[q] = i < end ? packed[i] : make_int2(0, 0);
-        }
+      for (int q = 0; q < EPL; ++q) {
+        const int i = b + q * 8 + sub;
+        rec[q] = i < end ? packed[i] : make_int2(0, 0);
+      }
 #pragma unroll 1
-        for (int e = b; e < end; e += EB) {
+      for (; wi < nwk; wi += n_wv) {
+        const int wn = wi + n_wv;
+        const int4 tkn = wn < nwk ? wtasks[w0 + wn] : make_int4(0, 0, 0, -1);
+        float4 acc = f4_zero();
+        const int bt = b, et = end;
+#pragma unroll 1
+        for (int e = bt; e < et; e += EB) {
           float4 xs[EB];
           int2 cur[EPL];  // this round's entries: their values are shuffled out again at the FMAs
 #pragma unroll
           for (int u = 0; u < EB; ++u) {
             const int c = grp_bcast(rec[u / 8].x, u % 8) & 0x7fffffff;
             xs[u] = f4_zero();
-            if (e + u < end) xs[u] = gather(c);
+            if (e + u < et) xs[u] = gather(c);
+          }
+          int nb = e + EB, nend = et;
+          if (e + EB >= et) {  // last round of this task: the next task's first entries
+            const int pl = (tkn.y - tkn.x + 7) >> 3;
+            nb = tkn.x + grp * pl;
+            nend = min(tkn.y, nb + pl);
+            b = nb;
+            end = nend;
           }
 #pragma unroll
           for (int q = 0; q < EPL; ++q) {
             cur[q] = rec[q];
-            const int i = e + EB + q * 8 + sub;
-            rec[q] = i < end ? packed[i] : make_int2(0, 0);
+            const int i = nb + q * 8 + sub;
+            rec[q] = i < nend ? packed[i] : make_int2(0, 0);
           }
 #pragma unroll
           for (int u = 0; u < EB; ++u)
-            if (e + u < end) acc = gmr::f4_fma(__int_as_float(grp_bcast(cur[u / 8].y, u % 8)), xs[u], acc);
+            if (e + u < et) acc = gmr::f4_fma(__int_as_float(grp_bcast(cur[u / 8].y, u % 8)), xs[u], acc);
+        }
+        if (bt >= et) {  // this group had no entries (a short block): still move on to the next task
+          const int pl = (tkn.y - tkn.x + 7) >> 3;
+          b = tkn.x + grp * pl;
+          end = min(tkn.y, b + pl);
+#pragma unroll
+          for (int q = 0; q < EPL; ++q) {
+            const int i = b + q * 8 + sub;
+            rec[q] = i < end ? packed[i] : make_int2(0, 0);
+          }
         }
         acc = wave_groups_sum(acc);
-        if (tk.w < 0) {
-          if (grp == 0) store(tk.z, acc);
+        const int4 tkc = tk;
+        tk = tkn;
+        if (tkc.w < 0) {
+          if (grp == 0) store(tkc.z, acc);
           continue;
         }
         if (grp == 0) {
           f32x4 pv = {acc.x, acc.y, acc.z, acc.w};
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pv), prs, (tk.w * 256 + c0) * 4, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pv), prs, (tkc.w * 256 + c0) * 4, 0, 16);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int h = slotmap[tk.w];
+        const int h = slotmap[tkc.w];
         const int4 hb = hubs[h];
         int* cnt = counters + (int64_t)h * kSideCounterWords + slice;
         int old = 0;
@@ -213,6 +246,89 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
           if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
+    }
+    if (hdr[H_DC]) {
+      // ---- short rows by degree class (plan GMR_SIDE_CLASSES): a wave job is 8 lane-group tasks of one
+      // degree d, each k = 16 / d whole rows (k d <= 16 entries, one gather round), rows of the class in
+      // row order.  d is uniform across the wave, so the row ends fall on the same entry slots in every
+      // group: k full-width stores per job instead of one masked store per slot, and slots past k d are
+      // skipped outright.  The next job's entries and row ids are in flight while this one gathers.
+      const int4* __restrict__ cls = reinterpret_cast<const int4*>(plan + hdr[H_CLS]) + side * (kSideDcMax + 1);
+      const int* __restrict__ perm = plan + hdr[H_PERM];
+      const int2* __restrict__ pB = reinterpret_cast<const int2*>(plan + hdr[H_PACKB]);
+      const int n_wv = P * wpx * NWV;
+      const int wv = n_wv - 1 - ((part_i * wpx + k) * NWV + __builtin_amdgcn_readfirstlane(wid));
+      {  // Y = beta Y on empty rows (lane groups, as the task plan)
+        const int n_lg = P * wpx * (kSideThreads / 8);
+        const int lg = n_lg - 1 - ((part_i * wpx + k) * (kSideThreads / 8) + wid * 8 + grp);
+        const int e0 = side == 0 ? 0 : hdr[H_NE0], ne = side == 0 ? hdr[H_NE0] : hdr[H_NE1];
+        for (int i = lg; i < ne; i += n_lg) store(empty[e0 + i], f4_zero());
+      }
+      // the side's class records, one per lane (lanes 0 .. 16): a job's class is found by one ballot over
+      // them (a serial scan of scalar loads cost a memory round trip per class)
+      const int4 cl_l = lane <= kSideDcMax ? cls[lane] : make_int4(INT32_MAX, 0, 0, 0);
+      const int nj = __builtin_amdgcn_readlane(cl_l.x, kSideDcMax);  // total jobs (the terminator's first job)
+      struct Job {
+        int d, k, nrow, ne;
+        int2 e0, e1;
+        int pr0, pr1;
+      };
+      auto load_job = [&](int job) {
+        Job J;
+        J.d = 0, J.k = 0, J.nrow = 0, J.ne = 0;
+        J.e0 = J.e1 = make_int2(0, 0);
+        J.pr0 = J.pr1 = 0;
+        if (job >= nj) return J;
+        // class = the number of classes 1 .. 15 whose first job is <= job (class 0 starts at job 0)
+        const unsigned long long bl = __ballot(lane >= 1 && lane < kSideDcMax && cl_l.x <= job);
+        const int ci = __popcll(bl);
+        const int4 c = make_int4(__builtin_amdgcn_readlane(cl_l.x, ci), __builtin_amdgcn_readlane(cl_l.y, ci),
+                                 __builtin_amdgcn_readlane(cl_l.z, ci),
+                                 __builtin_amdgcn_readlane(cl_l.w, ci));  // {first job, perm row, packedB entry, rows}
+        J.d = ci + 1;
+        J.k = kSideDcMax / J.d;
+        const int r0 = (job - c.x) * 8 * J.k + grp * J.k;  // this group's first row of the class
+        J.nrow = max(0, min(J.k, c.w - r0));
+        J.ne = J.nrow * J.d;
+        const int eb = c.z + r0 * J.d;
+        if (sub < J.ne) J.e0 = pB[eb + sub];
+        if (8 + sub < J.ne) J.e1 = pB[eb + 8 + sub];
+        if (sub < J.nrow) J.pr0 = perm[c.y + r0 + sub];
+        if (8 + sub < J.nrow) J.pr1 = perm[c.y + r0 + 8 + sub];
+        return J;
+      };
+      Job J = load_job(wv);
+#pragma unroll 1
+      for (int job = wv; job < nj; job += n_wv) {
+        const int kd = J.k * J.d;  // uniform: entry slots of this job
+        float4 xs[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          xs[u] = f4_zero();
+          if (u < kd) {
+            const int c = grp_bcast(u < 8 ? J.e0.x : J.e1.x, u % 8);
+            if (u < J.ne) xs[u] = gather(c);
+          }
+        }
+        const Job C = J;
+        J = load_job(job + n_wv);  // next job's entries and rows travel while these gathers land
+        float4 acc = f4_zero();
+        int j = 0, nxt = C.d - 1;  // uniform: row counter, slot of the next row end
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          if (u < kd) {
+            acc = gmr::f4_fma(__int_as_float(grp_bcast(u < 8 ? C.e0.y : C.e1.y, u % 8)), xs[u], acc);
+            if (u == nxt) {
+              const int row = __shfl(j < 8 ? C.pr0 : C.pr1, gbase + (j & 7));
+              if (j < C.nrow) store(row, acc);
+              acc = f4_zero();
+              ++j;
+              nxt += C.d;
+            }
+          }
+        }
+      }
+      continue;
     }
     // ---- short rows: lane-group tasks of <= T entries (whole rows), the next task's descriptor and
     // first entries in flight while the current one gathers
@@ -293,13 +409,39 @@ __global__ void __launch_bounds__(256) side_last_kernel(const int* __restrict__ 
 struct SidePlanHost {
   std::vector<int4> tasks[2], waves[2], hubs;
   std::vector<int> empty[2], slotmap;
+  bool dc = false;                 // degree-class plan: short rows in classes, not tasks
+  std::vector<int4> cls;           // per side kSideDcMax + 1 {first job, first perm row, first packedB entry, rows}
+  std::vector<int> perm, dsto;     // short rows (side, degree, row order) and their packedB offsets
+  int64_t short_entries = 0;
 };
 
 // rows of degree <= T: lane-group tasks of <= T entries (whole rows, cut at empty rows); longer rows:
 // wave tasks of <= 8 TW entries (blocks), a row of several blocks gets a hub record and slots
-void side_plan_host(const int32_t* rp, int64_t n_rows, int64_t split, int T, int TW, SidePlanHost& p) {
+void side_plan_host(const int32_t* rp, int64_t n_rows, int64_t split, int T, int TW, SidePlanHost& p, bool dc = false) {
   int slot = 0;
+  p.dc = dc;
+  if (dc) T = kSideDcMax;
   for (int s = 0; s < 2; ++s) {
+    if (dc) {  // classes: rows of degree d (1..16) in row order; a job = 8 tasks of k = 16 / d rows
+      const int64_t r0 = s == 0 ? 0 : split, r1 = s == 0 ? split : n_rows;
+      std::vector<int> by[kSideDcMax + 1];
+      for (int64_t r = r0; r < r1; ++r) {
+        const int d = rp[r + 1] - rp[r];
+        if (d >= 1 && d <= kSideDcMax) by[d].push_back((int)r);
+      }
+      int job = 0;
+      for (int d = 1; d <= kSideDcMax; ++d) {
+        const int k = kSideDcMax / d, n = (int)by[d].size();
+        p.cls.push_back(make_int4(job, (int)p.perm.size(), (int)p.short_entries, n));
+        for (int r : by[d]) {
+          p.perm.push_back(r);
+          p.dsto.push_back((int)p.short_entries);
+          p.short_entries += d;
+        }
+        job += (n + 8 * k - 1) / (8 * k);
+      }
+      p.cls.push_back(make_int4(job, (int)p.perm.size(), (int)p.short_entries, 0));  // terminator
+    }
     const int64_t r0 = s == 0 ? 0 : split, r1 = s == 0 ? split : n_rows;
     int beg = -1, row0 = -1, cnt = 0, end = 0;
     auto flush = [&]() {
@@ -326,6 +468,8 @@ void side_plan_host(const int32_t* rp, int64_t n_rows, int64_t split, int T, int
           p.slotmap.push_back(h);
         }
         slot += blocks;
+      } else if (dc) {
+        flush();  // degree-class plan: the short row is in its class (above)
       } else {
         if (cnt + deg > T) flush();
         if (beg < 0) {
@@ -345,7 +489,7 @@ void side_plan_host(const int32_t* rp, int64_t n_rows, int64_t split, int T, int
 int64_t r4(int64_t v) { return (v + 3) / 4 * 4; }
 
 struct SideLayout {
-  int64_t task, wave, empty, hub, slot, packed, words;
+  int64_t task, wave, empty, hub, slot, packed, cls, perm, dsto, packb, words;
 };
 SideLayout side_layout(const SidePlanHost& p, int64_t nnz) {
   SideLayout l;
@@ -355,7 +499,11 @@ SideLayout side_layout(const SidePlanHost& p, int64_t nnz) {
   l.hub = r4(l.empty + (int64_t)(p.empty[0].size() + p.empty[1].size()));
   l.slot = l.hub + 4 * (int64_t)p.hubs.size();
   l.packed = r4(l.slot + (int64_t)p.slotmap.size());
-  l.words = l.packed + 2 * nnz;
+  l.cls = r4(l.packed + 2 * nnz);  // int4 records: 16-byte aligned
+  l.perm = l.cls + 4 * (int64_t)p.cls.size();
+  l.dsto = l.perm + (int64_t)p.perm.size();
+  l.packb = r4(l.dsto + (int64_t)p.dsto.size());
+  l.words = l.packb + 2 * p.short_entries;
   return l;
 }
 
@@ -412,12 +560,13 @@ extern "C" int gmr_spmm_side_tune(int32_t wpx, int32_t eb) {
 // 16-23 = TW (entries per lane group of a hub block: blocks of 8 TW; 0 = 32)
 inline int side_T(int32_t Tw) { return Tw & 0xFFFF; }
 inline int side_TW(int32_t Tw) { return (Tw >> 16) & 0xFF ? (Tw >> 16) & 0xFF : 32; }
+inline bool side_DC(int32_t Tw) { return (Tw & GMR_SIDE_CLASSES) != 0; }
 
 extern "C" int64_t gmr_spmm_side_plan_words(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t Tw) {
   const int T = side_T(Tw), TW = side_TW(Tw);
   if (!rowptr_host || n_rows <= 0 || split < 0 || split > n_rows || T < 8 || T > 4096 || TW < 4) return -1;
   SidePlanHost p;
-  side_plan_host(rowptr_host, n_rows, split, T, TW, p);
+  side_plan_host(rowptr_host, n_rows, split, T, TW, p, side_DC(Tw));
   return side_layout(p, rowptr_host[n_rows]).words;
 }
 
@@ -428,7 +577,7 @@ extern "C" int gmr_spmm_side_plan_build(const int32_t* rowptr_host, int64_t n_ro
   GMR_ARG(T >= 8 && T <= 4096 && TW >= 4, "T must be in [8, 4096], TW >= 4");
   GMR_ARG(n_rows < (1 << 30) && rowptr_host[n_rows] < (1ll << 31) - 1, "too large for int32 plans");
   SidePlanHost p;
-  side_plan_host(rowptr_host, n_rows, split, T, TW, p);
+  side_plan_host(rowptr_host, n_rows, split, T, TW, p, side_DC(Tw));
   const int64_t nnz = rowptr_host[n_rows];
   const SideLayout l = side_layout(p, nnz);
   GMR_ARG(words >= l.words, "plan buffer smaller than gmr_spmm_side_plan_words(...)");
@@ -456,6 +605,20 @@ extern "C" int gmr_spmm_side_plan_build(const int32_t* rowptr_host, int64_t n_ro
   h[H_NW1] = (int)p.waves[1].size();
   h[H_TW] = TW;
   for (int i = H_TW + 1; i < kSideHdr; ++i) h[i] = 0;
+  GMR_ARG(l.words < INT32_MAX, "plan too large for int32 offsets");
+  h[H_DC] = p.dc ? 1 : 0;
+  h[H_CLS] = (int)l.cls;
+  h[H_PERM] = (int)l.perm;
+  h[H_DSTO] = (int)l.dsto;
+  h[H_NSR] = (int)p.perm.size();
+  h[H_PACKB] = (int)l.packb;
+  h[H_NSE] = (int)p.short_entries;
+  int4* cl = reinterpret_cast<int4*>(h + l.cls);
+  for (const int4& x : p.cls) *cl++ = x;
+  for (size_t i = 0; i < p.perm.size(); ++i) h[l.perm + i] = p.perm[i];
+  for (size_t i = 0; i < p.dsto.size(); ++i) h[l.dsto + i] = p.dsto[i];
+  for (int64_t i = l.packed + 2 * nnz; i < l.cls; ++i) h[i] = 0;
+  for (int64_t i = l.dsto + (int64_t)p.dsto.size(); i < l.packb; ++i) h[i] = 0;
   int4* t = reinterpret_cast<int4*>(h + l.task);
   for (int s = 0; s < 2; ++s)
     for (const int4& x : p.tasks[s]) *t++ = x;
@@ -488,6 +651,28 @@ extern "C" int gmr_spmm_side_pack(const int32_t* rowptr, const int32_t* col, con
   GMR_LAUNCHED();
   hipLaunchKernelGGL(side_last_kernel, dim3(gmr::grid_for(n_rows, 256, 4096)), dim3(256), 0, (hipStream_t)stream, rowptr,
                      n_rows, packed);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+// packedB: the short rows' (col, val) in class order, one thread per short row (<= 16 entries each)
+__global__ void __launch_bounds__(256) side_pack_classes_kernel(const int* __restrict__ rowptr, const int* __restrict__ col,
+                                                                const float* __restrict__ val, int n_short,
+                                                                const int* __restrict__ perm, const int* __restrict__ dsto,
+                                                                int2* __restrict__ pb) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n_short; q += gridDim.x * blockDim.x) {
+    const int r = perm[q], b = rowptr[r], e = rowptr[r + 1], o = dsto[q];
+    for (int i = b; i < e; ++i) pb[o + i - b] = make_int2(col[i], __float_as_int(val[i]));
+  }
+}
+
+extern "C" int gmr_spmm_side_pack_classes(const int32_t* rowptr, const int32_t* col, const float* val,
+                                          const int32_t* plan_host, int32_t* plan, void* stream) {
+  GMR_ARG(rowptr && col && val && plan_host && plan && plan_host[H_MAGIC] == kSideMagic, "bad args");
+  if (!plan_host[H_DC] || plan_host[H_NSR] == 0) return GMR_OK;
+  hipLaunchKernelGGL(side_pack_classes_kernel, dim3(gmr::grid_for(plan_host[H_NSR], 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, rowptr, col, val, plan_host[H_NSR], plan + plan_host[H_PERM],
+                     plan + plan_host[H_DSTO], reinterpret_cast<int2*>(plan + plan_host[H_PACKB]));
   GMR_LAUNCHED();
   return GMR_OK;
 }

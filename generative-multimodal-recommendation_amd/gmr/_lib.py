@@ -52,6 +52,7 @@ SIGNATURES = {
     "gmr_spmm_side_plan_build": (I32, [P, I64, I64, I32, P, I64]),
     "gmr_spmm_side_scratch_floats": (I64, [P]),
     "gmr_spmm_side_pack": (I32, [P, P, P, I64, I64, I64, P, P]),
+    "gmr_spmm_side_pack_classes": (I32, [P, P, P, P, P, P]),
     "gmr_spmm_side_tune": (I32, [I32, I32]),
     "gmr_spmm_side_f32": (I32, [P, I32, P, P, P, P, I64, F32, F32, P, P, P, I32, P]),
     "gmr_bipartite_nnz": (I64, [I64, I64, I64, I32]),

@@ -319,6 +319,9 @@ SPMM_SIDE = os.environ.get("GMR_SPMM_SIDE", "1") == "1"
 # short-row task entries: 16 for every graph (round-3 sweeps with 8 / 12 / 16 / 32 / 64-entry tasks,
 # profiles/r03o_sweep.txt, r03p_sweep.txt: 16 is best or tied at d <= 128); GMR_SPMM_SIDE_T overrides
 SPMM_SIDE_T = int(os.environ.get("GMR_SPMM_SIDE_T", "0"))
+# degree-class plan for the short rows (GMR_SIDE_CLASSES, include/gmr.h); GMR_SPMM_DC=0: the task plan
+SPMM_SIDE_CLASSES = 1 << 24
+SPMM_DC = os.environ.get("GMR_SPMM_DC", "1") == "1"
 SPMM_SIDE_TW = int(os.environ.get("GMR_SPMM_SIDE_TW", "32"))
 
 
@@ -356,7 +359,7 @@ class CSR:
         if side and SPMM_SIDE and class_split > 0 and self.n_cols == self.n_rows and self.nnz > 0:
             self.build_side_plan(class_split)
 
-    def build_side_plan(self, split, T=None):
+    def build_side_plan(self, split, T=None, classes=None):
         """Side-split plan (gmr_spmm_side_*): built on the host from a host copy of rowptr (one
         device sync per graph build), entries packed on the device; self.partial becomes the plan's
         scratch (zeroed: its hub counters re-arm themselves after every launch)."""
@@ -365,8 +368,10 @@ class CSR:
         if T is None:
             T = SPMM_SIDE_T or 16  # 16-entry tasks: norm_adj d = 64 / 128 -10 % vs 32 (profiles/r03o_sweep.txt)
         T = int(T)
-        if not T >> 16:
+        if not (T >> 16) & 0xFF:
             T |= SPMM_SIDE_TW << 16
+        if (SPMM_DC if classes is None else classes) and T & 0xFFFF == 16:
+            T |= SPMM_SIDE_CLASSES
         rp = np.ascontiguousarray(self.rowptr.cpu().numpy().astype(np.int32))
         rpp = rp.ctypes.data_as(ctypes.c_void_p)
         words = int(lib.gmr_spmm_side_plan_words(rpp, self.n_rows, int(split), int(T)))
@@ -379,6 +384,9 @@ class CSR:
         plan = torch.from_numpy(host).to(dev)
         _lib.call("gmr_spmm_side_pack", ptr(self.rowptr), ptr(self.col), ptr(self.val), self.n_rows, self.nnz,
                   int(host[14]), ptr(plan), stream())
+        _lib.call("gmr_spmm_side_pack_classes", ptr(self.rowptr), ptr(self.col), ptr(self.val),
+                  host.ctypes.data_as(ctypes.c_void_p), ptr(plan), stream())
+        self.side_classes = bool(host[20])
         nsc = int(lib.gmr_spmm_side_scratch_floats(host.ctypes.data_as(ctypes.c_void_p)))
         self.side = (plan, int(split))
         # workgroups per XCD by product width (profiles/r03b_sweep.txt): the short-task UI graphs and

@@ -162,13 +162,20 @@ int gmr_spmm_plan_info(const int32_t* plan, int32_t* host_hdr, void* stream);
  * per-block split sources / outputs (16-byte aligned, strides multiples of 4).  A short row's sum
  * is its entries in CSR order; a hub row adds its pieces in piece order: deterministic. */
 /* T: bits 0-15 = entries per short-row task (rows of degree > T are hub rows), bits 16-23 = entries
- * per lane group of a hub block (blocks of 8 x that; 0 = 32) */
+ * per lane group of a hub block (blocks of 8 x that; 0 = 32); | GMR_SIDE_CLASSES: degree-class plan —
+ * rows of degree 1 .. 16 are grouped by degree (a wave takes 8 tasks of 16 / d whole rows of one degree
+ * d, so every lane group's row ends fall on the same entry slots: full-width row stores), their
+ * (col, val) copied in class order by gmr_spmm_side_pack_classes (after gmr_spmm_side_pack, with the
+ * host plan); rows above 16 entries are hub rows.  Short-row sums keep CSR order from zero. */
+#define GMR_SIDE_CLASSES (1 << 24)
 int64_t gmr_spmm_side_plan_words(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t T);
 int gmr_spmm_side_plan_build(const int32_t* rowptr_host, int64_t n_rows, int64_t split, int32_t T, int32_t* plan_host,
                              int64_t words);
 int64_t gmr_spmm_side_scratch_floats(const int32_t* plan_host);
 int gmr_spmm_side_pack(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                        int64_t packed_off, int32_t* plan, void* stream);
+int gmr_spmm_side_pack_classes(const int32_t* rowptr, const int32_t* col, const float* val, const int32_t* plan_host,
+                               int32_t* plan, void* stream);
 /* launch shape for tuning sweeps: workgroups per XCD and entries in flight per lane group (8 / 16);
  * defaults GMR_SPMM_SIDE_WPX / GMR_SPMM_SIDE_EB (64 / 16) */
 int gmr_spmm_side_tune(int32_t wpx, int32_t eb);

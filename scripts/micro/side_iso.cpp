@@ -31,7 +31,7 @@
   } while (0)
 
 enum { H_MAGIC, H_NROWS, H_SPLIT, H_T, H_TASK, H_NT0, H_NT1, H_EMPTY, H_NE0, H_NE1, H_HUB, H_NHUB, H_SLOT, H_NSLOT,
-       H_PACKED, H_NNZ, H_WAVE, H_NW0, H_NW1, H_TW };
+       H_PACKED, H_NNZ, H_WAVE, H_NW0, H_NW1, H_TW, H_DC, H_CLS };
 
 int main(int argc, char** argv) {
   FILE* f = fopen(argc > 1 ? argv[1] : "graph.bin", "rb");
@@ -67,13 +67,14 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int T : {16, 32, 64}) {
+  for (int T : {16 | GMR_SIDE_CLASSES, 16, 32}) {
     const int32_t Tw = T | (32 << 16);
     const int64_t words = gmr_spmm_side_plan_words(rp.data(), n, split, Tw);
     std::vector<int32_t> plan(words);
     OK(gmr_spmm_side_plan_build(rp.data(), n, split, Tw, plan.data(), words));
     const int64_t sc = gmr_spmm_side_scratch_floats(plan.data());
-    printf("T=%d: tasks %d/%d waves %d/%d hubs %d slots %d empty %d/%d\n", T, plan[H_NT0], plan[H_NT1], plan[H_NW0],
+    printf("T=%d%s: tasks %d/%d waves %d/%d hubs %d slots %d empty %d/%d\n", T & 0xFFFF,
+           (T & GMR_SIDE_CLASSES) ? " classes" : "", plan[H_NT0], plan[H_NT1], plan[H_NW0],
            plan[H_NW1], plan[H_NHUB], plan[H_NSLOT], plan[H_NE0], plan[H_NE1]);
     int32_t* d_plan[5];
     const char* names[5] = {"full", "short tasks only", "hub waves only", "user side only", "item side only"};
@@ -83,9 +84,14 @@ int main(int argc, char** argv) {
       if (v == 2) p[H_NT0] = p[H_NT1] = p[H_NE0] = p[H_NE1] = 0;
       if (v == 3) p[H_NT1] = p[H_NW1] = p[H_NE1] = 0;
       if (v == 4) p[H_NT0] = p[H_NW0] = p[H_NE0] = 0;
+      if (p[H_DC]) {  // class jobs: the side's terminator record holds its job count
+        if (v == 2 || v == 4) p[p[H_CLS] + 4 * 16] = 0;
+        if (v == 2 || v == 3) p[p[H_CLS] + 4 * (17 + 16)] = 0;
+      }
       CK(hipMalloc(&d_plan[v], words * 4));
       CK(hipMemcpy(d_plan[v], p.data(), words * 4, hipMemcpyHostToDevice));
       OK(gmr_spmm_side_pack(d_rp, d_col, d_val, n, nnz, p[H_PACKED], d_plan[v], nullptr));
+      OK(gmr_spmm_side_pack_classes(d_rp, d_col, d_val, p.data(), d_plan[v], nullptr));
     }
     float* d_sc;
     CK(hipMalloc(&d_sc, sc * 4));
@@ -102,7 +108,7 @@ int main(int argc, char** argv) {
         y[b] = d_Y + 64 * b;
         ldl[b] = ldh[b] = ldy[b] = 64 * nb;
       }
-      for (int wpx : {64, 128, 256}) {
+      for (int wpx : {64, 128, 256, 512}) {
         OK(gmr_spmm_side_tune(wpx, 16));
         for (int v = 0; v < 5; ++v) {
           auto launch = [&] {
@@ -117,7 +123,8 @@ int main(int argc, char** argv) {
           CK(hipEventSynchronize(e1));
           float ms;
           CK(hipEventElapsedTime(&ms, e0, e1));
-          printf("  T %2d d %3d wpx %3d %-18s %7.2f us\n", T, 64 * nb, wpx, names[v], 1e3 * ms / reps);
+          printf("  T %2d%s d %3d wpx %3d %-18s %7.2f us\n", T & 0xFFFF, (T & GMR_SIDE_CLASSES) ? " cls" : "    ",
+                 64 * nb, wpx, names[v], 1e3 * ms / reps);
         }
       }
     }

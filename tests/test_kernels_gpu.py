@@ -852,17 +852,21 @@ def _side_graph(self_loops, U=3000, I=500, seed=41):
     return graph_ref.norm_adj_csr(U, I, rows, cols)
 
 
+@pytest.mark.parametrize("classes", [True, False])
 @pytest.mark.parametrize("nb", [1, 2, 4])
 @pytest.mark.parametrize("self_loops", [0, 1])
-def test_spmm_side_vs_fp64_and_lane(K, nb, self_loops):
-    """Side-split plan (csrc/spmm_side.hip): every row within fp32 tolerance of an fp64 product with
-    split sources, alpha / beta; rows of degree <= T (the plan's task size) bit-identical to the lane plan (both sum a
-    short row's entries in CSR order from zero); hub rows (pieces added in order by the last arriving
-    piece) identical across repeated launches (the counters re-arm) and with a second scratch."""
+def test_spmm_side_vs_fp64_and_lane(K, nb, self_loops, classes):
+    """Side-split plan (csrc/spmm_side.hip), degree-class (GMR_SIDE_CLASSES, the default) and task form:
+    every row within fp32 tolerance of an fp64 product with split sources, alpha / beta; rows of degree
+    <= T (16) bit-identical to the lane plan (both sum a short row's entries in CSR order from zero); hub
+    rows (pieces added in order by the last arriving piece) identical across repeated launches (the
+    counters re-arm) and with a second scratch."""
     rp, col, val = _side_graph(self_loops)
     U, I = 3000, 500
     N = U + I
     gs = K.CSR(_dev(rp), _dev(col), _dev(val), class_split=U, side=True)
+    gs.build_side_plan(U, classes=classes)
+    assert gs.side_classes == classes
     gl = K.CSR(_dev(rp), _dev(col), _dev(val), seg_nnz=LANE32)
     assert gs.side is not None and gl.side is None
     deg = np.diff(rp)
