@@ -37,6 +37,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "gmr_common.h"
@@ -52,7 +53,11 @@ enum { H_MAGIC, H_NROWS, H_SPLIT, H_T, H_TASK, H_NT0, H_NT1, H_EMPTY, H_NE0, H_N
        H_PACKED, H_NNZ, H_WAVE, H_NW0, H_NW1, H_TW,
        // degree-class plan (Tw flag GMR_SIDE_CLASSES): short rows grouped by degree
        H_DC, H_CLS, H_PERM, H_DSTO, H_NSR, H_PACKB, H_NSE };
-constexpr int kSideDcMax = 16;  // short rows of the degree-class plan: degree 1 .. 16 (one 16-entry round)
+// rows of the degree-class plan: degree 1 .. 16 (longer rows are hub rows: classes up to 48 with several
+// gather rounds per lane-group row measured slower on the item side, profiles/r04h_spmm_classes_probe.txt)
+constexpr int kSideDcMax = 16;
+constexpr int kSideDcRound = 16; // entries per lane-group gather round; rows of degree <= 16 share one round
+__host__ __device__ constexpr int dc_rows_per_task(int d) { return d <= kSideDcRound ? kSideDcRound / d : 1; }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -249,10 +254,11 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
     }
     if (hdr[H_DC]) {
       // ---- short rows by degree class (plan GMR_SIDE_CLASSES): a wave job is 8 lane-group tasks of one
-      // degree d, each k = 16 / d whole rows (k d <= 16 entries, one gather round), rows of the class in
-      // row order.  d is uniform across the wave, so the row ends fall on the same entry slots in every
-      // group: k full-width stores per job instead of one masked store per slot, and slots past k d are
-      // skipped outright.  The next job's entries and row ids are in flight while this one gathers.
+      // degree d: each task is k = 16 / d whole rows (k d <= 16 entries, one gather round); rows of the class
+      // in row order.  d is uniform across
+      // the wave, so the row ends fall on the same entry slots in every group: k full-width stores per job
+      // instead of one masked store per slot, and slots past k d are skipped outright.  The next round's
+      // (or job's) entries and row ids are in flight while the current gathers land.
       const int4* __restrict__ cls = reinterpret_cast<const int4*>(plan + hdr[H_CLS]) + side * (kSideDcMax + 1);
       const int* __restrict__ perm = plan + hdr[H_PERM];
       const int2* __restrict__ pB = reinterpret_cast<const int2*>(plan + hdr[H_PACKB]);
@@ -269,16 +275,17 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
       const int4 cl_l = lane <= kSideDcMax ? cls[lane] : make_int4(INT32_MAX, 0, 0, 0);
       const int nj = __builtin_amdgcn_readlane(cl_l.x, kSideDcMax);  // total jobs (the terminator's first job)
       struct Job {
-        int d, k, nrow, ne;
+        int d, k, nrow, ne, eb;
         int2 e0, e1;
         int pr0, pr1;
       };
       auto load_job = [&](int job) {
         Job J;
-        J.d = 0, J.k = 0, J.nrow = 0, J.ne = 0;
+        J.d = 0, J.k = 0, J.nrow = 0, J.ne = 0, J.eb = 0;
         J.e0 = J.e1 = make_int2(0, 0);
         J.pr0 = J.pr1 = 0;
-        if (job >= nj) return J;
+        // no early exit past the last job (its loads would sit under a branch): every load is issued, from
+        // clamped indices, and a job >= nj gets no rows
         // class = the number of classes 1 .. 15 whose first job is <= job (class 0 starts at job 0)
         const unsigned long long bl = __ballot(lane >= 1 && lane < kSideDcMax && cl_l.x <= job);
         const int ci = __popcll(bl);
@@ -286,41 +293,66 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
                                  __builtin_amdgcn_readlane(cl_l.z, ci),
                                  __builtin_amdgcn_readlane(cl_l.w, ci));  // {first job, perm row, packedB entry, rows}
         J.d = ci + 1;
-        J.k = kSideDcMax / J.d;
+        J.k = dc_rows_per_task(J.d);
         const int r0 = (job - c.x) * 8 * J.k + grp * J.k;  // this group's first row of the class
-        J.nrow = max(0, min(J.k, c.w - r0));
+        J.nrow = job < nj ? max(0, min(J.k, c.w - r0)) : 0;
         J.ne = J.nrow * J.d;
-        const int eb = c.z + r0 * J.d;
-        if (sub < J.ne) J.e0 = pB[eb + sub];
-        if (8 + sub < J.ne) J.e1 = pB[eb + 8 + sub];
-        if (sub < J.nrow) J.pr0 = perm[c.y + r0 + sub];
-        if (8 + sub < J.nrow) J.pr1 = perm[c.y + r0 + 8 + sub];
+        J.eb = c.z + r0 * J.d;
+        // unconditional loads (clamped index, value selected after): a load under a branch makes the
+        // compiler's vmcnt accounting give up and wait for every outstanding store with vmcnt(0)
+        const int nse = hdr[H_NSE] - 1, nsr = hdr[H_NSR] - 1;
+        const int2 a0 = pB[max(0, min(J.eb + sub, nse))], a1 = pB[max(0, min(J.eb + 8 + sub, nse))];
+        const int q0 = perm[max(0, min(c.y + r0 + sub, nsr))], q1 = perm[max(0, min(c.y + r0 + 8 + sub, nsr))];
+        J.e0 = sub < J.ne ? a0 : make_int2(0, 0);
+        J.e1 = 8 + sub < J.ne ? a1 : make_int2(0, 0);
+        J.pr0 = q0;
+        J.pr1 = q1;
         return J;
       };
+      // the job loop twice, for beta == 0 and beta != 0 (a load of Y under a run-time branch would cost
+      // the counted vmcnt waits of the whole loop)
+      auto run_jobs = [&](auto beta_tag) {
+        constexpr bool BETA = decltype(beta_tag)::value;
+        auto store_row = [&](int row, float4 acc) {
+          float* yp = yc + (int64_t)row * ldy;
+          float4 o = gmr::f4_scale(alpha, acc);
+          if constexpr (BETA) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
+          if (nt) {
+            f32x4 ov = {o.x, o.y, o.z, o.w};
+            __builtin_nontemporal_store(ov, reinterpret_cast<f32x4*>(yp));
+          } else {
+            *reinterpret_cast<float4*>(yp) = o;
+          }
+        };
       Job J = load_job(wv);
 #pragma unroll 1
       for (int job = wv; job < nj; job += n_wv) {
-        const int kd = J.k * J.d;  // uniform: entry slots of this job
+        const Job C = J;
+        // the next job's entries and rows are loaded BEFORE this job's gathers: they travel while the
+        // gathers land, and the wait for them at the next job counts the 16 younger gathers — it never
+        // waits for this job's row stores, which come after them in the in-order vmcnt stream
+        J = load_job(job + n_wv);
+        // all 16 gathers issued unconditionally (an idle slot re-reads row 0 of X, an L2 hit, and is
+        // zeroed), so the FMA of slot u waits with a counted vmcnt
         float4 xs[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-          xs[u] = f4_zero();
-          if (u < kd) {
-            const int c = grp_bcast(u < 8 ? J.e0.x : J.e1.x, u % 8);
-            if (u < J.ne) xs[u] = gather(c);
-          }
+          const int c = grp_bcast(u < 8 ? C.e0.x : C.e1.x, u % 8);
+          xs[u] = gather(u < C.ne ? c : 0);
         }
-        const Job C = J;
-        J = load_job(job + n_wv);  // next job's entries and rows travel while these gathers land
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (u >= C.ne) xs[u] = f4_zero();
         float4 acc = f4_zero();
         int j = 0, nxt = C.d - 1;  // uniform: row counter, slot of the next row end
+        const int kd = C.k * C.d;  // uniform: entry slots of this job's tasks
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
           if (u < kd) {
             acc = gmr::f4_fma(__int_as_float(grp_bcast(u < 8 ? C.e0.y : C.e1.y, u % 8)), xs[u], acc);
             if (u == nxt) {
               const int row = __shfl(j < 8 ? C.pr0 : C.pr1, gbase + (j & 7));
-              if (j < C.nrow) store(row, acc);
+              if (j < C.nrow) store_row(row, acc);
               acc = f4_zero();
               ++j;
               nxt += C.d;
@@ -328,6 +360,9 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
           }
         }
       }
+      };
+      if (beta != 0.f) run_jobs(std::true_type{});
+      else run_jobs(std::false_type{});
       continue;
     }
     // ---- short rows: lane-group tasks of <= T entries (whole rows), the next task's descriptor and
@@ -431,7 +466,7 @@ void side_plan_host(const int32_t* rp, int64_t n_rows, int64_t split, int T, int
       }
       int job = 0;
       for (int d = 1; d <= kSideDcMax; ++d) {
-        const int k = kSideDcMax / d, n = (int)by[d].size();
+        const int k = dc_rows_per_task(d), n = (int)by[d].size();
         p.cls.push_back(make_int4(job, (int)p.perm.size(), (int)p.short_entries, n));
         for (int r : by[d]) {
           p.perm.push_back(r);

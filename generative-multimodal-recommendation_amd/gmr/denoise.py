@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from . import dist
 from . import kernels as K
 from .kernels import ptr, stream
 from .slab import Slab
@@ -148,13 +149,22 @@ class Denoiser(nn.Module):
                slope=c1, beta=c2)
         return x
 
+    def slab_head_words(self):
+        """Gradient words before the [W2 | b2] tail (the part reduced after the whole backward)."""
+        return self.slab.offsets["W2"]
+
     # ------------------------------------------------------------------ backward
-    def backward(self, x_in, h, dout, dpre, t_rows, T, S):
-        """Parameter gradients (written into the slab's grad buffer) from dout = dL/d out."""
+    def backward(self, x_in, h, dout, dpre, t_rows, T, S, early_reduce=False):
+        """Parameter gradients (written into the slab's grad buffer) from dout = dL/d out.
+        early_reduce (data parallel): the [W2 | b2] tail of the gradient slab is final after its two
+        products, so its all-reduce starts there (handle in self.early_handle) and runs beside the
+        dpre / dW1 products; the caller reduces the head [: W2) (slab_head_words())."""
         s = self.slab
         I = self.I
         K.gemm(dout, h, s.gview("W2"), trans_a=True)                      # dW2 = dout^T h
         K.colsum(dout, s.gview("b2"))                                     # db2
+        if early_reduce:
+            self.early_handle = dist.all_reduce_start(s.grad[self.slab_head_words():])
         K.gemm(dout, s.view("W2"), dpre, epi=K.EPI_DTANH, aux=h)          # dpre = (dout W2) * (1 - h^2)
         K.gemm(dpre, x_in, s.gview("W1")[:, :I], trans_a=True)             # dW1[:, :I] = dpre^T x_in
         K.colsum(dpre, S, group=t_rows, n_groups=T)                       # S[t] = sum_{b: t_b = t} dpre[b]

@@ -549,7 +549,7 @@ class DiffMM(GeneralRecommender):
         return self._dw[slot]
 
     def diffusion_step(self, den, batch_users, feats, item_embeds, step, noise=None, keep=None, t=None,
-                       norm_rows=None, slot=0, row0=0):
+                       norm_rows=None, slot=0, row0=0, early_reduce=False):
         """One GaussianDiffusion.training_losses + backward for one denoiser (diffmm.py:453-477).
 
         Writes the denoiser's gradients into its slab; returns (diff_loss, gc_loss) per-row
@@ -583,7 +583,7 @@ class DiffMM(GeneralRecommender):
         _lib.call("gmr_diff_gc_rows", B, ptr(batch_users), ptr(self.user_ptr), ptr(self.user_items),
                   ptr(item_embeds), item_embeds.stride(0), ptr(Z), 64, gsc, ptr(w["Gc"]), 64, ptr(w["gc"]), stream())
         K.gemm(w["Gc"][:B], feats, o, trans_b=True, beta=1.0)                  # dout += G feats^T
-        den.backward(xi, h, o, w["dpre"][:B], tt, T, w["S"])
+        den.backward(xi, h, o, w["dpre"][:B], tt, T, w["S"], early_reduce=early_reduce)
         return w["diff"][:B], w["gc"][:B]
 
     @torch.no_grad()

@@ -370,7 +370,11 @@ class CSR:
         T = int(T)
         if not (T >> 16) & 0xFF:
             T |= SPMM_SIDE_TW << 16
-        if (SPMM_DC if classes is None else classes) and T & 0xFFFF == 16:
+        # the degree-class plan for the graph-conv adjacency (norm_adj, d = 128: 17.5 -> 15.5 us, d = 64 11.3 ->
+        # 11.1, profiles/r04i_spmm_classes_probe.txt); the rebuilt UI graphs (about two entries per row) keep
+        # the task plan (+2..5 % with classes there)
+        short = self.nnz < 4 * self.n_rows
+        if (SPMM_DC and not short if classes is None else classes) and T & 0xFFFF == 16:
             T |= SPMM_SIDE_CLASSES
         rp = np.ascontiguousarray(self.rowptr.cpu().numpy().astype(np.int32))
         rpp = rp.ctypes.data_as(ctypes.c_void_p)

@@ -400,23 +400,29 @@ class DiffMMTrainer(Trainer):
             # the two denoisers are independent until their Adam steps: the text one runs on a side
             # stream (own work buffers, slot 1) beside the image one; under DP the image gradient
             # exchange starts as soon as its step is issued (one bucket per slab)
+            # data parallel: each denoiser's [W2 | b2] gradient tail starts its all-reduce inside the
+            # backward as soon as it is final (beside the dpre / dW1 products), the head after it
             def one(j):
                 den, feats = dens[j]
                 if nb > 0:
-                    diff, gc = m.diffusion_step(den, users, feats, iE, base + j, norm_rows=norm, slot=j, row0=row0)
+                    diff, gc = m.diffusion_step(den, users, feats, iE, base + j, norm_rows=norm, slot=j, row0=row0,
+                                                early_reduce=W > 1)
                     _lib.call("gmr_sum_f64", nb, ptr(diff), 1.0 / norm, ptr(self._dloss[j:j + 1]), 1, stream())
                     _lib.call("gmr_sum_f64", nb, ptr(gc), m.e_loss / norm, ptr(self._dloss[j:j + 1]), 1, stream())
-                else:
+                else:  # an idle rank issues the same two reduces
                     den.slab.zero_grad()
+                    if W > 1:
+                        den.early_handle = dist.all_reduce_start(den.slab.grad[den.slab_head_words():])
+                return (den.early_handle if W > 1 else None,
+                        dist.all_reduce_start(den.slab.grad[:den.slab_head_words()]) if W > 1 else None)
 
             with st.on(1):
-                one(1)
-            one(0)
-            pending = [dist.all_reduce_start(dens[0][0].slab.grad) if W > 1 else None]
+                pend_t = one(1)
+            pend_i = one(0)
             st.join(1)
-            pending.append(dist.all_reduce_start(dens[1][0].slab.grad) if W > 1 else None)
-            for h, opt in zip(pending, opts):
-                dist.wait(h)
+            for hs, opt in zip((pend_i, pend_t), opts):
+                for h in hs:
+                    dist.wait(h)
                 opt.step()
             steps += 1
         dist.all_reduce_(self._dloss)
