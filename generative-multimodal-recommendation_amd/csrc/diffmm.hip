@@ -1171,6 +1171,125 @@ __global__ void __launch_bounds__(256, 2) cl6_kernel(int nf, int ns, const float
   }
 }
 
+// The same pass with the S product of block j + 1 issued before the exp / split phase of block j (PIPE,
+// GMR_CL_PIPE, default): the matrix pipe runs the next S while the vector pipe exponentiates and splits
+// this block's logits, instead of each wave alternating MFMA-only and VALU-only phases.  Both staged
+// blocks are in LDS by then (block j + 2 is staged into block j's buffer after its Y product), so the
+// staging, the chunking and every sum are those of cl6_kernel: bit-identical results.
+template <bool FAST, bool TABLE>
+__global__ void __launch_bounds__(256, 2) cl6p_kernel(int nf, int ns, const float* __restrict__ F, int64_t ldf,
+                                                      const float* __restrict__ Stg, int64_t lds,
+                                                      const float* __restrict__ w, float inv_t, int chunk,
+                                                      float* __restrict__ part_y, float* __restrict__ part_z) {
+  __shared__ __attribute__((aligned(16))) __bf16 s_stg[2 * kC6Stage];
+  __shared__ __attribute__((aligned(16))) float s_f[32 * kClLd];
+  __shared__ float s_w[2][32];
+  const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const int f = blockIdx.x * 128 + (threadIdx.x >> 6) * 32 + l32;  // the lane's fragment row
+  const int c = blockIdx.y, s0 = c * chunk, s1 = min(ns, s0 + chunk);
+  c6bf8 fr[4][3];  // K-step k: d = 16 k + 8 h + 0..7
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float4 a = f4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (f < nf) {
+      a = ld4(F + (int64_t)f * ldf + 16 * k + 8 * h);
+      b = ld4(F + (int64_t)f * ldf + 16 * k + 8 * h + 4);
+    }
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    c6_split8(v, fr[k]);
+  }
+  auto sprod = [&](const __bf16* A) {  // S^T of a staged block
+    clx16 sacc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sacc[e] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c6bf8 a[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const c6bf8*>(A + p * kC6PA + l32 * kC6A + 16 * k + 8 * h);
+      sacc = c6_mfma6(a, fr[k], sacc);
+    }
+    return sacc;
+  };
+  auto stage = [&](int j, int buf) {  // block starting at row j -> s_stg[buf] (and its weights), two barriers
+    float4 st[2];
+    float sw = 0.f;
+    cl_load(st, Stg, lds, j, s1);
+    if (TABLE && threadIdx.x < 32) sw = j + (int)threadIdx.x < s1 ? w[j + threadIdx.x] : 0.f;
+    cl_store(st, s_f);
+    __syncthreads();
+    c6_convert(s_f, s_stg + buf * kC6Stage);
+    if (TABLE && threadIdx.x < 32) s_w[buf][threadIdx.x] = sw;
+    __syncthreads();
+  };
+  clx16 y0, y1;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) y0[e] = y1[e] = 0.f;
+  float z = 0.f;
+  stage(s0, 0);
+  if (s0 + 32 < s1) stage(s0 + 32, 1);
+  clx16 scur = sprod(s_stg);
+  int cur = 0;
+  float4 st[2];
+  float sw = 0.f;
+  for (int j = s0; j < s1; j += 32) {
+    const bool more = j + 32 < s1, refill = j + 64 < s1;
+    if (refill) {  // block j + 2's rows travel while this block is computed
+      cl_load(st, Stg, lds, j + 64, s1);
+      if (TABLE && threadIdx.x < 32) sw = j + 64 + (int)threadIdx.x < s1 ? w[j + 64 + threadIdx.x] : 0.f;
+    }
+    const __bf16* A = s_stg + cur * kC6Stage;
+    clx16 snext;
+    if (more) snext = sprod(s_stg + (cur ^ 1) * kC6Stage);  // the matrix pipe's next S ...
+    float ev[16];  // ... while this block's logits are exponentiated
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int r = (e & 3) + 8 * (e >> 2) + 4 * h;
+      const float x = j + r < s1 ? cl_exp<FAST>(inv_t, scur[e]) : 0.f;
+      if (TABLE) {
+        ev[e] = s_w[cur][r] * x;
+      } else {
+        ev[e] = x;
+        z += x;
+      }
+    }
+    const __bf16* Bt = A + 3 * kC6PA;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {  // Y^T (64 d x 32) += Stg^T E^T, K = 32 staged rows in two steps
+      const float evs[8] = {ev[8 * t2], ev[8 * t2 + 1], ev[8 * t2 + 2], ev[8 * t2 + 3],
+                            ev[8 * t2 + 4], ev[8 * t2 + 5], ev[8 * t2 + 6], ev[8 * t2 + 7]};
+      c6bf8 eb[3], a0[3], a1[3];
+      c6_split8(evs, eb);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        a0[p] = *reinterpret_cast<const c6bf8*>(Bt + p * kC6PB + l32 * kC6B + 8 * (2 * t2 + h));
+        a1[p] = *reinterpret_cast<const c6bf8*>(Bt + p * kC6PB + (32 + l32) * kC6B + 8 * (2 * t2 + h));
+      }
+      y0 = c6_mfma6(a0, eb, y0);
+      y1 = c6_mfma6(a1, eb, y1);
+    }
+    if (refill) {  // block j + 2 takes this block's buffer (s_f's last reader, a convert, finished before a barrier)
+      cl_store(st, s_f);
+      __syncthreads();  // ... and every wave is done with this block's buffer
+      c6_convert(s_f, s_stg + cur * kC6Stage);
+      if (TABLE && threadIdx.x < 32) s_w[cur][threadIdx.x] = sw;
+      __syncthreads();
+    }
+    if (more) scur = snext;
+    cur ^= 1;
+  }
+  if (f < nf) cl_put(part_y + ((int64_t)c * nf + f) * 64, y0, y1, h);
+  if (!TABLE) {
+    const float zf = z + __shfl_xor(z, 32);
+    if (f < nf && h == 0) part_z[(int64_t)c * nf + f] = zf;
+  }
+}
+
+int cl_pipe() {  // read per call (a getenv), so a test can compare both forms in one process
+  const char* e = getenv("GMR_CL_PIPE");
+  return !(e && atoi(e) == 0);
+}
+
 int cl_x6() {  // read per call (a getenv), so a test can compare both pipes in one process
   const char* e = getenv("GMR_CL_X6");
   return !(e && atoi(e) == 0);
@@ -1236,8 +1355,11 @@ extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int6
   }();
   if (cl_x6()) {  // split-bf16 passes (128 fragment rows per workgroup)
     const dim3 ga((unsigned)((B + 127) / 128), (unsigned)p.nca), gb((unsigned)((n + 127) / 128), (unsigned)p.ncb);
-    auto rows6 = fast ? cl6_kernel<true, false> : cl6_kernel<false, false>;
-    auto table6 = fast ? cl6_kernel<true, true> : cl6_kernel<false, true>;
+    const bool pipe = cl_pipe();
+    auto rows6 = pipe ? (fast ? cl6p_kernel<true, false> : cl6p_kernel<false, false>)
+                      : (fast ? cl6_kernel<true, false> : cl6_kernel<false, false>);
+    auto table6 = pipe ? (fast ? cl6p_kernel<true, true> : cl6p_kernel<false, true>)
+                       : (fast ? cl6_kernel<true, true> : cl6_kernel<false, true>);
     hipLaunchKernelGGL(rows6, ga, dim3(256), 0, st, B, (int)n, P, ldp, T, ldt, nullptr, inv_temp, p.chunk_a, part_u,
                        part_z);
     GMR_LAUNCHED();

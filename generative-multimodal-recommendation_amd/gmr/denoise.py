@@ -24,10 +24,12 @@ def _r4(n):
     return (n + 3) // 4 * 4
 
 
-# the graph rebuild's p_sample products from pre-split operands (gmr_gemm_p3_f32: the weights split once per
-# rebuild, x and h carried as bf16 plane sets by the products' epilogues); GMR_P3=0 keeps the split-bf16
-# GEMM that splits fp32 operands on the fly (gemm_x6)
-P3 = os.environ.get("GMR_P3", "1") != "0"
+# GMR_P3=1: the graph rebuild's p_sample products from pre-split operands (gmr_gemm_p3_f32: the weights split
+# once per rebuild, x and h carried as bf16 plane sets by the products' epilogues).  Opt-in: faster alone
+# (hidden product 1.70 -> 1.52 ms) but the plane sets carry 6 bytes per element where fp32 carries 4, and
+# with the image and text sweeps running concurrently the rebuild phase takes 37.3 ms vs 33.0 ms for the
+# default split-bf16 GEMM that splits fp32 operands on the fly (gemm_x6; profiles/r04j_ab.txt)
+P3 = os.environ.get("GMR_P3", "0") != "0"
 
 
 class _Linear(nn.Module):

@@ -86,8 +86,13 @@ def _near_tie_ok(vals_ref_row, idx_ref_row, ours_item, tol):
     return len(hit) > 0 and vals_ref_row[0] - vals_ref_row[hit[0]] <= tol * max(1.0, abs(float(vals_ref_row[0])))
 
 
-def test_p_sample_top1_all_users(baby):
+@pytest.mark.parametrize("p3", [False, True], ids=["x6", "p3"])
+def test_p_sample_top1_all_users(baby, p3, monkeypatch):
+    """Both forms of the rebuild products: the default on-the-fly split-bf16 GEMM and the opt-in
+    pre-split plane sets (GMR_P3=1, gmr_gemm_p3_f32)."""
+    from gmr import denoise as dn
     from gmr import kernels as K
+    monkeypatch.setattr(dn, "P3", p3)
     m, g = baby["model"], baby["g"]
     U = m.n_users
     for mod in ("image", "text"):

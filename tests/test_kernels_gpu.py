@@ -454,6 +454,32 @@ def test_contrast_two_fragments_bit_exact(K, B, n, monkeypatch):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,n", [(2048, 19445), (2048, 7050), (300, 7050), (37, 100), (300, 33), (64, 65)])
+def test_contrast_pipelined_bit_exact(K, B, n, monkeypatch):
+    """GMR_CL_PIPE (default): the split-bf16 InfoNCE passes with the next block's S product issued before
+    this block's exp / split keep the staging, chunking and every sum of the unpipelined passes: loss,
+    dP and dT bit for bit (chunks of one, two and many 32-row blocks, ragged last blocks)."""
+    monkeypatch.setenv("GMR_CL_X6", "1")
+    rng = _rng(13)
+    C = rng.standard_normal((n, 128)).astype(np.float32)
+    C /= np.linalg.norm(C, axis=1, keepdims=True)
+    nodes = rng.integers(0, n, B).astype(np.int32)
+    Cd, nd = _dev(C), _dev(nodes)
+    P = torch.empty((B, 64), device=DEV)
+    K.gather_rows(Cd[:, :64], nd, P, off=0)
+    ws = K.contrast_workspace(B, n, DEV, "test_cl_pipe")
+    outs = []
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("GMR_CL_PIPE", pipe)
+        loss = torch.empty(B, device=DEV)
+        contrib = torch.empty((B, 128), device=DEV)
+        dt = torch.empty((n, 128), device=DEV)
+        K.contrast_fused(P, Cd[:, 64:], Cd, nd, 0, 1.0 / 0.2, 0.01 / B, loss, contrib, dt[:, 64:], ws)
+        outs.append((loss.cpu(), contrib.cpu(), dt[:, 64:].cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("nb", [1, 2, 4])
 def test_spmm_chunk_rows_spanning_groups(K, nb):
     """Chunk plan: rows of degree 1..128 packed into 128-entry tasks, many of them crossing the
