@@ -109,6 +109,7 @@ SIGNATURES = {
     "gmr_mask_scores_f32": (I32, [I64, P, P, P, I64, F32, P]),
     "gmr_topk_rows_f32": (I32, [I64, I64, P, I64, I32, P, I64, P, P]),
     "gmr_score_topk_f32": (I32, [I64, P, P, I64, I64, P, I64, I64, P, P, F32, I32, P, I64, P, P]),
+    "gmr_score_topk_x6": (I32, [I64, P, P, I64, I64, P, I64, I64, I64, P, P, F32, I32, P, I64, P, P]),
     "gmr_eval_metrics_partials": (I64, [I64]),
     "gmr_eval_metrics": (I32, [I64, P, I64, I32, P, P, I32, P, P, P, P]),
     "gmr_eval_metrics_sel": (I32, [I64, P, P, I64, I32, P, P, I32, P, P, P, P]),

@@ -593,13 +593,38 @@ def topk_rows(scores, k, out_idx, out_val=None):
     return out_idx
 
 
+# GMR_EVAL_X6=1: the fused eval scores d = 64 embeddings on the bf16 matrix cores from exact three-way splits
+# (gmr_score_topk_x6; the item table split once per table version).  Opt-in: the kernel is bound by its
+# selection bookkeeping, not the score products (694 us fp32 vs 712 us split per 19,445-user pass,
+# profiles/r04l_topk.txt), so the default keeps the fp32 MFMA scores
+EVAL_X6 = os.environ.get("GMR_EVAL_X6", "0") != "0"
+_item_planes = {}
+
+
+def _planes_of(itm):
+    """Plane set of the item table, cached per (storage, version, shape): one split per eval pass."""
+    key = (itm.data_ptr(), itm._version, tuple(itm.shape), _ld(itm), itm.device)
+    hit = _item_planes.get("key")
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    pl = Planes(itm.shape[0], itm.shape[1], itm.device).load(itm)
+    _item_planes["key"] = (key, pl)
+    return pl
+
+
 def score_topk(usr, itm, users, mask_ptr, mask_cols, k, out_idx, out_val=None, fill=-1e10):
-    """Fused eval (gmr_score_topk_f32): top-k of usr[users] . itm^T with each row's train positives
+    """Fused eval (gmr_score_topk_f32 / _x6): top-k of usr[users] . itm^T with each row's train positives
     (mask_cols[mask_ptr[r]:mask_ptr[r+1]], sorted) set to fill; no rows x items score buffer."""
     n = users.numel() if users is not None else out_idx.shape[0]
     if out_idx.shape[0] < n or mask_ptr.numel() < n + 1 or mask_ptr.dtype != torch.int64:
         raise ValueError("score_topk: out_idx / mask_ptr (int64, n + 1) too small for the rows")
     if n == 0:  # an empty rank shard: nothing to score (the C-ABI rejects n_rows < 1)
+        return out_idx
+    if EVAL_X6 and itm.shape[1] == 64 and usr.shape[1] == 64:
+        pl = _planes_of(itm)
+        _lib.call("gmr_score_topk_x6", n, ptr(users), ptr(usr), _ld(usr), itm.shape[0], pl.ptr(), pl.ld, pl.ps, 64,
+                  ptr(mask_ptr), ptr(mask_cols), float(fill), int(k), ptr(out_idx), _ld(out_idx), ptr(out_val),
+                  stream())
         return out_idx
     _lib.call("gmr_score_topk_f32", n, ptr(users), ptr(usr), _ld(usr), itm.shape[0], ptr(itm), _ld(itm), itm.shape[1],
               ptr(mask_ptr), ptr(mask_cols), float(fill), int(k), ptr(out_idx), _ld(out_idx), ptr(out_val), stream())

@@ -418,6 +418,14 @@ int gmr_score_topk_f32(int64_t n_rows, const int32_t* users, const float* user_t
                        const float* item_table, int64_t ld_item, int64_t dim, const int64_t* mask_ptr,
                        const int32_t* mask_cols, float fill, int32_t k, int32_t* out_idx, int64_t ld_idx,
                        float* out_val, void* stream);
+/* The same with the scores on the bf16 matrix cores (round 4): the item table as a plane set
+ * (gmr_split3_planes: item_planes[p * plane_stride + i * ld_plane + c], x = hi + mid + lo exactly) and
+ * the six-product split of gmr_gemm_p3_f32 (fp32-accurate sums, 2.7x the fp32 MFMA rate); the user
+ * table stays fp32 and is split in registers.  dim 64; ld_plane a multiple of 8. */
+int gmr_score_topk_x6(int64_t n_rows, const int32_t* users, const float* user_table, int64_t ld_user, int64_t n_items,
+                      const uint16_t* item_planes, int64_t ld_plane, int64_t plane_stride, int64_t dim,
+                      const int64_t* mask_ptr, const int32_t* mask_cols, float fill, int32_t k, int32_t* out_idx,
+                      int64_t ld_idx, float* out_val, void* stream);
 /* Recall/NDCG/Precision/MAP sums over users at ks (topk_evaluator.py:107-120, metrics.py):
  * out_sums[metric*8 + j], metric 0 recall 1 ndcg 2 precision 3 map, j < n_ks (fp64). */
 int64_t gmr_eval_metrics_partials(int64_t n_users);

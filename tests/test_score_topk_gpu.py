@@ -1,4 +1,4 @@
-"""Fused eval kernel (gmr_score_topk_f32): scores = U[users] . I^T -> train positives set to -1e10 ->
+"""Fused eval kernel (gmr_score_topk_f32 / gmr_score_topk_x6): scores = U[users] . I^T -> train positives set to -1e10 ->
 top-k (score desc, ties -> lowest index), the reference's common/trainer.py:379-386 with
 models/diffmm.py:276-277, without the E x I score matrix.
 
@@ -12,6 +12,15 @@ import torch
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, params=[False, True], ids=["fp32", "x6"])
+def scoring(request, monkeypatch):
+    """Every test on both score forms: fp32 MFMA (gmr_score_topk_f32, the default) and, for d = 64, the
+    split-bf16 MFMA from item planes (gmr_score_topk_x6, GMR_EVAL_X6=1)."""
+    from gmr import kernels as K
+    monkeypatch.setattr(K, "EVAL_X6", request.param)
+    return request.param
 
 
 def _mask(rng, n_rows, n_items, max_len, full_row=None):
