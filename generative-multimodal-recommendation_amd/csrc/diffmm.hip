@@ -1074,13 +1074,50 @@ __device__ __forceinline__ clx16 c6_mfma6(const c6bf8 (&a)[3], const c6bf8 (&b)[
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
 }
 
+// In-launch reduction of the table pass (replaces cl_table_reduce_kernel): each i-chunk block of a
+// 128-row table tile stores its partial, publishes it (agent-scope release) and counts itself in the
+// tile's counter; the block that arrives last (acquire) sums the tile's partials in chunk order c = 0,
+// 1, ... (cl_table_reduce_kernel's order: same bits) into dT and resets the counter for the next call.
+constexpr int kClCounters = 8192;  // counter words leading the contrast workspace (tables <= 1M rows)
+__device__ __forceinline__ void cl_table_fixup(int* cnt, const float* __restrict__ part, int n, float* __restrict__ dT,
+                                               int64_t ld) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (int)gridDim.y - 1;
+    if (last) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const int nc = (int)gridDim.y;
+  const int64_t j0 = (int64_t)blockIdx.x * 128;
+  for (int g = threadIdx.x; g < 128 * 16; g += blockDim.x) {
+    const int64_t j = j0 + (g >> 4);
+    if (j >= n) continue;
+    const int c4 = (g & 15) * 4;
+    float4 a = ld4(part + j * 64 + c4);
+    for (int c = 1; c < nc; ++c) a = gmr::f4_add(a, ld4(part + ((int64_t)c * n + j) * 64 + c4));
+    st4(dT + j * ld + c4, a);
+  }
+}
+
 // TABLE = false (rows pass): F = P (queries), Stg = T (keys), part_y / part_z per query chunk;
 // TABLE = true (table pass): F = T rows, Stg = P rows weighted by w = r_i, part_y = dT partials
 template <bool FAST, bool TABLE>
 __global__ void __launch_bounds__(256, 2) cl6_kernel(int nf, int ns, const float* __restrict__ F, int64_t ldf,
                                                      const float* __restrict__ Stg, int64_t lds,
                                                      const float* __restrict__ w, float inv_t, int chunk,
-                                                     float* __restrict__ part_y, float* __restrict__ part_z) {
+                                                     float* __restrict__ part_y, float* __restrict__ part_z,
+                                                     int* __restrict__ cnt, float* __restrict__ dT, int64_t ld_dt) {
   __shared__ __attribute__((aligned(16))) __bf16 s_stg[2 * kC6Stage];
   __shared__ __attribute__((aligned(16))) float s_f[32 * kClLd];
   __shared__ float s_w[2][32];
@@ -1169,6 +1206,7 @@ __global__ void __launch_bounds__(256, 2) cl6_kernel(int nf, int ns, const float
     const float zf = z + __shfl_xor(z, 32);
     if (f < nf && h == 0) part_z[(int64_t)c * nf + f] = zf;
   }
+  if (TABLE && cnt) cl_table_fixup(cnt + blockIdx.x, part_y, nf, dT, ld_dt);
 }
 
 // The same pass with the S product of block j + 1 issued before the exp / split phase of block j (PIPE,
@@ -1180,7 +1218,8 @@ template <bool FAST, bool TABLE>
 __global__ void __launch_bounds__(256, 2) cl6p_kernel(int nf, int ns, const float* __restrict__ F, int64_t ldf,
                                                       const float* __restrict__ Stg, int64_t lds,
                                                       const float* __restrict__ w, float inv_t, int chunk,
-                                                      float* __restrict__ part_y, float* __restrict__ part_z) {
+                                                      float* __restrict__ part_y, float* __restrict__ part_z,
+                                                      int* __restrict__ cnt, float* __restrict__ dT, int64_t ld_dt) {
   __shared__ __attribute__((aligned(16))) __bf16 s_stg[2 * kC6Stage];
   __shared__ __attribute__((aligned(16))) float s_f[32 * kClLd];
   __shared__ float s_w[2][32];
@@ -1283,6 +1322,12 @@ __global__ void __launch_bounds__(256, 2) cl6p_kernel(int nf, int ns, const floa
     const float zf = z + __shfl_xor(z, 32);
     if (f < nf && h == 0) part_z[(int64_t)c * nf + f] = zf;
   }
+  if (TABLE && cnt) cl_table_fixup(cnt + blockIdx.x, part_y, nf, dT, ld_dt);
+}
+
+int cl_fixup() {  // GMR_CL_FIXUP=0: the table partials reduced by cl_table_reduce_kernel (read per call)
+  const char* e = getenv("GMR_CL_FIXUP");
+  return !(e && atoi(e) == 0);
 }
 
 int cl_pipe() {  // read per call (a getenv), so a test can compare both forms in one process
@@ -1326,10 +1371,11 @@ ClPlan cl_plan(int64_t B, int64_t n) {
 
 }  // namespace
 
+// workspace: [kClCounters table-tile counters (zero between calls) | part_u | part_z | r | part_t]
 extern "C" int64_t gmr_contrast_workspace_floats(int32_t B, int64_t n) {
   if (B <= 0 || n <= 0) return -1;
   const ClPlan p = cl_plan(B, n);
-  return (int64_t)p.nca * B * 65 + B + (int64_t)p.ncb * n * 64;
+  return kClCounters + (int64_t)p.nca * B * 65 + B + (int64_t)p.ncb * n * 64;
 }
 
 extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int64_t ldp, const float* T, int64_t ldt,
@@ -1344,7 +1390,8 @@ extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int6
   GMR_ARG((((uintptr_t)P | (uintptr_t)T | (uintptr_t)dT) & 15) == 0, "P, T and dT must be 16-byte aligned");
   GMR_ARG(workspace_floats >= gmr_contrast_workspace_floats(B, n), "workspace too small");
   const ClPlan p = cl_plan(B, n);
-  float* part_u = workspace;
+  int* counters = reinterpret_cast<int*>(workspace);
+  float* part_u = workspace + kClCounters;
   float* part_z = part_u + (int64_t)p.nca * B * 64;
   float* r = part_z + (int64_t)p.nca * B;
   float* part_t = r + B;
@@ -1361,17 +1408,21 @@ extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int6
     auto table6 = pipe ? (fast ? cl6p_kernel<true, true> : cl6p_kernel<false, true>)
                        : (fast ? cl6_kernel<true, true> : cl6_kernel<false, true>);
     hipLaunchKernelGGL(rows6, ga, dim3(256), 0, st, B, (int)n, P, ldp, T, ldt, nullptr, inv_temp, p.chunk_a, part_u,
-                       part_z);
+                       part_z, nullptr, nullptr, 0);
     GMR_LAUNCHED();
     hipLaunchKernelGGL(cl_finalize_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, p.nca, part_u, part_z,
                        CLN, nodes, node_off, inv_temp, coef, loss, contrib, ld_contrib, r);
     GMR_LAUNCHED();
+    // the table pass reduces its own partials (last block per tile) when its tiles fit the counters
+    const bool fix = cl_fixup() && gb.x <= (unsigned)kClCounters;
     hipLaunchKernelGGL(table6, gb, dim3(256), 0, st, (int)n, B, T, ldt, P, ldp, r, inv_temp, p.chunk_b, part_t,
-                       nullptr);
+                       nullptr, fix ? counters : nullptr, dT, ld_dt);
     GMR_LAUNCHED();
-    hipLaunchKernelGGL(cl_table_reduce_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n, p.ncb,
-                       part_t, dT, ld_dt);
-    GMR_LAUNCHED();
+    if (!fix) {
+      hipLaunchKernelGGL(cl_table_reduce_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n, p.ncb,
+                         part_t, dT, ld_dt);
+      GMR_LAUNCHED();
+    }
     return GMR_OK;
   }
   const int nf = cl_nf();

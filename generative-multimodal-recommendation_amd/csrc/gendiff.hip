@@ -4,6 +4,8 @@
 //   ModalDenoiseTransformer (models/genrecv1.py:650-710) row kernels — LayerNorm (+ residual,
 //   + dropout, + GELU) forward/backward, adaLN modulation, dropout masks, time embedding, SiLU.
 // The dense products of the transformer run on the MFMA GEMM (gemm.hip).
+#include <algorithm>
+
 #include "gmr_common.h"
 
 namespace {
@@ -345,6 +347,115 @@ __global__ void dropout_kernel(int64_t rows, int D, int group, const float* __re
   y[r * ldy + c] = k ? x[r * ldx + c] / p_keep : 0.f;
 }
 
+// ---------------------------------------------------------------- cross-attention on the zero memory
+// nn.TransformerDecoderLayer's multihead_attn over the all-zero memory (models/genrecv1.py:650-710):
+// every key / value is the in-projection bias, so head h's attention output is bv'_h for every row and
+// the block is out_proj(dropout_head(bv')) + b_o.  With head dropout that is, per row, a mixture of
+// nhead fixed vectors: CA[r] = b_o + sum_h keep[r][h] P[h], P[h][j] = sum_{c in head h} Wo[j][c] bv'[c] /
+// p_keep, so the B x D x D product of the unfused path becomes a table of nhead x D (once per weight
+// version) and a per-row sum; its backward, the per-head column sums Gs[h][j] = sum_r keep[r][h] dCA[r][j].
+// P[l][h][j] for the L layers at once (layer l's tensors at woc0 / bvc0 + l * lstride; Wo row-major, ld D)
+__global__ void xattn_table_kernel(int L, int D, int nhead, const float* __restrict__ woc0,
+                                   const float* __restrict__ bvc0, int64_t lstride, float p_keep, float* __restrict__ P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)L * nhead * D) return;
+  const int j = (int)(i % D), h = (int)((i / D) % nhead);
+  const int64_t l = i / ((int64_t)D * nhead);
+  const float* w = woc0 + l * lstride + (int64_t)j * D;
+  const float* b = bvc0 + l * lstride;
+  const int g = D / nhead;
+  float s = 0.f;
+  for (int c = h * g; c < (h + 1) * g; ++c) s = fmaf(w[c], b[c] / p_keep, s);
+  P[i] = s;
+}
+
+// one row per block: the row's nhead keep flags (the head-dropout draw of dropout_kernel, group D / nhead:
+// Philox counter (row0 + r) * nhead + h) or the given mask, then CA[r][j] = sum_h keep P[h][j] + b_o[j]
+__global__ void __launch_bounds__(256) xattn_fwd_kernel(int D, int nhead, const float* __restrict__ P,
+                                                        const float* __restrict__ bo, float p_keep,
+                                                        const uint8_t* __restrict__ mask_in, uint8_t* __restrict__ mask_out,
+                                                        int64_t ldm, uint64_t seed, uint64_t step, int64_t row0,
+                                                        float* __restrict__ CA, int64_t ldc) {
+  __shared__ float kf[64];
+  const int64_t r = blockIdx.x;
+  if ((int)threadIdx.x < nhead) {
+    const int h = threadIdx.x;
+    bool k;
+    if (mask_in) {
+      k = mask_in[r * ldm + h] != 0;
+    } else {
+      const uint4 rr = gmr::Philox::gen(seed, step, (uint64_t)((row0 + r) * nhead + h));
+      k = unit01(rr.x) < p_keep;
+      if (mask_out) mask_out[r * ldm + h] = k ? 1 : 0;
+    }
+    kf[h] = k ? 1.f : 0.f;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < D; j += blockDim.x) {
+    float s = 0.f;
+    for (int h = 0; h < nhead; ++h)
+      if (kf[h] != 0.f) s += P[(int64_t)h * D + j];
+    CA[r * ldc + j] = s + bo[j];
+  }
+}
+
+// per-head column sums of dCA over a chunk of rows -> part[chunk][h][j] (64 columns x 4 row lanes per block)
+constexpr int kXattnMaxHeads = 16;
+__global__ void __launch_bounds__(256) xattn_bwd_part_kernel(int64_t rows, int D, int nhead,
+                                                             const float* __restrict__ dCA, int64_t ld,
+                                                             const uint8_t* __restrict__ mask, int64_t ldm,
+                                                             int64_t chunk, float* __restrict__ part) {
+  __shared__ float red[4][kXattnMaxHeads][64];
+  const int tx = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + tx;
+  const int64_t r0 = (int64_t)blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
+  float acc[kXattnMaxHeads];
+#pragma unroll
+  for (int h = 0; h < kXattnMaxHeads; ++h) acc[h] = 0.f;
+  if (j < D)
+    for (int64_t r = r0 + rl; r < r1; r += 4) {
+      const float d = dCA[r * ld + j];
+#pragma unroll
+      for (int h = 0; h < kXattnMaxHeads; ++h)
+        if (h < nhead && mask[r * ldm + h]) acc[h] += d;
+    }
+#pragma unroll
+  for (int h = 0; h < kXattnMaxHeads; ++h) red[rl][h][tx] = acc[h];
+  __syncthreads();
+  if (rl == 0 && j < D)
+    for (int h = 0; h < nhead; ++h)
+      part[((int64_t)blockIdx.y * nhead + h) * D + j] = (red[0][h][tx] + red[1][h][tx]) + (red[2][h][tx] + red[3][h][tx]);
+}
+
+// Gs[h][j] = sum over the chunks (fixed order)
+__global__ void xattn_bwd_reduce_kernel(int D, int nhead, int chunks, const float* __restrict__ part,
+                                        float* __restrict__ G) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nhead * D) return;
+  float s = 0.f;
+  for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * nhead * D + i];
+  G[i] = s;
+}
+
+// dWo[j][c] += Gs[h(c)][j] bv'[c] / p_keep (Bc = keep bv' / p_keep); dbv'[c] += sum_j Wo[j][c] Gs[h(c)][j] / p_keep
+__global__ void xattn_bwd_apply_kernel(int D, int nhead, const float* __restrict__ G, const float* __restrict__ wo,
+                                       const float* __restrict__ bv, float p_keep, float* __restrict__ g_wo,
+                                       float* __restrict__ g_bv) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t DD = (int64_t)D * D;
+  const int g = D / nhead;
+  if (i < DD) {
+    const int j = (int)(i / D), c = (int)(i % D);
+    g_wo[i] += G[(int64_t)(c / g) * D + j] * (bv[c] / p_keep);
+  } else if (i < DD + D) {
+    const int c = (int)(i - DD);
+    const float* gh = G + (int64_t)(c / g) * D;
+    float s = 0.f;
+    for (int j = 0; j < D; ++j) s = fmaf(wo[(int64_t)j * D + c], gh[j], s);
+    g_bv[c] += s / p_keep;
+  }
+}
+
 // temb[t] = [cos(t f_k) | sin(t f_k)], f_k = exp(-ln(1e4) k / half) (:692-696); odd sizes zero-pad
 __global__ void time_embedding_kernel(int T, int E, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -501,6 +612,60 @@ extern "C" int gmr_dropout_f32(int64_t rows, int32_t D, int32_t group, const flo
   GMR_ARG(p_keep > 0.f && p_keep <= 1.f, "p_keep in (0, 1]");
   hipLaunchKernelGGL(dropout_kernel, dim3(gmr::grid_for(rows * D, 256)), dim3(256), 0, (hipStream_t)stream, rows, D,
                      group, x, ldx, p_keep, mask_in, mask_out, ldm, seed, step, row0, y, ldy);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_xattn_table_f32(int32_t L, int32_t D, int32_t nhead, const float* woc0, const float* bvc0,
+                                   int64_t layer_stride, float p_keep, float* P, void* stream) {
+  GMR_ARG(woc0 && bvc0 && P && L > 0 && D > 0 && nhead > 0 && nhead <= 64 && D % nhead == 0, "bad args");
+  GMR_ARG(p_keep > 0.f && p_keep <= 1.f, "p_keep in (0, 1]");
+  const int64_t n = (int64_t)L * nhead * D;
+  hipLaunchKernelGGL(xattn_table_kernel, dim3(gmr::grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, L, D, nhead,
+                     woc0, bvc0, layer_stride, p_keep, P);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_xattn_fwd_f32(int64_t rows, int32_t D, int32_t nhead, const float* P, const float* bo, float p_keep,
+                                 const uint8_t* mask_in, uint8_t* mask_out, int64_t ldm, uint64_t seed, uint64_t step,
+                                 int64_t row0, float* CA, int64_t ldc, void* stream) {
+  GMR_ARG(P && bo && CA && rows > 0 && rows < (1ll << 31) && D > 0 && nhead > 0 && nhead <= 64 && D % nhead == 0 &&
+              ldm >= nhead && ldc >= D && row0 >= 0,
+          "bad args");
+  GMR_ARG(p_keep > 0.f && p_keep <= 1.f, "p_keep in (0, 1]");
+  hipLaunchKernelGGL(xattn_fwd_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, D, nhead, P, bo, p_keep,
+                     mask_in, mask_out, ldm, seed, step, row0, CA, ldc);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int64_t gmr_xattn_bwd_workspace_floats(int64_t rows, int32_t D, int32_t nhead) {
+  const int64_t chunks = std::min<int64_t>(32, std::max<int64_t>(1, (rows + 127) / 128));
+  return chunks * nhead * D + (int64_t)nhead * D;
+}
+
+extern "C" int gmr_xattn_bwd_f32(int64_t rows, int32_t D, int32_t nhead, const float* dCA, int64_t ld,
+                                 const uint8_t* mask, int64_t ldm, const float* wo, const float* bv, float p_keep,
+                                 float* g_wo, float* g_bv, float* ws, int64_t ws_floats, void* stream) {
+  GMR_ARG(dCA && mask && wo && bv && g_wo && g_bv && ws && rows > 0 && D > 0 && nhead > 0 &&
+              nhead <= kXattnMaxHeads && D % nhead == 0 && ld >= D && ldm >= nhead,
+          "bad args");
+  GMR_ARG(p_keep > 0.f && p_keep <= 1.f, "p_keep in (0, 1]");
+  GMR_ARG(ws_floats >= gmr_xattn_bwd_workspace_floats(rows, D, nhead), "workspace too small");
+  const int64_t chunks = std::min<int64_t>(32, std::max<int64_t>(1, (rows + 127) / 128));
+  const int64_t chunk = (rows + chunks - 1) / chunks;
+  float* part = ws;
+  float* G = ws + chunks * nhead * D;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(xattn_bwd_part_kernel, dim3((unsigned)((D + 63) / 64), (unsigned)chunks), dim3(256), 0, st, rows, D,
+                     nhead, dCA, ld, mask, ldm, chunk, part);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(xattn_bwd_reduce_kernel, dim3(gmr::grid_for((int64_t)nhead * D, 256)), dim3(256), 0, st, D, nhead,
+                     (int)chunks, part, G);
+  GMR_LAUNCHED();
+  hipLaunchKernelGGL(xattn_bwd_apply_kernel, dim3(gmr::grid_for((int64_t)D * D + D, 256)), dim3(256), 0, st, D, nhead,
+                     G, wo, bv, p_keep, g_wo, g_bv);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -63,6 +63,11 @@ class TransformerDenoiser:
                   ("adaLN_modulation_1_weight", (2 * D, E), None), ("adaLN_modulation_1_bias", (2 * D,), None)]
         self.names = [s[0] for s in specs]
         self.slab = Slab(specs, device)
+        # floats between one decoder layer's tensors and the next's (the same spec list per layer)
+        o = self.slab.offsets
+        self.layer_stride = (o["transformer_decoder_layers_1_linear1_weight"] - o["transformer_decoder_layers_0_linear1_weight"]
+                             if num_layers > 1 else 0)
+        self._cache = None  # (T, train_drop, keep) of the time tables / cross-attention tables held
         self.training = True
         self._ws = None
         self._temb = None
@@ -107,7 +112,7 @@ class TransformerDenoiser:
         u8 = lambda *s: torch.empty(s, dtype=torch.uint8, device=dev)  # noqa: E731
         w = {"B": B, "h0": f(B, D), "h": f(L + 1, B, D), "V": f(L, B, D), "SAin": f(L, B, D),
              "SA": f(L, B, D), "s1": f(L, B, D), "h1": f(L, B, D), "m1": f(L, 3, B),
-             "CA": f(L, B, D), "Bc": f(L, B, D), "s2": f(L, B, D), "h2": f(L, B, D),
+             "CA": f(L, B, D), "s2": f(L, B, D), "h2": f(L, B, D),
              "F1": f(L, B, D), "F2": f(L, B, D), "s3": f(L, B, D), "m2": f(L, 3, B), "m3": f(L, 3, B),
              "o1": f(B, H2), "og": f(B, H2), "mo": f(2, B),
              "mask_a": u8(L, B, self.nhead), "mask_c": u8(L, B, self.nhead), "mask_1": u8(L, B, D),
@@ -116,14 +121,20 @@ class TransformerDenoiser:
              "dh": f(B, D), "dA": f(B, D), "dB": f(B, D), "dC": f(B, D), "dg": f(B, H2), "do1": f(B, H2),
              "prod": f(B, D), "ln_parts": f(int(_lib.load().gmr_layernorm_parts_floats(B, D))),
              "te": f(T, self.E), "ste": f(T, self.E), "TB": f(T, D), "S": f(T, 2 * D), "cav": f(L, D),
-             "dS": f(2 * T, D), "dTB": f(T, D), "dte": f(T, self.E), "col": f(2 * D)}
+             "dS": f(2 * T, D), "dTB": f(T, D), "dte": f(T, self.E), "col": f(2 * D),
+             "xP": f(L, self.nhead, D),
+             "xws": f(int(_lib.load().gmr_xattn_bwd_workspace_floats(B, D, self.nhead)))}
         self._ws = w
         return w
 
-    def _tables(self, T):
-        """te = emb_layer(temb(t)), TB = te W_in[:, I:]^T + b_in, S = SiLU(te) W_ada^T + b_ada, t < T."""
+    def _tables(self, T, reuse=False):
+        """te = emb_layer(temb(t)), TB = te W_in[:, I:]^T + b_in, S = SiLU(te) W_ada^T + b_ada, t < T.
+        reuse: the caller guarantees the weights are those of the previous forward (a p_sample step after
+        its first), so tables of the same T are kept."""
         w = self._work(1)
         I, E, D = self.I, self.E, self.D
+        if reuse and self._cache is not None and self._cache[0] == T:
+            return w["te"][:T], w["ste"][:T], w["TB"][:T], w["S"][:T]
         if self._temb is None or self._temb.shape[0] != T:
             self._temb = torch.empty((T, E), dtype=torch.float32, device=self.device)
             _lib.call("gmr_time_embedding", T, E, ptr(self._temb), stream())
@@ -137,18 +148,28 @@ class TransformerDenoiser:
         return te, ste, TB, S
 
     # ------------------------------------------------------------------ forward
-    def forward(self, x, t_rows=None, t_const=None, T=5, out=None, masks=None, seed=None, step=0, row0=0):
+    def forward(self, x, t_rows=None, t_const=None, T=5, out=None, masks=None, seed=None, step=0, row0=0,
+                reuse_tables=False):
         """logits = model(x, t) for x (B x I, fp32, ld % 4 == 0) and per-row t (int32 device tensor) or
         a constant t.  Train mode draws the dropout masks (Philox seed/step, keyed by the global row
         row0 + r, so a data-parallel rank draws what one process holding the whole batch draws) unless
-        `masks` gives them ({'a','c','1','2','3','f'} -> uint8 (L, B, ...)); returns out (B x I)."""
+        `masks` gives them ({'a','c','1','2','3','f'} -> uint8 (L, B, ...)); returns out (B x I).
+        reuse_tables: the weights are the previous forward's (p_sample steps after the first): the time
+        tables and the cross-attention tables of the same T and mode are kept."""
         B = x.shape[0]
         w = self._work(B)
         D, I, L, H2 = self.D, self.I, self.L, self.H2
-        te, ste, TB, S = self._tables(T)
-        self._T = T
         train_drop = self.training and self.p > 0.0
         keep = 1.0 - self.p
+        mode = (T, train_drop, keep)
+        reuse = reuse_tables and self._cache == mode
+        te, ste, TB, S = self._tables(T, reuse)
+        self._T = T
+        if train_drop and not reuse:  # cross-attention head tables of the L layers (gmr_xattn_table_f32)
+            p0 = "transformer_decoder_layers_0_"
+            _lib.call("gmr_xattn_table_f32", L, D, self.nhead, ptr(self.v(p0 + "multihead_attn_out_proj_weight")),
+                      ptr(self.v(p0 + "multihead_attn_in_proj_bias")[2 * D:]), self.layer_stride, keep, ptr(w["xP"]),
+                      stream())
         seed = self._seed if seed is None else seed
         win = self.v("input_proj_weight")
         h0 = w["h0"][:B]
@@ -182,14 +203,21 @@ class TransformerDenoiser:
             h2 = w["h2"][l, :B]
             m2 = w["m2"][l]
             if train_drop:
-                Bc, CA = w["Bc"][l, :B], w["CA"][l, :B]
-                self._drop(bvc.view(1, D), Bc, "c", l, masks, keep, seed, step, row0, group=D // self.nhead, ldx=0)
-                K.gemm(Bc, woc, CA, trans_b=True, epi=K.EPI_BIAS, bias=boc)
+                # out_proj(dropout_head(b_v)) + b_o as a per-row mixture of the layer's head vectors
+                CA = w["CA"][l, :B]
+                mbuf = w["mask_c"][l, :B]
+                given = masks.get("c") if masks else None
+                if given is not None:
+                    mbuf.copy_(given[l])
+                _lib.call("gmr_xattn_fwd_f32", B, D, self.nhead, ptr(w["xP"][l]), ptr(boc), keep,
+                          ptr(mbuf) if given is not None else None, ptr(mbuf) if given is None else None,
+                          mbuf.stride(0), seed, self._site_step(step, l, "c"), int(row0), ptr(CA), K._ld(CA), stream())
                 self._ln(h1, CA, D, w["mask_2"][l, :B], "2", l, masks, keep, seed, step, row0, self.v(p + "norm2_weight"),
                          self.v(p + "norm2_bias"), h2, w["s2"][l, :B], m2[0, :B], m2[1, :B])
             else:
                 cav = w["cav"][l:l + 1]
-                K.gemm(bvc.view(1, D), woc, cav, trans_b=True, epi=K.EPI_BIAS, bias=boc)
+                if not reuse:
+                    K.gemm(bvc.view(1, D), woc, cav, trans_b=True, epi=K.EPI_BIAS, bias=boc)
                 self._ln(h1, cav, 0, None, "2", l, masks, keep, seed, step, row0, self.v(p + "norm2_weight"),
                          self.v(p + "norm2_bias"), h2, w["s2"][l, :B], m2[0, :B], m2[1, :B])
             F1, F2 = w["F1"][l, :B], w["F2"][l, :B]
@@ -214,6 +242,7 @@ class TransformerDenoiser:
         K.gemm(og, self.v("output_proj_3_weight"), out, trans_b=True, epi=K.EPI_BIAS,
                bias=self.v("output_proj_3_bias"))
         self._last = (B, x, t_rows, t_const, train_drop, keep)
+        self._cache = mode
         return out
 
     def _drop(self, x, y, site, l, masks, keep, seed, step, row0, group, ldx=None):
@@ -295,11 +324,12 @@ class TransformerDenoiser:
             gbvc = self.g(p + "multihead_attn_in_proj_bias")[2 * D:]
             if train_drop:
                 dCA = self._mask_grad(dh, w["mask_2"][l, :B], keep, dB)
-                K.gemm(dCA, w["Bc"][l, :B], self.g(p + "multihead_attn_out_proj_weight"), trans_a=True, beta=1.0)
+                mc = w["mask_c"][l, :B]
+                xws = w["xws"]
+                _lib.call("gmr_xattn_bwd_f32", B, D, self.nhead, ptr(dCA), K._ld(dCA), ptr(mc), mc.stride(0), ptr(woc),
+                          ptr(bvc), keep, ptr(self.g(p + "multihead_attn_out_proj_weight")), ptr(gbvc), ptr(xws),
+                          xws.numel(), stream())
                 K.colsum(dCA, self.g(p + "multihead_attn_out_proj_bias"), accumulate=True)
-                K.gemm(dCA, woc, dC)                                              # d Bc
-                dBc = self._mask_grad(dC, w["mask_c"][l, :B], keep, dC, group=D // self.nhead)
-                K.colsum(dBc, gbvc, accumulate=True)
             else:
                 col = w["col"][:D].view(1, D)
                 K.colsum(dh, col)

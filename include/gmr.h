@@ -593,6 +593,24 @@ int gmr_adaln_bwd(int64_t rows, int32_t D, const float* h0, int64_t ld0, const f
 int gmr_dropout_f32(int64_t rows, int32_t D, int32_t group, const float* x, int64_t ldx, float p_keep,
                     const uint8_t* mask_in, uint8_t* mask_out, int64_t ldm, uint64_t seed, uint64_t step, int64_t row0,
                     float* y, int64_t ldy, void* stream);
+/* Cross-attention of the decoder layers on their all-zero memory (models/genrecv1.py:650-710): head h
+ * outputs the value bias bv'_h on every row, so with head dropout the block is, per row, a mixture of
+ * nhead fixed vectors.  gmr_xattn_table_f32: P[l][h][j] = sum_{c in head h} Wo_l[j][c] bv'_l[c] / p_keep
+ * for the L layers (layer l's tensors at woc0 / bvc0 + l * layer_stride floats; Wo row-major, ld D).
+ * gmr_xattn_fwd_f32: CA[r] = b_o + sum_h keep[r][h] P[h] (keep drawn as gmr_dropout_f32 with group
+ * D / nhead draws it, or read from mask_in; mask_out records it).  gmr_xattn_bwd_f32: from dCA (B x D)
+ * and the masks, dWo += Gs[h(c)][j] bv'[c] / p_keep and dbv' += sum_j Wo[j][c] Gs[h(c)][j] / p_keep,
+ * Gs[h][j] = sum_r keep[r][h] dCA[r][j]; nhead <= 16; ws of gmr_xattn_bwd_workspace_floats floats.
+ * They replace the B x D x D out-projection GEMM, its transposed-operand gradient and dBc products. */
+int gmr_xattn_table_f32(int32_t L, int32_t D, int32_t nhead, const float* woc0, const float* bvc0,
+                        int64_t layer_stride, float p_keep, float* P, void* stream);
+int gmr_xattn_fwd_f32(int64_t rows, int32_t D, int32_t nhead, const float* P, const float* bo, float p_keep,
+                      const uint8_t* mask_in, uint8_t* mask_out, int64_t ldm, uint64_t seed, uint64_t step, int64_t row0,
+                      float* CA, int64_t ldc, void* stream);
+int64_t gmr_xattn_bwd_workspace_floats(int64_t rows, int32_t D, int32_t nhead);
+int gmr_xattn_bwd_f32(int64_t rows, int32_t D, int32_t nhead, const float* dCA, int64_t ld, const uint8_t* mask,
+                      int64_t ldm, const float* wo, const float* bv, float p_keep, float* g_wo, float* g_bv, float* ws,
+                      int64_t ws_floats, void* stream);
 /* sinusoidal time embedding table T x E (:692-696); SiLU (dy == NULL) or its backward */
 int gmr_time_embedding(int32_t T, int32_t E, float* out, void* stream);
 int gmr_silu_f32(int64_t n, const float* x, const float* dy, float* y, void* stream);

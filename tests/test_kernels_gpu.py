@@ -450,8 +450,9 @@ def test_contrast_two_fragments_bit_exact(K, B, n, monkeypatch):
         dt = torch.empty((n, 128), device=DEV)
         K.contrast_fused(P, Cd[:, 64:], Cd, nd, 0, 10.0, 0.01 / B, loss, contrib, dt[:, 64:], ws)
         outs.append((loss.cpu(), contrib.cpu(), dt[:, 64:].cpu()))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("B,n", [(2048, 19445), (2048, 7050), (300, 7050), (37, 100), (300, 33), (64, 65)])
@@ -459,6 +460,18 @@ def test_contrast_pipelined_bit_exact(K, B, n, monkeypatch):
     """GMR_CL_PIPE (default): the split-bf16 InfoNCE passes with the next block's S product issued before
     this block's exp / split keep the staging, chunking and every sum of the unpipelined passes: loss,
     dP and dT bit for bit (chunks of one, two and many 32-row blocks, ragged last blocks)."""
+    _contrast_env_bit_exact(K, B, n, monkeypatch, "GMR_CL_PIPE")
+
+
+@pytest.mark.parametrize("B,n", [(2048, 19445), (2048, 7050), (300, 1000), (40, 97)])
+def test_contrast_table_fixup_bit_exact(K, B, n, monkeypatch):
+    """GMR_CL_FIXUP (default): the table pass sums its chunk partials itself (the last block of each
+    128-row tile, in chunk order, counters left zero for the next call) instead of cl_table_reduce_kernel:
+    dT bit for bit, and repeated calls (the counters reset) stay identical."""
+    _contrast_env_bit_exact(K, B, n, monkeypatch, "GMR_CL_FIXUP", repeats=3)
+
+
+def _contrast_env_bit_exact(K, B, n, monkeypatch, env, repeats=1):
     monkeypatch.setenv("GMR_CL_X6", "1")
     rng = _rng(13)
     C = rng.standard_normal((n, 128)).astype(np.float32)
@@ -467,17 +480,18 @@ def test_contrast_pipelined_bit_exact(K, B, n, monkeypatch):
     Cd, nd = _dev(C), _dev(nodes)
     P = torch.empty((B, 64), device=DEV)
     K.gather_rows(Cd[:, :64], nd, P, off=0)
-    ws = K.contrast_workspace(B, n, DEV, "test_cl_pipe")
+    ws = K.contrast_workspace(B, n, DEV, "test_cl_" + env)
     outs = []
-    for pipe in ("0", "1"):
-        monkeypatch.setenv("GMR_CL_PIPE", pipe)
+    for pipe in ["0"] + ["1"] * repeats:
+        monkeypatch.setenv(env, pipe)
         loss = torch.empty(B, device=DEV)
         contrib = torch.empty((B, 128), device=DEV)
         dt = torch.empty((n, 128), device=DEV)
         K.contrast_fused(P, Cd[:, 64:], Cd, nd, 0, 1.0 / 0.2, 0.01 / B, loss, contrib, dt[:, 64:], ws)
         outs.append((loss.cpu(), contrib.cpu(), dt[:, 64:].cpu()))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("nb", [1, 2, 4])
