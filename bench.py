@@ -273,7 +273,10 @@ def cpu_baseline(model, tl, reps=3):
     n_dif = -(-U // B)
     epoch = t_bpr * n_bpr + t_dif * n_dif + t_ps * n_dif
     fmt = lambda xs: "/".join(f"{x:.2f}" for x in xs)  # noqa: E731
-    return {"value": round(U / epoch, 2), "unit": "users/s", "cores": threads, "kind": "port",
+    # cores = the torch intra-op threads the port ran on (capped at 16: the GPU box's CPU share per job,
+    # whatever os.cpu_count() reports there); host_cpus = what the host reports
+    return {"value": round(U / epoch, 2), "unit": "users/s", "cores": threads, "host_cpus": os.cpu_count(),
+            "kind": "port",
             "sample": f"oracle (torch-CPU fp32 restatement), median of {reps} timed runs after a warm run: "
                       f"1 BPR+contrastive step (B=2048, fwd+bwd) = {t_bpr:.2f}s ({fmt(s_bpr)}), "
                       f"1 diffusion batch x2 denoisers = {t_dif:.2f}s ({fmt(s_dif)} per denoiser), "

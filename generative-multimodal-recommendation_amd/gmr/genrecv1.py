@@ -654,7 +654,8 @@ class FlipDiffusion:
                   stream())
         probs = probs_out if probs_out is not None else w["probs"][:B, :I]
         for j, i in enumerate(reversed(range(T))):
-            den.forward(xt, t_const=i, T=T, out=z, seed=seed, step=step * 16 + 1 + j, row0=row0, reuse_tables=j > 0)
+            den.forward(xt, t_const=i, T=T, out=z, seed=seed, step=step * 16 + 1 + j, row0=row0, reuse_tables=j > 0,
+                        keep_acts=False)
             draws = inj.get("draws")
             dr = draws[j] if draws is not None else None
             _lib.call("gmr_flip_step", B, I, ptr(z), z.stride(0), ptr(tab), T, qs - 1, int(i == 0), ptr(dr),

@@ -12,7 +12,9 @@ once per call.  Forward keeps every activation the hand-derived backward needs.
 Parameters live in one Slab under the reference's parameter names ('.' -> '_'); Q/K rows of the
 in_proj matrices and the unused `time_emb` MLP are kept (zero gradient) so state dicts line up.
 """
+import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -26,6 +28,11 @@ from .slab import Slab
 
 def _round4(n):
     return (n + 3) // 4 * 4
+
+
+# GMR_DEC_FUSED (default 1): forwards that keep no activations (the p_sample steps) run the decoder stack as
+# one launch (gmr_decoder_fwd_f32, csrc/decoder.hip) when d_model = 512 and nhead = 8; 0: layer by layer
+DEC_FUSED = os.environ.get("GMR_DEC_FUSED", "1") != "0"
 
 
 class TransformerDenoiser:
@@ -68,6 +75,19 @@ class TransformerDenoiser:
         self.layer_stride = (o["transformer_decoder_layers_1_linear1_weight"] - o["transformer_decoder_layers_0_linear1_weight"]
                              if num_layers > 1 else 0)
         self._cache = None  # (T, train_drop, keep) of the time tables / cross-attention tables held
+        # fused decoder stack (gmr_decoder_*): layer 0's slab offsets of its four weights and eleven vectors
+        self._dec_ok = D == 512 and nhead == 8
+        self._dec_planes = None
+        self._planes_ok = False
+        if self._dec_ok:
+            p0 = "transformer_decoder_layers_0_"
+            self._dec_w = (ctypes.c_int64 * 4)(o[p0 + "self_attn_in_proj_weight"] + 2 * D * D,
+                                               o[p0 + "self_attn_out_proj_weight"], o[p0 + "linear1_weight"],
+                                               o[p0 + "linear2_weight"])
+            self._dec_v = (ctypes.c_int64 * 11)(*[o[p0 + n] + (2 * D if n.endswith("in_proj_bias") else 0) for n in (
+                "self_attn_in_proj_bias", "self_attn_out_proj_bias", "norm1_weight", "norm1_bias",
+                "multihead_attn_out_proj_bias", "norm2_weight", "norm2_bias", "linear1_bias", "linear2_bias",
+                "norm3_weight", "norm3_bias")])
         self.training = True
         self._ws = None
         self._temb = None
@@ -149,27 +169,32 @@ class TransformerDenoiser:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, t_rows=None, t_const=None, T=5, out=None, masks=None, seed=None, step=0, row0=0,
-                reuse_tables=False):
+                reuse_tables=False, keep_acts=True):
         """logits = model(x, t) for x (B x I, fp32, ld % 4 == 0) and per-row t (int32 device tensor) or
         a constant t.  Train mode draws the dropout masks (Philox seed/step, keyed by the global row
         row0 + r, so a data-parallel rank draws what one process holding the whole batch draws) unless
         `masks` gives them ({'a','c','1','2','3','f'} -> uint8 (L, B, ...)); returns out (B x I).
         reuse_tables: the weights are the previous forward's (p_sample steps after the first): the time
-        tables and the cross-attention tables of the same T and mode are kept."""
+        tables and the cross-attention tables of the same T and mode are kept.  The decoder stack runs
+        fused (GMR_DEC_FUSED, d_model 512, no injected masks); keep_acts=False (no backward follows: the
+        p_sample steps) stores only its last layer's rows."""
         B = x.shape[0]
         w = self._work(B)
         D, I, L, H2 = self.D, self.I, self.L, self.H2
         train_drop = self.training and self.p > 0.0
         keep = 1.0 - self.p
-        mode = (T, train_drop, keep)
+        fused = DEC_FUSED and self._dec_ok and masks is None
+        mode = (T, train_drop, keep, fused)
         reuse = reuse_tables and self._cache == mode
+        if not reuse:
+            self._planes_ok = False  # the weights may have changed since the planes were split
         te, ste, TB, S = self._tables(T, reuse)
         self._T = T
-        if train_drop and not reuse:  # cross-attention head tables of the L layers (gmr_xattn_table_f32)
+        if (train_drop or fused) and not reuse:  # cross-attention head tables of the L layers (gmr_xattn_table_f32)
             p0 = "transformer_decoder_layers_0_"
             _lib.call("gmr_xattn_table_f32", L, D, self.nhead, ptr(self.v(p0 + "multihead_attn_out_proj_weight")),
-                      ptr(self.v(p0 + "multihead_attn_in_proj_bias")[2 * D:]), self.layer_stride, keep, ptr(w["xP"]),
-                      stream())
+                      ptr(self.v(p0 + "multihead_attn_in_proj_bias")[2 * D:]), self.layer_stride,
+                      keep if train_drop else 1.0, ptr(w["xP"]), stream())
         seed = self._seed if seed is None else seed
         win = self.v("input_proj_weight")
         h0 = w["h0"][:B]
@@ -180,7 +205,9 @@ class TransformerDenoiser:
         h = w["h"][0, :B]
         _lib.call("gmr_adaln_fwd", B, D, ptr(h0), D, ptr(t_rows), -1 if t_rows is not None else int(t_const), ptr(S),
                   2 * D, ptr(h), D, stream())
-        for l in range(L):
+        if fused:
+            h = self._decoder_fused(w, B, h, train_drop, keep, seed, step, row0, keep_acts)
+        for l in range(L if not fused else 0):
             p = f"transformer_decoder_layers_{l}_"
             wv = self.v(p + "self_attn_in_proj_weight")[2 * D:]
             bv = self.v(p + "self_attn_in_proj_bias")[2 * D:]
@@ -243,6 +270,35 @@ class TransformerDenoiser:
                bias=self.v("output_proj_3_bias"))
         self._last = (B, x, t_rows, t_const, train_drop, keep)
         self._cache = mode
+        return out
+
+    def _decoder_fused(self, w, B, h, train_drop, keep, seed, step, row0, keep_acts):
+        """The L decoder layers in one launch (gmr_decoder_fwd_f32): rows h (B x D) -> w['h'][L]; the weights'
+        bf16 planes split once per weight version, the dropout masks drawn with the layer-by-layer path's
+        keys into the same mask buffers; keep_acts: the activations the backward reads go to the same
+        workspace tensors the layer-by-layer forward fills."""
+        D, L, nh = self.D, self.L, self.nhead
+        if self._dec_planes is None:
+            self._dec_planes = torch.empty(L * 12 * D * D, dtype=torch.int16, device=self.device)
+        if not self._planes_ok:
+            _lib.call("gmr_decoder_split_f32", L, D, ptr(self.slab.data), ctypes.cast(self._dec_w, ctypes.c_void_p),
+                      self.layer_stride, ptr(self._dec_planes), stream())
+            self._planes_ok = True
+        ma, mc, m1, m2, m3, mf = (w["mask_" + k] for k in ("a", "c", "1", "2", "3", "f"))
+        if train_drop:
+            _lib.call("gmr_decoder_masks_u8", B, L, D, nh, keep, seed, step, int(row0), ptr(ma), ptr(mc), ma.stride(0),
+                      ptr(m1), ptr(m2), ptr(m3), ptr(mf), m1.stride(0), stream())
+        out = w["h"][L, :B]
+        acts = None
+        if keep_acts:
+            bufs = [w["h"], w["SAin"] if train_drop else w["V"], w["s1"], w["s2"], w["h2"], w["F1"], w["s3"], w["m1"],
+                    w["m2"], w["m3"]]
+            acts = (ctypes.c_void_p * 10)(*[t.data_ptr() for t in bufs])
+        _lib.call("gmr_decoder_fwd_f32", B, L, D, nh, ptr(h), K._ld(h), ptr(out), K._ld(out), ptr(self.slab.data),
+                  ctypes.cast(self._dec_v, ctypes.c_void_p), self.layer_stride, ptr(self._dec_planes), ptr(w["xP"]),
+                  keep, int(train_drop), ptr(ma), ptr(mc), ma.stride(0), ptr(m1), ptr(m2), ptr(m3), ptr(mf),
+                  m1.stride(0), ctypes.cast(acts, ctypes.c_void_p) if acts is not None else None, D, w["h"].stride(0),
+                  w["B"], stream())
         return out
 
     def _drop(self, x, y, site, l, masks, keep, seed, step, row0, group, ldx=None):
