@@ -578,6 +578,50 @@ __global__ void keep_mask_kernel(int64_t n, float p_keep, uint64_t seed, uint64_
   out[i] = (float)(r.x >> 8) * (1.0f / 16777216.0f) < p_keep ? 1 : 0;
 }
 
+// GenRecV1's four in-batch InfoNCE terms (genrecv1.py:389-397) through the fused contrast kernel
+// (gmr_contrast_fused_f32): each term k pairs query table i1[k] with key table i2[k] of the nv tables
+// [4][Bg][64]; a rank's queries are rows [row0, row0 + B) of the step, the keys all Bg rows.
+struct NceTerms {
+  int i1[4], i2[4];
+};
+
+// CLN_k[i] = [nv[i1_k][row0 + i] | nv[i2_k][row0 + i]]: the (query, positive) pair rows the contrast reads
+// (nv tables tab rows apart, CLN terms ct rows apart)
+__global__ void nce_pairs_kernel(int nterms, int64_t B, int64_t tab, int64_t ct, int64_t row0, NceTerms t,
+                                 const float* __restrict__ nv, float* __restrict__ cln) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (k, row, 128 columns / 4)
+  if (i >= nterms * B * 32) return;
+  const int k = (int)(i / (B * 32));
+  const int64_t r = (i / 32) % B;
+  const int c4 = (int)(i % 32) * 4;
+  const int src = c4 < 64 ? t.i1[k] : t.i2[k];
+  const float4 v = *reinterpret_cast<const float4*>(nv + ((int64_t)src * tab + row0 + r) * 64 + (c4 & 63));
+  *reinterpret_cast<float4*>(cln + ((int64_t)k * ct + r) * 128 + c4) = v;
+}
+
+// g[j][r] = the terms' gradients of nv[j][r], summed in term order: a query block's dP (contrib
+// columns 0..63) where j = i1_k, and where j = i2_k the logsumexp part dT_k[r] plus, on the rank's rows,
+// the positive part (contrib columns 64..127)
+__global__ void nce_combine_kernel(int nterms, int64_t B, int64_t Bg, int64_t tab, int64_t ct, int64_t dts,
+                                   int64_t row0, NceTerms t, const float* __restrict__ contrib,
+                                   const float* __restrict__ dT, float* __restrict__ g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (j, r, c)
+  if (i >= 4 * Bg * 64) return;
+  const int j = (int)(i / (Bg * 64));
+  const int64_t r = (i / 64) % Bg;
+  const int c = (int)(i % 64);
+  const bool mine = r >= row0 && r < row0 + B;
+  float s = 0.f;
+  for (int k = 0; k < nterms; ++k) {
+    if (t.i1[k] == j && mine) s += contrib[((int64_t)k * ct + r - row0) * 128 + c];
+    if (t.i2[k] == j) {
+      s += dT[((int64_t)k * dts + r) * 64 + c];
+      if (mine) s += contrib[((int64_t)k * ct + r - row0) * 128 + 64 + c];
+    }
+  }
+  g[((int64_t)j * tab + r) * 64 + c] = s;
+}
+
 dim3 rows16(int64_t n) { return dim3((unsigned)gmr::grid_for(n * 16, 256)); }
 
 }  // namespace
@@ -746,6 +790,41 @@ extern "C" int gmr_axpy_dev_f32(int64_t n, const float* alpha, const float* x, f
 extern "C" int gmr_mul_f32(int64_t n, const float* a, const float* b, float* out, void* stream) {
   GMR_ARG(a && b && out && n > 0, "bad args");
   hipLaunchKernelGGL(mul_flat_kernel, dim3(gmr::grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, a, b, out);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_nce_pairs_f32(int32_t nterms, int64_t B, int64_t Bg, int64_t row0, const int32_t* i1,
+                                 const int32_t* i2, const float* nv, int64_t tab, float* cln, int64_t ct, void* stream) {
+  GMR_ARG(nv && cln && i1 && i2 && nterms > 0 && nterms <= 4 && B > 0 && Bg >= B && row0 >= 0 && row0 + B <= Bg &&
+              tab >= Bg && ct >= B,
+          "bad args");
+  NceTerms t{};
+  for (int k = 0; k < nterms; ++k) {
+    GMR_ARG(i1[k] >= 0 && i1[k] < 4 && i2[k] >= 0 && i2[k] < 4, "term tables index the 4 nv tables");
+    t.i1[k] = i1[k];
+    t.i2[k] = i2[k];
+  }
+  hipLaunchKernelGGL(nce_pairs_kernel, dim3(gmr::grid_for((int64_t)nterms * B * 32, 256)), dim3(256), 0,
+                     (hipStream_t)stream, nterms, B, tab, ct, row0, t, nv, cln);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_nce_combine_f32(int32_t nterms, int64_t B, int64_t Bg, int64_t row0, const int32_t* i1,
+                                   const int32_t* i2, const float* contrib, int64_t ct, const float* dT, int64_t dts,
+                                   float* g, int64_t tab, void* stream) {
+  GMR_ARG(contrib && dT && g && i1 && i2 && nterms > 0 && nterms <= 4 && B > 0 && Bg >= B && row0 >= 0 &&
+              row0 + B <= Bg && ct >= B && dts >= Bg && tab >= Bg,
+          "bad args");
+  NceTerms t{};
+  for (int k = 0; k < nterms; ++k) {
+    GMR_ARG(i1[k] >= 0 && i1[k] < 4 && i2[k] >= 0 && i2[k] < 4, "term tables index the 4 nv tables");
+    t.i1[k] = i1[k];
+    t.i2[k] = i2[k];
+  }
+  hipLaunchKernelGGL(nce_combine_kernel, dim3(gmr::grid_for(4 * Bg * 64, 256)), dim3(256), 0, (hipStream_t)stream,
+                     nterms, B, Bg, tab, ct, dts, row0, t, contrib, dT, g);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -166,6 +166,8 @@ SIGNATURES = {
     "gmr_xattn_bwd_workspace_floats": (I64, [I64, I32, I32]),
     "gmr_xattn_bwd_f32": (I32, [I64, I32, I32, P, I64, P, I64, P, P, F32, P, P, P, I64, P]),
     "gmr_decoder_split_f32": (I32, [I32, I32, P, P, I64, P, P]),
+    "gmr_nce_pairs_f32": (I32, [I32, I64, I64, I64, P, P, P, I64, P, I64, P]),
+    "gmr_nce_combine_f32": (I32, [I32, I64, I64, I64, P, P, P, I64, P, I64, P, I64, P]),
     "gmr_decoder_masks_u8": (I32, [I64, I32, I32, I32, F32, U64, U64, I64, P, P, I64, P, P, P, P, I64, P]),
     "gmr_decoder_fwd_f32": (I32, [I64, I32, I32, I32, P, I64, P, I64, P, P, I64, P, P, F32, I32, P, P, I64, P, P, P, P,
                                   I64, P, I64, I64, I64, P]),

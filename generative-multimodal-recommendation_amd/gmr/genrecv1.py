@@ -15,6 +15,8 @@ Layout in HBM (N = U + I, d = 64): one rec slab [E0 = user_embedding; item_id_em
 every other rec parameter under its reference name], the denoiser slab, N x 64 activation tables.
 BatchNorm running statistics are kept per module and updated in the reference's call order.
 """
+import ctypes
+import os
 import numpy as np
 import torch
 import torch.nn as nn
@@ -27,6 +29,10 @@ from .kernels import ptr, stream
 from .kmeans import kmeans_labels
 from .slab import Slab
 from .transformer import TransformerDenoiser
+
+# GMR_NCE_FUSED (default 1): the four in-batch InfoNCE terms of the rec step through the fused contrast kernel
+# (gmr_contrast_fused_f32 + gmr_nce_pairs / _combine); 0: logits GEMM + row softmax + two gradient GEMMs per term
+NCE_FUSED = os.environ.get("GMR_NCE_FUSED", "1") != "0"
 
 BN_NAMES = ["image_residual_project_1", "image_modal_project_1", "text_residual_project_1",
             "text_modal_project_1", "caculate_common_1", "gate_image_modal_1", "gate_text_modal_1",
@@ -344,6 +350,31 @@ class GenRecV1(GeneralRecommender):
         K.gemm(L, v2, w["g"][i1][row0:row0 + B], alpha=inv_t, beta=1.0)
         K.gemm(L, v1, w["g"][i2][:Bg], trans_a=True, alpha=inv_t, beta=1.0)
 
+    def _nce_fused(self, w, terms, nr, loss, row0, B, Bg):
+        """The four in-batch InfoNCE terms through the fused contrast kernel (gmr_contrast_fused_f32: no B x Bg
+        logit block, no GEMM launches): pair rows, one contrast call per term, then every nv row's
+        gradient in one combine pass (w['g'] overwritten)."""
+        nv, g = w["nv"], w["g"]
+        tab = nv.stride(0) // 64
+        if "nce_cln" not in w:
+            Bm = w["B"]
+            f = lambda *sh: torch.empty(sh, dtype=torch.float32, device=self.device)  # noqa: E731
+            w["nce_cln"], w["nce_ctr"], w["nce_dt"] = f(4, Bm, 128), f(4, Bm, 128), f(4, Bm, 64)
+            w["nce_nodes"] = torch.arange(Bm, dtype=torch.int32, device=self.device)
+            self._nce_i1 = (ctypes.c_int32 * 4)(*[t[0] for t in terms])
+            self._nce_i2 = (ctypes.c_int32 * 4)(*[t[1] for t in terms])
+        cln, ctr, dt = w["nce_cln"], w["nce_ctr"], w["nce_dt"]
+        i1p, i2p = ctypes.cast(self._nce_i1, ctypes.c_void_p), ctypes.cast(self._nce_i2, ctypes.c_void_p)
+        _lib.call("gmr_nce_pairs_f32", 4, B, Bg, row0, i1p, i2p, ptr(nv), tab, ptr(cln), cln.stride(0) // 128, stream())
+        ws = K.contrast_workspace(B, Bg, self.device, "gr_nce")
+        for k, (i1, i2, reg) in enumerate(terms):
+            rows = w["rows"][k][:B]
+            K.contrast_fused(nv[i1][row0:row0 + B], nv[i2][:Bg], cln[k], w["nce_nodes"][:B], 0, 1.0 / self.temp,
+                             reg / nr, rows, ctr[k][:B], dt[k][:Bg], ws)
+            _lib.call("gmr_sum_f32", B, ptr(rows), reg / nr, ptr(loss), 1, stream())
+        _lib.call("gmr_nce_combine_f32", 4, B, Bg, row0, i1p, i2p, ptr(ctr), ctr.stride(0) // 128, ptr(dt),
+                  dt.stride(0) // 64, ptr(g), tab, stream())
+
     def rec_step(self, users, pos, neg, plan_bpr=None, plan_cl=None, norm_rows=None, reg_share=1.0, masks=None,
                  gbatch=None):
         """calculate_loss (:355-405) and all rec-parameter gradients (into rec_slab.grad).
@@ -379,12 +410,15 @@ class GenRecV1(GeneralRecommender):
         for j, (src, idx, off) in enumerate(((C, gu, 0), (C, gp, U), (SIDE, gu, 0), (SIDE, gp, U))):
             K.gather_rows(src, idx, w["raw"][j][:Bg], off=off)
             K.normalize_rows(w["raw"][j][:Bg], w["nv"][j][:Bg], w["nrm"][j][:Bg])
-        K.zero_(w["g"])
-        for k, (i1, i2, reg) in enumerate(((3, 1, self.ssl_reg1), (2, 0, self.ssl_reg1),
-                                           (0, 1, self.ssl_reg2), (0, 3, self.ssl_reg2))):
-            rows = w["rows"][k][:B]
-            self._nce(w, i1, i2, reg / nr, rows, row0, B, Bg)
-            _lib.call("gmr_sum_f32", B, ptr(rows), reg / nr, ptr(loss), 1, stream())
+        terms = ((3, 1, self.ssl_reg1), (2, 0, self.ssl_reg1), (0, 1, self.ssl_reg2), (0, 3, self.ssl_reg2))
+        if NCE_FUSED:
+            self._nce_fused(w, terms, nr, loss, row0, B, Bg)
+        else:
+            K.zero_(w["g"])
+            for k, (i1, i2, reg) in enumerate(terms):
+                rows = w["rows"][k][:B]
+                self._nce(w, i1, i2, reg / nr, rows, row0, B, Bg)
+                _lib.call("gmr_sum_f32", B, ptr(rows), reg / nr, ptr(loss), 1, stream())
         dC, dS = w["dC"], w["dS"]
         K.zero_(dC)
         K.zero_(dS)

@@ -489,6 +489,17 @@ int gmr_nce_rows_f32(int64_t B, float* L, int64_t ld, float coef, float* loss, v
 /* the same for a data-parallel rank's block: rows [diag_off, diag_off + rows) of the global batch
  * against all cols keys (row r's positive at column diag_off + r; genrecv1.py:407-414 over the
  * global batch) */
+/* GenRecV1's in-batch InfoNCE terms through gmr_contrast_fused_f32 (round 4; genrecv1.py:389-397): term k
+ * pairs the normalised query table i1[k] with key table i2[k] of nv [4][tab][64] (i1 / i2: host arrays of
+ * nterms <= 4 entries; Bg rows used per table).  gmr_nce_pairs_f32 writes the (query, positive) pair rows
+ * CLN [nterms][ct][128] of the rank's rows [row0, row0 + B); after one contrast call per term (contrib
+ * [nterms][ct][128], dT [nterms][dts][64]) gmr_nce_combine_f32 writes every nv row's gradient g [4][tab][64],
+ * summed in term order. */
+int gmr_nce_pairs_f32(int32_t nterms, int64_t B, int64_t Bg, int64_t row0, const int32_t* i1, const int32_t* i2,
+                      const float* nv, int64_t tab, float* cln, int64_t ct, void* stream);
+int gmr_nce_combine_f32(int32_t nterms, int64_t B, int64_t Bg, int64_t row0, const int32_t* i1, const int32_t* i2,
+                        const float* contrib, int64_t ct, const float* dT, int64_t dts, float* g, int64_t tab,
+                        void* stream);
 int gmr_nce_rows_off_f32(int64_t rows, int64_t cols, float* L, int64_t ld, int64_t diag_off, float coef, float* loss,
                          void* stream);
 /* BPR with log-sigmoid (:377-380) over one (U + I) x 64 table; contrib = [dU; dP; dN] */
