@@ -255,7 +255,7 @@ class GenRecV1(GeneralRecommender):
              "nv": f(4, B, 64), "nrm": f(4, B), "raw": f(4, B, 64), "L": f(B, Bp), "rows": f(4, B), "loss": f(4),
              # backward
              "dC": f(N, 64), "dS": f(N, 64), "dM": f(2, N, 64), "da": f(2, N), "dPG": f(2, N, 64),
-             "dZ": f(N, 64), "T1": f(N, 64), "T2": f(N, 64), "dP": f(I, 64), "dF": f(I, 64), "dX": f(I, 64),
+             "dZ": f(N, 64), "dZ2": f(2, N, 64), "T1": f(N, 64), "T2": f(N, 64), "dP": f(I, 64), "dF": f(I, 64), "dX": f(I, 64),
              "dZi": f(I, 64)}
         self._w = w
         return w
@@ -326,8 +326,9 @@ class GenRecV1(GeneralRecommender):
             ii.spmm(MOD[U:], [(w["Pm"][m],)])                 # item_item_GCN (n_layers = 1)
             self.R.spmm(MOD[:U], [(MOD[U:],)])                 # users <- R @ items
         wc2 = self.P("caculate_common_3_weight").view(64)
+        # caculate_common's Linear on both modality tables in one product (the same weight: 2N stacked rows)
+        self._linear(w["MOD"].view(2 * N, 64), "caculate_common_0", w["Zc"].view(2 * N, 64))
         for m in range(2):
-            self._linear(w["MOD"][m], "caculate_common_0", w["Zc"][m])
             self._bn(w, 6 + m, w["Zc"][m], N, ACT_TANH, train, post=POST_ROWDOT, aux=wc2, rowdot=w["a"][m])
         for m, gate in enumerate(("gate_image_modal", "gate_text_modal")):
             self._linear(w["C"], gate + "_0", w["Zp"][m])
@@ -492,9 +493,11 @@ class GenRecV1(GeneralRecommender):
             self._bn_bwd(w, 8 + m, w["Zp"][m], N, ACT_SIGMOID, dy=w["dPG"][m], dz=dZ)
             self._linear_bwd(dZ, w["C"], gate + "_0", dx=dC, dx_beta=1.0)
         # attention scores (caculate_common on IMG / TXT, :313-323)
+        dZ2 = w["dZ2"]
         for m in range(2):
-            self._bn_bwd(w, 6 + m, w["Zc"][m], N, ACT_TANH, da=w["da"][m], dz=dZ)
-            self._linear_bwd(dZ, w["MOD"][m], "caculate_common_0", dx=dM[m], dx_beta=1.0)
+            self._bn_bwd(w, 6 + m, w["Zc"][m], N, ACT_TANH, da=w["da"][m], dz=dZ2[m])
+        self._linear_bwd(dZ2.view(2 * N, 64), w["MOD"].view(2 * N, 64), "caculate_common_0", dx=dM.view(2 * N, 64),
+                         dx_beta=1.0)
         # item_item_GCN branches (:266-306)
         for m, (mod, gate) in enumerate((("image", "gate_image_modal"), ("text", "gate_text_modal"))):
             d = dM[m]
