@@ -473,6 +473,52 @@ __global__ void __launch_bounds__(1024) kpp_pick_kernel(int64_t n, const float* 
   }
 }
 
+// greedy k-means++ step (sklearn's _kmeans_plusplus with n_local_trials candidates, KMeans' default seeding):
+// the potential sum_r min(mind[r], |x_r - c_t|^2) of each candidate t (dots = X . Cc^T, fixed-order sums),
+// the candidate of the lowest potential (ties -> lowest t) becomes center j and updates mind
+__global__ void __launch_bounds__(1024) kpp_greedy_kernel(int64_t n, int L, const float* __restrict__ xsq,
+                                                          const float* __restrict__ dots, int64_t ldd,
+                                                          const float* __restrict__ ccsq, float* __restrict__ mind,
+                                                          const float* __restrict__ Cc, int64_t ldcc, int d,
+                                                          float* __restrict__ C, int64_t ldc, int j,
+                                                          float* __restrict__ csq) {
+  __shared__ double part[1024];
+  __shared__ double pot[16];
+  __shared__ int best_s;
+  const int t0 = threadIdx.x;
+  const int64_t chunk = (n + 1023) / 1024;
+  const int64_t r0 = t0 * chunk, r1 = r0 + chunk < n ? r0 + chunk : n;
+  for (int t = 0; t < L; ++t) {
+    double s = 0.0;
+    for (int64_t r = r0; r < r1; ++r) {
+      const float dd = fmaxf(xsq[r] - 2.f * dots[r * ldd + t] + ccsq[t], 0.f);
+      s += (double)fminf(mind[r], dd);
+    }
+    part[t0] = s;
+    __syncthreads();
+    if (t0 == 0) {
+      double tot = 0.0;
+      for (int i = 0; i < 1024; ++i) tot += part[i];
+      pot[t] = tot;
+    }
+    __syncthreads();
+  }
+  if (t0 == 0) {
+    int b = 0;
+    for (int t = 1; t < L; ++t)
+      if (pot[t] < pot[b]) b = t;
+    best_s = b;
+  }
+  __syncthreads();
+  const int b = best_s;
+  for (int64_t r = t0; r < n; r += 1024) {
+    const float dd = fmaxf(xsq[r] - 2.f * dots[r * ldd + b] + ccsq[b], 0.f);
+    mind[r] = fminf(mind[r], dd);
+  }
+  for (int c = t0; c < d; c += 1024) C[(int64_t)j * ldc + c] = Cc[(int64_t)b * ldcc + c];
+  if (t0 == 0) csq[j] = ccsq[b];
+}
+
 __global__ void copy_row_kernel(int d, const float* __restrict__ X, int64_t ldx, const int* __restrict__ idx,
                                 float* __restrict__ C, int64_t ldc, int j, const float* __restrict__ xsq,
                                 float* __restrict__ csq) {
@@ -662,6 +708,17 @@ extern "C" int gmr_kmeans_pp_pick(int64_t n, const float* mind, uint64_t seed, u
                                   void* stream) {
   GMR_ARG(out && n > 0, "bad args");
   hipLaunchKernelGGL(kpp_pick_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, n, mind, seed, step, out);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_kmeans_pp_greedy(int64_t n, int32_t L, const float* xsq, const float* dots, int64_t ldd,
+                                    const float* ccsq, float* mind, const float* Cc, int64_t ldcc, int32_t d, float* C,
+                                    int64_t ldc, int32_t j, float* csq, void* stream) {
+  GMR_ARG(xsq && dots && ccsq && mind && Cc && C && csq && n > 0 && L >= 1 && L <= 16 && d > 0 && j >= 0 && ldd >= L,
+          "bad args");
+  hipLaunchKernelGGL(kpp_greedy_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, n, L, xsq, dots, ldd, ccsq, mind,
+                     Cc, ldcc, d, C, ldc, j, csq);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -549,6 +549,13 @@ int gmr_kmeans_standardize(int64_t n, int32_t d, const float* X, int64_t ldx, fl
 int gmr_kmeans_pp_pick(int64_t n, const float* mind, uint64_t seed, uint64_t step, int32_t* out, void* stream);
 int gmr_kmeans_take_center(int32_t d, const float* X, int64_t ldx, const int32_t* idx, float* C, int64_t ldc,
                            int32_t j, const float* xsq, float* csq, void* stream);
+/* greedy k-means++ step (sklearn's default seeding: L = 2 + floor(ln k) candidates, round 4): given dots =
+ * X . Cc^T (n x L) of the candidate rows Cc and their squared norms ccsq, picks the candidate of the lowest
+ * potential sum_r min(mind[r], |x_r - c|^2) (fixed-order sums, ties -> lowest), copies it to C[j], sets
+ * csq[j] and lowers mind. */
+int gmr_kmeans_pp_greedy(int64_t n, int32_t L, const float* xsq, const float* dots, int64_t ldd, const float* ccsq,
+                         float* mind, const float* Cc, int64_t ldcc, int32_t d, float* C, int64_t ldc, int32_t j,
+                         float* csq, void* stream);
 int gmr_kmeans_min_dist(int64_t n, const float* xsq, const float* dots, const float* csq, int32_t j, float* mind,
                         int32_t first, void* stream);
 int64_t gmr_kmeans_parts(int64_t n);
