@@ -435,10 +435,11 @@ __global__ void standardize_kernel(int64_t n, int d, const float* __restrict__ X
 
 // squared distance of every point to centroid j (given the point norms and the dot column)
 __global__ void min_dist_update_kernel(int64_t n, const float* __restrict__ xsq, const float* __restrict__ dots,
-                                       const float* __restrict__ csq, int j, float* __restrict__ mind, int first) {
+                                       int64_t ldd, const float* __restrict__ csq, int j, float* __restrict__ mind,
+                                       int first) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
-  const float d = fmaxf(xsq[r] - 2.f * dots[r] + csq[j], 0.f);
+  const float d = fmaxf(xsq[r] - 2.f * dots[r * ldd] + csq[j], 0.f);
   mind[r] = first ? d : fminf(mind[r], d);
 }
 
@@ -731,11 +732,11 @@ extern "C" int gmr_kmeans_take_center(int32_t d, const float* X, int64_t ldx, co
   return GMR_OK;
 }
 
-extern "C" int gmr_kmeans_min_dist(int64_t n, const float* xsq, const float* dots, const float* csq, int32_t j,
-                                   float* mind, int32_t first, void* stream) {
-  GMR_ARG(xsq && dots && csq && mind && n > 0 && j >= 0, "bad args");
+extern "C" int gmr_kmeans_min_dist(int64_t n, const float* xsq, const float* dots, int64_t ld_dots, const float* csq,
+                                   int32_t j, float* mind, int32_t first, void* stream) {
+  GMR_ARG(xsq && dots && csq && mind && n > 0 && j >= 0 && ld_dots >= 1, "bad args");
   hipLaunchKernelGGL(min_dist_update_kernel, dim3(gmr::grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, xsq,
-                     dots, csq, (int)j, mind, first);
+                     dots, ld_dots, csq, (int)j, mind, first);
   GMR_LAUNCHED();
   return GMR_OK;
 }

@@ -144,7 +144,7 @@ SIGNATURES = {
     "gmr_kmeans_standardize": (I32, [I64, I32, P, I64, P, P, P, I64, P, P]),
     "gmr_kmeans_pp_pick": (I32, [I64, P, U64, U64, P, P]),
     "gmr_kmeans_take_center": (I32, [I32, P, I64, P, P, I64, I32, P, P, P]),
-    "gmr_kmeans_min_dist": (I32, [I64, P, P, P, I32, P, I32, P]),
+    "gmr_kmeans_min_dist": (I32, [I64, P, P, I64, P, I32, P, I32, P]),
     "gmr_kmeans_pp_greedy": (I32, [I64, I32, P, P, I64, P, P, P, I64, I32, P, I64, I32, P, P]),
     "gmr_kmeans_parts": (I64, [I64]),
     "gmr_kmeans_assign": (I32, [I64, I32, P, I64, P, P, P, P, I64, P, P, P]),

@@ -44,7 +44,7 @@ def kmeans_labels(X, k, seed=0, max_iter=300):
     _lib.call("gmr_kmeans_pp_pick", n, None, seed, 0, ptr(pick), stream())
     _lib.call("gmr_kmeans_take_center", d, ptr(Y), ld, ptr(pick), ptr(C), ld, 0, ptr(xsq), ptr(csq), stream())
     K.gemm(Y, C[0:1], dots, trans_b=True)
-    _lib.call("gmr_kmeans_min_dist", n, ptr(xsq), ptr(dots), ptr(csq), 0, ptr(mind), 1, stream())
+    _lib.call("gmr_kmeans_min_dist", n, ptr(xsq), ptr(dots), K._ld(dots), ptr(csq), 0, ptr(mind), 1, stream())
     for j in range(1, k):
         for t in range(L):
             _lib.call("gmr_kmeans_pp_pick", n, ptr(mind), seed, 1024 + 16 * j + t, ptr(cand[t:t + 1]), stream())

@@ -556,8 +556,8 @@ int gmr_kmeans_take_center(int32_t d, const float* X, int64_t ldx, const int32_t
 int gmr_kmeans_pp_greedy(int64_t n, int32_t L, const float* xsq, const float* dots, int64_t ldd, const float* ccsq,
                          float* mind, const float* Cc, int64_t ldcc, int32_t d, float* C, int64_t ldc, int32_t j,
                          float* csq, void* stream);
-int gmr_kmeans_min_dist(int64_t n, const float* xsq, const float* dots, const float* csq, int32_t j, float* mind,
-                        int32_t first, void* stream);
+int gmr_kmeans_min_dist(int64_t n, const float* xsq, const float* dots, int64_t ld_dots, const float* csq, int32_t j,
+                        float* mind, int32_t first, void* stream);
 int64_t gmr_kmeans_parts(int64_t n);
 int gmr_kmeans_assign(int64_t n, int32_t k, const float* dots, int64_t ldd, const float* csq, const float* xsq,
                       int32_t* label, float* onehot_t, int64_t ldo, int32_t* changed, double* inertia_parts,
