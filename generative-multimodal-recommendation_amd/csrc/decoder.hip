@@ -8,7 +8,8 @@
 //                                                                   eval: every head kept, P without 1/p)
 //   F1   = drop_f(relu(h2 W1^T + b1))
 //   h'   = LN3(h2 + drop3(F1 W2^T + b2))
-// The unfused path runs this as 4 GEMM launches + 6 row kernels per layer.  Here a workgroup owns 16 rows
+// The unfused path runs this as 4 GEMM launches + 6 row kernels per layer.  Here a workgroup owns 32 rows
+// (16 with GMR_DEC_ROWS=16)
 // and carries them through all L layers in LDS: the four products per layer run on the bf16 matrix
 // cores from exact three-way splits (the six products of gemm_x6.hip, fp32-accurate sums; the weights
 // arrive pre-split as bf16 planes, gmr_decoder_split_f32, the activations are split in registers at
@@ -30,7 +31,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kDD = 512;        // d_model
 constexpr int kNH = 8;          // heads (64 columns each)
-constexpr int kDR = 16;         // rows per workgroup
 constexpr int kDW = 8;          // waves per workgroup: wave w owns columns [64 w, 64 w + 64)
 constexpr int kDLd = kDD + 4;   // LDS row stride (floats): the 16 rows of a fragment read hit distinct banks
 constexpr int64_t kPlane = (int64_t)kDD * kDD;
@@ -73,11 +73,13 @@ __device__ __forceinline__ f32x4 dec_mfma6(const bf16x8 (&a)[3], const bf16x8 (&
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
 }
 
-// acc[t] = A (16 x 512, LDS) . W^T for the wave's four 16-column tiles (columns 64 w + 16 t + (lane & 15)).
-// Fragments of v_mfma_f32_16x16x32_bf16: lane l holds A[l & 15][k0 + 8 (l >> 4) + j] and W[n][same k];
-// the result element e of lane l is row 4 (l >> 4) + e, column l & 15 of the tile.
-__device__ __forceinline__ void dec_gemm(const float* A, const __bf16* __restrict__ Wm, f32x4 (&acc)[4], int w,
+// acc[rt][t] = A (32 x 512, LDS) . W^T for the wave's four 16-column tiles (columns 64 w + 16 t + (lane & 15))
+// and both 16-row tiles rt.  Fragments of v_mfma_f32_16x16x32_bf16: lane l holds A[16 rt + (l & 15)][k0 + 8 (l >> 4)
+// + j] and W[n][same k]; result element e of lane l is row 16 rt + 4 (l >> 4) + e, column l & 15 of the tile.
+template <int kDR>
+__device__ __forceinline__ void dec_gemm(const float* A, const __bf16* __restrict__ Wm, f32x4 (&acc)[kDR / 16][4], int w,
                                          int lane) {
+  constexpr int kRT = kDR / 16;
   const int row = lane & 15, g = lane >> 4;
   const __bf16* wb = Wm + (int64_t)(64 * w + row) * kDD + 8 * g;
   auto load = [&](bf16x8 (&b)[4][3], int k0) {
@@ -87,16 +89,21 @@ __device__ __forceinline__ void dec_gemm(const float* A, const __bf16* __restric
       for (int p = 0; p < 3; ++p) b[t][p] = *reinterpret_cast<const bf16x8*>(wb + p * kPlane + t * 16 * kDD + k0);
   };
   auto step = [&](const bf16x8 (&b)[4][3], int k0) {
-    const float* ap = A + row * kDLd + k0 + 8 * g;
-    const float4 x0 = *reinterpret_cast<const float4*>(ap), x1 = *reinterpret_cast<const float4*>(ap + 4);
-    const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-    bf16x8 a[3];
-    dec_split8(v, a);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = dec_mfma6(a, b[t], acc[t]);
+    for (int rt = 0; rt < kRT; ++rt) {
+      const float* ap = A + (16 * rt + row) * kDLd + k0 + 8 * g;
+      const float4 x0 = *reinterpret_cast<const float4*>(ap), x1 = *reinterpret_cast<const float4*>(ap + 4);
+      const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      bf16x8 a[3];
+      dec_split8(v, a);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[rt][t] = dec_mfma6(a, b[t], acc[rt][t]);
+    }
   };
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int rt = 0; rt < kRT; ++rt)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 b0[4][3], b1[4][3];
   load(b0, 0);
 #pragma unroll 1
@@ -108,15 +115,15 @@ __device__ __forceinline__ void dec_gemm(const float* A, const __bf16* __restric
   }
 }
 
-// LayerNorm of the 16 rows of S into X (two rows per wave; lane holds columns j * 64 + lane, summed in j
+// LayerNorm of the 32 rows of S into X (four rows per wave; lane holds columns j * 64 + lane, summed in j
 // order: ln_fwd_kernel's arithmetic), eps 1e-5
-template <bool STORE>
+template <int kDR, bool STORE>
 __device__ __forceinline__ void dec_ln(const float* S, float* X, const float* __restrict__ wt, const float* __restrict__ bs,
                                        int w, int lane, int64_t r0, int64_t B, float* __restrict__ gx,
                                        float* __restrict__ st, int64_t ab) {
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int r = 2 * w + q;
+  for (int q = 0; q < kDR / kDW; ++q) {
+    const int r = (kDR / kDW) * w + q;
     float v[8];
     float sum = 0.f;
 #pragma unroll
@@ -146,7 +153,8 @@ __device__ __forceinline__ void dec_ln(const float* S, float* X, const float* __
   }
 }
 
-// the 16 rows of an LDS matrix -> rows r0.. of a [Bmax][D] activation buffer (rows < B)
+// the 32 rows of an LDS matrix -> rows r0.. of a [Bmax][D] activation buffer (rows < B)
+template <int kDR>
 __device__ __forceinline__ void dec_store(const float* S, float* __restrict__ g, int64_t r0, int64_t B) {
   for (int i = threadIdx.x; i < kDR * kDD / 4; i += 64 * kDW) {
     const int r = i / (kDD / 4), c4 = (i % (kDD / 4)) * 4;
@@ -154,13 +162,15 @@ __device__ __forceinline__ void dec_store(const float* S, float* __restrict__ g,
   }
 }
 
-template <bool STORE>
+template <int kDR, bool STORE>
 __global__ void __launch_bounds__(64 * kDW, 1) decoder_fwd_kernel(int64_t B, int L, const float* __restrict__ h0,
                                                                   int64_t ld0, float* __restrict__ out, int64_t ldo,
                                                                   DecArgs p, float keep, int train) {
-  __shared__ __attribute__((aligned(16))) float X[kDR * kDLd];  // h, h1, h2 (the residual stream)
-  __shared__ __attribute__((aligned(16))) float Y[kDR * kDLd];  // SAin, F1 (the second products' A operand)
-  __shared__ __attribute__((aligned(16))) float Z[kDR * kDLd];  // pre-LayerNorm sums
+  // X: the residual stream h, h1, h2; Y: the second products' A operand (SAin, F1) and, after a product has
+  // read it, the pre-LayerNorm sums s1, s2, s3
+  __shared__ __attribute__((aligned(16))) float X[kDR * kDLd];
+  __shared__ __attribute__((aligned(16))) float Y[kDR * kDLd];
+  constexpr int kRT = kDR / 16;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int64_t r0 = (int64_t)blockIdx.x * kDR;
   for (int i = tid; i < kDR * kDD / 4; i += 64 * kDW) {
@@ -173,10 +183,23 @@ __global__ void __launch_bounds__(64 * kDW, 1) decoder_fwd_kernel(int64_t B, int
   const float inv_keep = 1.f / keep;
   const int g = lane >> 4, cl = lane & 15;
   // the lane's output rows (clamped for the masks of a ragged last block: those rows are never stored)
-  int64_t rg[4];
+  int rg[kRT][4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) rg[e] = min(r0 + 4 * g + e, B - 1);
-  f32x4 acc[4];
+  for (int rt = 0; rt < kRT; ++rt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rg[rt][e] = (int)min(r0 + 16 * rt + 4 * g + e, B - 1);
+  f32x4 acc[kRT][4];
+  // epilogue over the wave's fragment elements: f(row in block, global row for masks, column, value)
+  auto epi = [&](auto&& f) {
+#pragma unroll
+    for (int rt = 0; rt < kRT; ++rt)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int c = 64 * w + 16 * t + cl;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f(16 * rt + 4 * g + e, rg[rt][e], c, acc[rt][t][e]);
+      }
+  };
   for (int l = 0; l < L; ++l) {
     const float* P = p.slab + (int64_t)l * p.lstride;
     const __bf16* Wl = p.W + (int64_t)l * 12 * kPlane;
@@ -185,101 +208,81 @@ __global__ void __launch_bounds__(64 * kDW, 1) decoder_fwd_kernel(int64_t B, int
     const uint8_t* mf = p.mf + l * p.msd;
     const uint8_t* m3 = p.m3 + l * p.msd;
     // 1. SAin = dropout_head(h Wv^T + bv) -> Y   (wave w's 64 columns are head w)
-    dec_gemm(X, Wl, acc, w, lane);
+    dec_gemm<kDR>(X, Wl, acc, w, lane);
     {
       const float* bv = P + p.off[O_BV];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int c = 64 * w + 16 * t + cl;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = acc[t][e] + bv[c];
-          if (train) v = ma[rg[e] * kNH + w] ? v / keep : 0.f;
-          Y[(4 * g + e) * kDLd + c] = v;
-        }
-      }
+      epi([&](int r, int rr, int c, float a) {
+        float v = a + bv[c];
+        if (train) v = ma[rr * kNH + w] ? v / keep : 0.f;
+        Y[r * kDLd + c] = v;
+      });
     }
     __syncthreads();
-    if (STORE) dec_store(Y, p.sa + l * p.asd, r0, B);
-    // 2. s1 = h + drop1(SAin Wo^T + bo) -> Z
-    dec_gemm(Y, Wl + 3 * kPlane, acc, w, lane);
+    if (STORE) dec_store<kDR>(Y, p.sa + l * p.asd, r0, B);
+    // 2. s1 = h + drop1(SAin Wo^T + bo) -> Y (once every wave has read SAin)
+    dec_gemm<kDR>(Y, Wl + 3 * kPlane, acc, w, lane);
+    __syncthreads();
     {
       const float* bo = P + p.off[O_BO];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int c = 64 * w + 16 * t + cl;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = acc[t][e] + bo[c];
-          if (train) v = m1[rg[e] * kDD + c] ? v * inv_keep : 0.f;
-          const int o = (4 * g + e) * kDLd + c;
-          Z[o] = X[o] + v;
-        }
-      }
+      epi([&](int r, int rr, int c, float a) {
+        float v = a + bo[c];
+        if (train) v = m1[rr * kDD + c] ? v * inv_keep : 0.f;
+        Y[r * kDLd + c] = X[r * kDLd + c] + v;
+      });
     }
     __syncthreads();
-    if (STORE) dec_store(Z, p.s1 + l * p.asd, r0, B);
-    dec_ln<STORE>(Z, X, P + p.off[O_N1W], P + p.off[O_N1B], w, lane, r0, B, nullptr, p.st1 + l * p.ast, p.ab);  // h1
+    if (STORE) dec_store<kDR>(Y, p.s1 + l * p.asd, r0, B);
+    dec_ln<kDR, STORE>(Y, X, P + p.off[O_N1W], P + p.off[O_N1B], w, lane, r0, B, nullptr, p.st1 + l * p.ast, p.ab);  // h1
     __syncthreads();
-    // 3. s2 = h1 + drop2(CA) -> Z, CA = b_o' + sum_h keep_c[h] P[h] (eval: all heads, no drop)
+    // 3. s2 = h1 + drop2(CA) -> Y, CA = b_o' + sum_h keep_c[h] P[h] (eval: all heads, no drop)
     {
       const float* boc = P + p.off[O_BOC];
       const uint8_t* mc = p.mc + l * p.msh;
       const uint8_t* m2 = p.m2 + l * p.msd;
+      const float* xp = p.xP + (int64_t)l * kNH * kDD;
       for (int i = tid; i < kDR * kDD; i += 64 * kDW) {
         const int r = i / kDD, c = i % kDD;
         const int64_t rr = min(r0 + r, B - 1);
-        const float* xp = p.xP + (int64_t)l * kNH * kDD;
         float s = 0.f;
 #pragma unroll
         for (int h = 0; h < kNH; ++h)
           if (!train || mc[rr * kNH + h]) s += xp[h * kDD + c];
         float ca = s + boc[c];
         if (train) ca = m2[rr * kDD + c] ? ca * inv_keep : 0.f;
-        Z[r * kDLd + c] = X[r * kDLd + c] + ca;
+        Y[r * kDLd + c] = X[r * kDLd + c] + ca;
       }
     }
     __syncthreads();
-    if (STORE) dec_store(Z, p.s2 + l * p.asd, r0, B);
-    dec_ln<STORE>(Z, X, P + p.off[O_N2W], P + p.off[O_N2B], w, lane, r0, B, STORE ? p.h2 + l * p.asd : nullptr,
+    if (STORE) dec_store<kDR>(Y, p.s2 + l * p.asd, r0, B);
+    dec_ln<kDR, STORE>(Y, X, P + p.off[O_N2W], P + p.off[O_N2B], w, lane, r0, B, STORE ? p.h2 + l * p.asd : nullptr,
                   p.st2 + l * p.ast, p.ab);  // h2
     __syncthreads();
     // 4. F1 = drop_f(relu(h2 W1^T + b1)) -> Y
-    dec_gemm(X, Wl + 6 * kPlane, acc, w, lane);
+    dec_gemm<kDR>(X, Wl + 6 * kPlane, acc, w, lane);
     {
       const float* b1 = P + p.off[O_B1];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int c = 64 * w + 16 * t + cl;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = fmaxf(acc[t][e] + b1[c], 0.f);
-          if (train) v = mf[rg[e] * kDD + c] ? v / keep : 0.f;
-          Y[(4 * g + e) * kDLd + c] = v;
-        }
-      }
+      epi([&](int r, int rr, int c, float a) {
+        float v = fmaxf(a + b1[c], 0.f);
+        if (train) v = mf[rr * kDD + c] ? v / keep : 0.f;
+        Y[r * kDLd + c] = v;
+      });
     }
     __syncthreads();
-    if (STORE) dec_store(Y, p.f1 + l * p.asd, r0, B);
-    // 5. s3 = h2 + drop3(F1 W2^T + b2) -> Z; h' = LN3(s3) -> X
-    dec_gemm(Y, Wl + 9 * kPlane, acc, w, lane);
+    if (STORE) dec_store<kDR>(Y, p.f1 + l * p.asd, r0, B);
+    // 5. s3 = h2 + drop3(F1 W2^T + b2) -> Y (once every wave has read F1); h' = LN3(s3) -> X
+    dec_gemm<kDR>(Y, Wl + 9 * kPlane, acc, w, lane);
+    __syncthreads();
     {
       const float* b2 = P + p.off[O_B2];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int c = 64 * w + 16 * t + cl;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = acc[t][e] + b2[c];
-          if (train) v = m3[rg[e] * kDD + c] ? v * inv_keep : 0.f;
-          const int o = (4 * g + e) * kDLd + c;
-          Z[o] = X[o] + v;
-        }
-      }
+      epi([&](int r, int rr, int c, float a) {
+        float v = a + b2[c];
+        if (train) v = m3[rr * kDD + c] ? v * inv_keep : 0.f;
+        Y[r * kDLd + c] = X[r * kDLd + c] + v;
+      });
     }
     __syncthreads();
-    if (STORE) dec_store(Z, p.s3 + l * p.asd, r0, B);
-    dec_ln<STORE>(Z, X, P + p.off[O_N3W], P + p.off[O_N3B], w, lane, r0, B,
+    if (STORE) dec_store<kDR>(Y, p.s3 + l * p.asd, r0, B);
+    dec_ln<kDR, STORE>(Y, X, P + p.off[O_N3W], P + p.off[O_N3B], w, lane, r0, B,
                   STORE && l + 1 < L ? p.hs + (l + 1) * p.asd : nullptr, p.st3 + l * p.ast, p.ab);  // h' (the last: out)
     __syncthreads();
   }
@@ -404,7 +407,13 @@ extern "C" int gmr_decoder_fwd_f32(int64_t B, int32_t L, int32_t D, int32_t nhea
   a.mf = mask_f;
   a.msh = msh;
   a.msd = msd;
-  const dim3 grid((unsigned)((B + kDR - 1) / kDR));
+  // rows per workgroup: 32 (default; two 16-row MFMA tiles share every weight fragment, halving the weight
+  // stream from L2 / MALL) or 16 (GMR_DEC_ROWS=16: twice the workgroups for small batches)
+  static const int rows = [] {
+    const char* e = getenv("GMR_DEC_ROWS");
+    return e && atoi(e) == 16 ? 16 : 32;
+  }();
+  const dim3 grid((unsigned)((B + rows - 1) / rows));
   if (acts) {
     GMR_ARG(acts[0] && acts[1] && acts[2] && acts[3] && acts[4] && acts[5] && acts[6] && acts[7] && acts[8] && acts[9],
             "acts: ten activation buffers");
@@ -422,10 +431,12 @@ extern "C" int gmr_decoder_fwd_f32(int64_t B, int32_t L, int32_t D, int32_t nhea
     a.asd = act_stride;
     a.ast = 3 * stat_rows;
     a.ab = stat_rows;
-    hipLaunchKernelGGL(decoder_fwd_kernel<true>, grid, dim3(64 * kDW), 0, (hipStream_t)stream, B, L, h0, ld0, out, ldo,
+    auto kern = rows == 16 ? decoder_fwd_kernel<16, true> : decoder_fwd_kernel<32, true>;
+    hipLaunchKernelGGL(kern, grid, dim3(64 * kDW), 0, (hipStream_t)stream, B, L, h0, ld0, out, ldo,
                        a, p_keep, train);
   } else {
-    hipLaunchKernelGGL(decoder_fwd_kernel<false>, grid, dim3(64 * kDW), 0, (hipStream_t)stream, B, L, h0, ld0, out, ldo,
+    auto kern = rows == 16 ? decoder_fwd_kernel<16, false> : decoder_fwd_kernel<32, false>;
+    hipLaunchKernelGGL(kern, grid, dim3(64 * kDW), 0, (hipStream_t)stream, B, L, h0, ld0, out, ldo,
                        a, p_keep, train);
   }
   GMR_LAUNCHED();
