@@ -1105,7 +1105,15 @@ __device__ __forceinline__ void cl_table_fixup(int* cnt, const float* __restrict
     if (j >= n) continue;
     const int c4 = (g & 15) * 4;
     float4 a = ld4(part + j * 64 + c4);
-    for (int c = 1; c < nc; ++c) a = gmr::f4_add(a, ld4(part + ((int64_t)c * n + j) * 64 + c4));
+    int c = 1;
+    for (; c + 8 <= nc; c += 8) {  // eight chunk partials in flight (they come from other XCDs' L2s), summed in order
+      float4 t[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t[q] = ld4(part + ((int64_t)(c + q) * n + j) * 64 + c4);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a = gmr::f4_add(a, t[q]);
+    }
+    for (; c < nc; ++c) a = gmr::f4_add(a, ld4(part + ((int64_t)c * n + j) * 64 + c4));
     st4(dT + j * ld + c4, a);
   }
 }

@@ -437,22 +437,39 @@ __global__ void xattn_bwd_reduce_kernel(int D, int nhead, int chunks, const floa
   G[i] = s;
 }
 
-// dWo[j][c] += Gs[h(c)][j] bv'[c] / p_keep (Bc = keep bv' / p_keep); dbv'[c] += sum_j Wo[j][c] Gs[h(c)][j] / p_keep
-__global__ void xattn_bwd_apply_kernel(int D, int nhead, const float* __restrict__ G, const float* __restrict__ wo,
-                                       const float* __restrict__ bv, float p_keep, float* __restrict__ g_wo,
-                                       float* __restrict__ g_bv) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t DD = (int64_t)D * D;
+// dWo[j][c] += Gs[h(c)][j] bv'[c] / p_keep (Bc = keep bv' / p_keep); dbv'[c] += sum_j Wo[j][c] Gs[h(c)][j] / p_keep.
+// The first D / 16 blocks reduce dbv' (16 columns x 16 row lanes, summed across the lanes in a fixed order: one
+// thread per column walking all D rows was a serial tail of the launch); the rest update dWo elementwise.
+constexpr int kXattnBvCols = 16;
+__global__ void __launch_bounds__(256) xattn_bwd_apply_kernel(int D, int nhead, const float* __restrict__ G,
+                                                              const float* __restrict__ wo, const float* __restrict__ bv,
+                                                              float p_keep, float* __restrict__ g_wo,
+                                                              float* __restrict__ g_bv) {
   const int g = D / nhead;
-  if (i < DD) {
+  const int nbv = (D + kXattnBvCols - 1) / kXattnBvCols;
+  if ((int)blockIdx.x < nbv) {
+    __shared__ float red[256 / kXattnBvCols][kXattnBvCols];
+    const int cc = threadIdx.x % kXattnBvCols, rl = threadIdx.x / kXattnBvCols;
+    const int c = blockIdx.x * kXattnBvCols + cc;
+    float s = 0.f;
+    if (c < D) {
+      const float* gh = G + (int64_t)(c / g) * D;
+      for (int j = rl; j < D; j += 256 / kXattnBvCols) s = fmaf(wo[(int64_t)j * D + c], gh[j], s);
+    }
+    red[rl][cc] = s;
+    __syncthreads();
+    if (rl == 0 && c < D) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 256 / kXattnBvCols; ++q) t += red[q][cc];
+      g_bv[c] += t / p_keep;
+    }
+    return;
+  }
+  const int64_t i = (int64_t)(blockIdx.x - nbv) * blockDim.x + threadIdx.x;
+  if (i < (int64_t)D * D) {
     const int j = (int)(i / D), c = (int)(i % D);
     g_wo[i] += G[(int64_t)(c / g) * D + j] * (bv[c] / p_keep);
-  } else if (i < DD + D) {
-    const int c = (int)(i - DD);
-    const float* gh = G + (int64_t)(c / g) * D;
-    float s = 0.f;
-    for (int j = 0; j < D; ++j) s = fmaf(wo[(int64_t)j * D + c], gh[j], s);
-    g_bv[c] += s / p_keep;
   }
 }
 
@@ -664,7 +681,9 @@ extern "C" int gmr_xattn_bwd_f32(int64_t rows, int32_t D, int32_t nhead, const f
   hipLaunchKernelGGL(xattn_bwd_reduce_kernel, dim3(gmr::grid_for((int64_t)nhead * D, 256)), dim3(256), 0, st, D, nhead,
                      (int)chunks, part, G);
   GMR_LAUNCHED();
-  hipLaunchKernelGGL(xattn_bwd_apply_kernel, dim3(gmr::grid_for((int64_t)D * D + D, 256)), dim3(256), 0, st, D, nhead,
+  hipLaunchKernelGGL(xattn_bwd_apply_kernel,
+                     dim3((unsigned)((D + kXattnBvCols - 1) / kXattnBvCols + gmr::grid_for((int64_t)D * D, 256))),
+                     dim3(256), 0, st, D, nhead,
                      G, wo, bv, p_keep, g_wo, g_bv);
   GMR_LAUNCHED();
   return GMR_OK;

@@ -30,9 +30,11 @@ def _round4(n):
     return (n + 3) // 4 * 4
 
 
-# GMR_DEC_FUSED (default 1): forwards that keep no activations (the p_sample steps) run the decoder stack as
-# one launch (gmr_decoder_fwd_f32, csrc/decoder.hip) when d_model = 512 and nhead = 8; 0: layer by layer
-DEC_FUSED = os.environ.get("GMR_DEC_FUSED", "1") != "0"
+# GMR_DEC_FUSED=1 (opt-in): run the decoder stack as one launch (gmr_decoder_fwd_f32, csrc/decoder.hip) when
+# d_model = 512 and nhead = 8.  Default 0, layer by layer: at the GenRecV1 batch (2,048 rows) the fused stack
+# fills 64 of 256 CUs and re-streams every weight plane per 32-row block, 1.49 ms per call vs ~0.7 ms for the
+# tiled GEMMs + row kernels (epoch 165 vs 121 ms, profiles/r04s_genrecv1_ab.txt)
+DEC_FUSED = os.environ.get("GMR_DEC_FUSED", "0") != "0"
 
 
 class TransformerDenoiser:
