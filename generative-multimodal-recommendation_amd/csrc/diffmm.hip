@@ -1333,9 +1333,12 @@ __global__ void __launch_bounds__(256, 2) cl6p_kernel(int nf, int ns, const floa
   if (TABLE && cnt) cl_table_fixup(cnt + blockIdx.x, part_y, nf, dT, ld_dt);
 }
 
-int cl_fixup() {  // GMR_CL_FIXUP=0: the table partials reduced by cl_table_reduce_kernel (read per call)
+// GMR_CL_FIXUP=1 (opt-in; read per call): the table pass reduces its own partials (last block per tile).
+// Default 0, cl_table_reduce_kernel: the last block's serial sum is a tail of the launch, 180 / 101 us vs
+// 165 / 80 us per call at the DiffMM baby shapes, epoch 99.0 vs 97.0 ms (profiles/r04u_ab.txt)
+int cl_fixup() {
   const char* e = getenv("GMR_CL_FIXUP");
-  return !(e && atoi(e) == 0);
+  return e && atoi(e) == 1;
 }
 
 int cl_pipe() {  // read per call (a getenv), so a test can compare both forms in one process

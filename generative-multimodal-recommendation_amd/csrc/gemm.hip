@@ -631,12 +631,15 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
     // fill < 80 % of the resident slots (256 x 128: one block per CU; 128^2: two) and slabs stay >= 512
     // deep (measured: the 7050 x 1000 x 2048 weight gradients 253 -> 222 us unsplit, the 2048-row
     // diffusion products best at 4 slabs; profiles/r02x6_study.txt)
-    // (GMR_X6_MIN_SLAB: the minimum slab depth, default 512; for A/B runs of the small 64^2 products)
-    static const int64_t min_slab = [] {
+    // 64^2 plans split down to 256-deep slabs (the GenRecV1 2048 x 512 x 512 decoder products: one tile per
+    // CU and a latency-bound 512-deep k loop unsplit; epoch 118.0 -> 114.5 ms, profiles/r04u_ab.txt),
+    // the larger tiles to 512 (GMR_X6_MIN_SLAB overrides both, for A/B runs)
+    static const int64_t min_slab_env = [] {
       const char* e = getenv("GMR_X6_MIN_SLAB");
       const int v = e ? atoi(e) : 0;
-      return (int64_t)(v >= 64 ? v : 512);
+      return (int64_t)(v >= 64 ? v : 0);
     }();
+    const int64_t min_slab = min_slab_env ? min_slab_env : p.bm == 64 ? 256 : 512;
     const int64_t slots = p.bm == 64 ? 768 : p.bm * p.bn == 128 * 128 ? 512 : 256;
     splits = 1;
     while (p.tm * p.tn * splits * 5 < slots * 4 && K / (splits * 2) >= min_slab && splits < 16) splits *= 2;

@@ -465,7 +465,7 @@ def test_contrast_pipelined_bit_exact(K, B, n, monkeypatch):
 
 @pytest.mark.parametrize("B,n", [(2048, 19445), (2048, 7050), (300, 1000), (40, 97)])
 def test_contrast_table_fixup_bit_exact(K, B, n, monkeypatch):
-    """GMR_CL_FIXUP (default): the table pass sums its chunk partials itself (the last block of each
+    """GMR_CL_FIXUP=1 (opt-in): the table pass sums its chunk partials itself (the last block of each
     128-row tile, in chunk order, counters left zero for the next call) instead of cl_table_reduce_kernel:
     dT bit for bit, and repeated calls (the counters reset) stay identical."""
     _contrast_env_bit_exact(K, B, n, monkeypatch, "GMR_CL_FIXUP", repeats=3)
