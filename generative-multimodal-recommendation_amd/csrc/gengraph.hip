@@ -443,7 +443,20 @@ __global__ void min_dist_update_kernel(int64_t n, const float* __restrict__ xsq,
   mind[r] = first ? d : fminf(mind[r], d);
 }
 
-// k-means++ pick: one workgroup; point chosen with probability mind[r] / sum (Philox draw)
+// sum of the 1,024 per-thread partials, by wave 0 in a fixed order (16 consecutive partials per lane, then a
+// shuffle tree): the result in lane 0 (the serial 1,024-step sum of one thread was most of the launch)
+__device__ __forceinline__ double kpp_wave_total(const double* part, int lane) {
+  double v = 0.0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v += part[lane * 16 + q];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+  return v;
+}
+
+// k-means++ pick: one workgroup; point chosen with probability mind[r] / sum (Philox draw).  Wave 0 scans the
+// 64 group sums of 16 partials (shuffle scan, fixed order), a ballot finds the group holding u, one lane walks
+// its <= 16 partials and then the <= chunk points of the partial
 __global__ void __launch_bounds__(1024) kpp_pick_kernel(int64_t n, const float* __restrict__ mind, uint64_t seed,
                                                         uint64_t step, int* __restrict__ out) {
   __shared__ double part[1024];
@@ -454,24 +467,34 @@ __global__ void __launch_bounds__(1024) kpp_pick_kernel(int64_t n, const float* 
   for (int64_t r = r0; r < r1; ++r) s += mind ? (double)mind[r] : 1.0;
   part[t] = s;
   __syncthreads();
-  if (t == 0) {
-    double tot = 0.0;
-    for (int j = 0; j < 1024; ++j) tot += part[j];
-    const uint4 rr = gmr::Philox::gen(seed, step, 0);
-    const double u = ((double)rr.x + (double)rr.y * 4294967296.0) / 18446744073709551616.0 * tot;
-    double acc = 0.0;
-    int j = 0;
-    for (; j < 1023 && acc + part[j] <= u; ++j) acc += part[j];
-    const int64_t a = j * chunk, e = a + chunk < n ? a + chunk : n;
-    int64_t pick = a < n ? a : n - 1;
-    for (int64_t r = a; r < e; ++r) {
-      const double m = mind ? (double)mind[r] : 1.0;
-      pick = r;
-      if (acc + m > u && m > 0) break;
-      acc += m;
-    }
-    out[0] = (int)pick;
+  if (t >= 64) return;
+  double g = 0.0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) g += part[t * 16 + q];
+  double inc = g;  // inclusive scan over the 64 groups
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double o = __shfl_up(inc, off);
+    if (t >= off) inc += o;
   }
+  const double tot = __shfl(inc, 63);
+  const uint4 rr = gmr::Philox::gen(seed, step, 0);
+  const double u = ((double)rr.x + (double)rr.y * 4294967296.0) / 18446744073709551616.0 * tot;
+  const unsigned long long bal = __ballot(inc > u);
+  const int grp = bal ? __ffsll(bal) - 1 : 63;  // no group above u (rounding, or every mind 0): the last
+  if (t != grp) return;
+  double acc = inc - g;
+  int j = grp * 16;
+  for (; j < grp * 16 + 15 && acc + part[j] <= u; ++j) acc += part[j];
+  const int64_t a = j * chunk, e = a + chunk < n ? a + chunk : n;
+  int64_t pick = a < n ? a : n - 1;
+  for (int64_t r = a; r < e; ++r) {
+    const double m = mind ? (double)mind[r] : 1.0;
+    pick = r;
+    if (acc + m > u && m > 0) break;
+    acc += m;
+  }
+  out[0] = (int)pick;
 }
 
 // greedy k-means++ step (sklearn's _kmeans_plusplus with n_local_trials candidates, KMeans' default seeding):
@@ -497,10 +520,9 @@ __global__ void __launch_bounds__(1024) kpp_greedy_kernel(int64_t n, int L, cons
     }
     part[t0] = s;
     __syncthreads();
-    if (t0 == 0) {
-      double tot = 0.0;
-      for (int i = 0; i < 1024; ++i) tot += part[i];
-      pot[t] = tot;
+    if (t0 < 64) {
+      const double tot = kpp_wave_total(part, t0);
+      if (t0 == 0) pot[t] = tot;
     }
     __syncthreads();
   }

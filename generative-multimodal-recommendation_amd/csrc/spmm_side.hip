@@ -237,9 +237,11 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
         const int4 hb = hubs[h];
         int* cnt = counters + (int64_t)h * kSideCounterWords + slice;
         int old = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this block's partial before its count
         if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         old = __shfl(old, 0);
         if (old == hb.z - 1) {  // last block of the row: every block sum is published
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // ... and visible to this wave's loads
           float4 s = f4_zero();
           for (int j = grp; j < hb.z; j += 8) {
             const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(prs, ((hb.y + j) * 256 + c0) * 4, 0, 16);

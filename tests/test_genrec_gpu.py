@@ -422,3 +422,36 @@ def test_trainer_epoch_and_eval():
     assert np.all(np.isfinite(dl))
     res = trainer.evaluate(vl)
     assert 0.0 <= res["recall@20"] <= 1.0
+
+
+@pytest.mark.parametrize("n", [6710, 100, 1024, 4097])
+def test_kmeans_pp_pick_weighted_draw(n):
+    """gmr_kmeans_pp_pick (k-means++ candidate draw with probability mind[r] / sum, csrc/gengraph.hip): a single
+    non-zero weight is always picked (first, last and inner points; n below, at and above the 1,024 partials);
+    two weights are picked in their ratio (binomial 5-sigma bound over 600 draws); mind = NULL picks uniformly."""
+    from gmr import _lib
+    from gmr.kernels import ptr, stream
+    draws = 600
+    out = torch.empty(draws, dtype=torch.int32, device=DEV)
+
+    def pick(mind, k=draws):
+        for i in range(k):
+            _lib.call("gmr_kmeans_pp_pick", n, ptr(mind) if mind is not None else None, 7, 100 + i, ptr(out[i:i + 1]),
+                      stream())
+        return out[:k].cpu().numpy()
+
+    for p in (0, n - 1, n // 3):
+        mind = torch.zeros(n, device=DEV)
+        mind[p] = 0.37
+        assert (pick(mind, 20) == p).all()
+    p1, p2 = n // 5, n - 2
+    mind = torch.zeros(n, device=DEV)
+    mind[p1], mind[p2] = 1.0, 3.0
+    got = pick(mind)
+    assert set(np.unique(got)) <= {p1, p2}
+    f = (got == p1).mean()
+    assert abs(f - 0.25) < 5 * np.sqrt(0.25 * 0.75 / draws)
+    got = pick(None)
+    assert got.min() >= 0 and got.max() < n
+    hist = np.bincount(got * 4 // n, minlength=4) / draws
+    assert np.abs(hist - 0.25).max() < 5 * np.sqrt(0.25 * 0.75 / draws)
