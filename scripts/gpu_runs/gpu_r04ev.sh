@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-4 evidence on the current library: full GPU suite, smoke, serial rocprof summary of the bench
-# epoch, PMC passes for the DiffMM workload (stamped to this library, copied into profiles/ so the
-# bench line carries their traffic), default bench line (with the DiffRec / GenRecV1 legs).
+# epoch, PMC passes for the DiffMM, GenRecV1 and DiffRec workloads (stamped to this library, copied into profiles/ so the
+# bench line and its legs carry their traffic), default bench line (with the DiffRec / GenRecV1 legs).
 # usage: bash scripts/gpu_runs/gpu_r04ev.sh <tag>
 set -o pipefail
 TAG=${1:-r04ev}
@@ -12,8 +12,10 @@ timeout -k 10 1000 python -u -m pytest -v --timeout 300 --timeout-method thread 
 echo "tests rc=$rc" >> gpurun_out/${TAG}_tests.log; tail -2 gpurun_out/${TAG}_tests.log; fatal $rc tests
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.log 2>&1; fatal $? smoke
 GMR_SERIAL=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o prof -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-legs --no-probe > gpurun_out/${TAG}_prof.log 2>&1; fatal $? prof
-bash scripts/pmc_collect.sh $TAG diffmm > /dev/null; fatal $? pmc
-cp gpurun_out/${TAG}_pmc_diffmm.json profiles/
+for m in diffmm genrecv1 diffrec; do
+  bash scripts/pmc_collect.sh $TAG $m > gpurun_out/${TAG}_pmc_$m.log 2>&1; fatal $? pmc_$m
+  cp gpurun_out/${TAG}_pmc_$m.json profiles/
+done
 GMR_PROBE_REPORT=1 timeout -k 10 700 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err; fatal $? bench
 cut -c1-400 gpurun_out/${TAG}_bench.json
 echo all-done
