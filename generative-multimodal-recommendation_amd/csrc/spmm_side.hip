@@ -236,12 +236,16 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
         const int h = slotmap[tkc.w];
         const int4 hb = hubs[h];
         int* cnt = counters + (int64_t)h * kSideCounterWords + slice;
+        // Ordering without agent-scope fences (an agent-scope release on gfx950 writes back the XCD's dirty
+        // L2 lines: per hub partial it took the epoch's SpMM class 12.6 -> 21.2 ms, profiles/r04ev2_bench.err):
+        // the partial is stored and re-read with device-scope (sc1) buffer ops, which bypass the per-XCD L2s;
+        // the store has completed (vmcnt(0), whose "memory" clobber also keeps the compiler from moving the
+        // counter add above it) before the add is issued; the last block's loads are control-dependent on
+        // the add's returned value, so they issue after every other block's add, i.e. after its store.
         int old = 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this block's partial before its count
         if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         old = __shfl(old, 0);
         if (old == hb.z - 1) {  // last block of the row: every block sum is published
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // ... and visible to this wave's loads
           float4 s = f4_zero();
           for (int j = grp; j < hb.z; j += 8) {
             const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(prs, ((hb.y + j) * 256 + c0) * 4, 0, 16);
