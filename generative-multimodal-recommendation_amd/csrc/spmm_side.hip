@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
         const int4 hb = hubs[h];
         int* cnt = counters + (int64_t)h * kSideCounterWords + slice;
         // Ordering without agent-scope fences (an agent-scope release on gfx950 writes back the XCD's dirty
-        // L2 lines: per hub partial it took the epoch's SpMM class 12.6 -> 21.2 ms, profiles/r04ev2_bench.err):
+        // L2 lines: per hub partial it took the epoch's SpMM class 12.6 -> 21.2 ms, profiles/r04ev2_bench.err, profiles/r04ev2_bench_fenced_spmm.json):
         // the partial is stored and re-read with device-scope (sc1) buffer ops, which bypass the per-XCD L2s;
         // the store has completed (vmcnt(0), whose "memory" clobber also keeps the compiler from moving the
         // counter add above it) before the add is issued; the last block's loads are control-dependent on

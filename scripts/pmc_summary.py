@@ -22,14 +22,15 @@ CLASSES = {"gemm": ("gemm_kernel", "gemm_glds_kernel", "splitk_reduce_kernel"),
            "gemm_x6": ("gemm_x6_kernel", "gemm_p3_kernel", "split3_planes_kernel"),
            "spmm": ("spmm_seg_kernel", "spmm_fix_kernel", "spmm_lane_kernel", "spmm_lane_jobs_kernel",
                     "lane_fix_kernel", "lane_fix_jobs_kernel", "spmm_blk_kernel", "spmm_chunk_kernel", "spmm_side_kernel"),
-           "infonce": ("cl_rows_kernel", "cl_table_kernel", "cl6_kernel", "cl_finalize_kernel", "cl_table_reduce_kernel")}
+           "infonce": ("cl_rows_kernel", "cl_table_kernel", "cl6_kernel", "cl6p_kernel", "cl_finalize_kernel",
+                       "cl_table_reduce_kernel")}
 # launches of a class = launches of its primary kernels (one per gmr_* call)
 PRIMARY = {"gemm": ("gemm_kernel", "gemm_glds_kernel"), "gemm_x6": ("gemm_x6_kernel", "gemm_p3_kernel"),
            "spmm": ("spmm_seg_kernel", "spmm_lane_kernel", "spmm_lane_jobs_kernel", "spmm_blk_kernel",
                     "spmm_chunk_kernel", "spmm_side_kernel"),
            "infonce": ("cl_rows_kernel", "cl6_rows")}
 UTIL = {"gemm": ("gemm_kernel", "gemm_glds_kernel"), "gemm_x6": ("gemm_x6_kernel", "gemm_p3_kernel"), "spmm": (),
-        "infonce": ("cl_rows_kernel", "cl_table_kernel", "cl6_kernel")}
+        "infonce": ("cl_rows_kernel", "cl_table_kernel", "cl6_kernel", "cl6p_kernel")}
 
 
 def load(path, counter):
@@ -40,7 +41,7 @@ def load(path, counter):
         name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
         base = name.split("<")[0]
         out.append((r.get("Dispatch_Id") or r.get("Correlation_Id"), base, float(r["Counter_Value"])))
-        if base == "cl6_kernel" and name.replace(" ", "").endswith(",false>"):
+        if base in ("cl6_kernel", "cl6p_kernel") and name.replace(" ", "").endswith(",false>"):
             out.append((None, "cl6_rows", 0.0))  # one split-bf16 InfoNCE call = one rows pass (marker)
     return out
 
