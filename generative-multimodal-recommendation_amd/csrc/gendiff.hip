@@ -157,11 +157,18 @@ __global__ void __launch_bounds__(256) flip_loss_kernel(int B, int I, const floa
 }
 
 // ----------------------------------------------------------------- LayerNorm (one wave per row, D <= 1024)
-// s = a + keep * scale * b (b: matrix, or a broadcast vector when ldb == 0); y = LN(s) w + bias [-> GELU]
+// s = a + keep * scale * b (b: matrix, or a broadcast vector when ldb == 0); y = LN(s) w + bias [-> GELU].
+// LnDraw.on: the keep bytes are drawn here (gmr_keep_mask_u8's Philox key, counter ctr0 + r D + c) and stored
+// to keep, instead of read from it: the residual-branch dropout without its separate mask launch.
+struct LnDraw {
+  float p_keep;
+  uint64_t seed, step, ctr0;
+  int on;
+};
 template <int PER>  // floats per lane (D = 64 * PER; PER 1 with Dsmall = 32 or 64)
 __global__ void __launch_bounds__(256) ln_fwd_kernel(int Dsmall, int64_t rows, const float* __restrict__ a, int64_t lda,
                                                      const float* __restrict__ bsrc, int64_t ldb,
-                                                     const uint8_t* __restrict__ keep, int64_t ldk, float kscale,
+                                                     uint8_t* __restrict__ keep, int64_t ldk, float kscale, LnDraw dr,
                                                      const float* __restrict__ w, const float* __restrict__ bias,
                                                      float eps, int gelu, float* __restrict__ y, int64_t ldy,
                                                      float* __restrict__ s_out, int64_t lds,
@@ -181,7 +188,14 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(int Dsmall, int64_t rows, c
       x = a[r * lda + c];
       if (bsrc) {
         float bb = bsrc[(ldb ? r * ldb : 0) + c];
-        if (keep) bb = keep[r * ldk + c] ? bb * kscale : 0.f;
+        if (dr.on) {
+          const uint4 q = gmr::Philox::gen(dr.seed, dr.step, dr.ctr0 + (uint64_t)(r * D + c));
+          const uint8_t k = (float)(q.x >> 8) * (1.0f / 16777216.0f) < dr.p_keep ? 1 : 0;
+          keep[r * ldk + c] = k;
+          bb = k ? bb * kscale : 0.f;
+        } else if (keep) {
+          bb = keep[r * ldk + c] ? bb * kscale : 0.f;
+        }
         x += bb;
       }
     }
@@ -548,17 +562,18 @@ extern "C" int gmr_flip_loss_rows(int32_t B, int32_t I, const float* x0, int64_t
   return GMR_OK;
 }
 
-extern "C" int gmr_layernorm_fwd(int64_t rows, int32_t D, const float* a, int64_t lda, const float* b, int64_t ldb,
-                                 const uint8_t* keep, int64_t ld_keep, float keep_scale, const float* w,
-                                 const float* bias, float eps, int32_t gelu, float* y, int64_t ldy, float* s_out,
-                                 int64_t lds, float* mean, float* rstd, void* stream) {
+namespace {
+int layernorm_launch(int64_t rows, int32_t D, const float* a, int64_t lda, const float* b, int64_t ldb, uint8_t* keep,
+                     int64_t ld_keep, float keep_scale, LnDraw dr, const float* w, const float* bias, float eps,
+                     int32_t gelu, float* y, int64_t ldy, float* s_out, int64_t lds, float* mean, float* rstd,
+                     void* stream) {
   GMR_ARG(a && w && bias && y && mean && rstd && rows > 0, "bad args");
   GMR_ARG(D == 32 || D == 64 || D == 128 || D == 256 || D == 512 || D == 1024, "D must be 32..1024 (power of two)");
   const dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
 #define GMR_LNF(P)                                                                                                \
   hipLaunchKernelGGL(ln_fwd_kernel<P>, grid, dim3(256), 0, st, (int)D, rows, a, lda, b, ldb, keep, ld_keep,        \
-                     keep_scale, w, bias, eps, (int)gelu, y, ldy, s_out, lds, mean, rstd)
+                     keep_scale, dr, w, bias, eps, (int)gelu, y, ldy, s_out, lds, mean, rstd)
   switch (D) {
     case 32:
     case 64: GMR_LNF(1); break;
@@ -570,6 +585,26 @@ extern "C" int gmr_layernorm_fwd(int64_t rows, int32_t D, const float* a, int64_
 #undef GMR_LNF
   GMR_LAUNCHED();
   return GMR_OK;
+}
+}  // namespace
+
+extern "C" int gmr_layernorm_fwd(int64_t rows, int32_t D, const float* a, int64_t lda, const float* b, int64_t ldb,
+                                 const uint8_t* keep, int64_t ld_keep, float keep_scale, const float* w,
+                                 const float* bias, float eps, int32_t gelu, float* y, int64_t ldy, float* s_out,
+                                 int64_t lds, float* mean, float* rstd, void* stream) {
+  return layernorm_launch(rows, D, a, lda, b, ldb, const_cast<uint8_t*>(keep), ld_keep, keep_scale, LnDraw{1.f, 0, 0, 0, 0},
+                          w, bias, eps, gelu, y, ldy, s_out, lds, mean, rstd, stream);
+}
+
+extern "C" int gmr_layernorm_drop_fwd(int64_t rows, int32_t D, const float* a, int64_t lda, const float* b, int64_t ldb,
+                                      float p_keep, uint64_t seed, uint64_t step, uint64_t ctr0, uint8_t* keep_out,
+                                      int64_t ld_keep, float keep_scale, const float* w, const float* bias, float eps,
+                                      int32_t gelu, float* y, int64_t ldy, float* s_out, int64_t lds, float* mean,
+                                      float* rstd, void* stream) {
+  GMR_ARG(b && ldb > 0 && keep_out && ld_keep >= D, "the dropped branch b and the keep buffer are required");
+  GMR_ARG(p_keep > 0.f && p_keep <= 1.f, "p_keep in (0, 1]");
+  return layernorm_launch(rows, D, a, lda, b, ldb, keep_out, ld_keep, keep_scale, LnDraw{p_keep, seed, step, ctr0, 1}, w,
+                          bias, eps, gelu, y, ldy, s_out, lds, mean, rstd, stream);
 }
 
 extern "C" int64_t gmr_layernorm_parts_floats(int64_t rows, int32_t D) {

@@ -155,6 +155,8 @@ SIGNATURES = {
     "gmr_flip_loss_rows": (I32, [I32, I32, P, I64, P, I64, P, P, I32, F32, P, I64, P, P, P]),
     "gmr_flip_total": (I32, [P, P, F32, P, P]),
     "gmr_layernorm_fwd": (I32, [I64, I32, P, I64, P, I64, P, I64, F32, P, P, F32, I32, P, I64, P, I64, P, P, P]),
+    "gmr_layernorm_drop_fwd": (I32, [I64, I32, P, I64, P, I64, F32, U64, U64, U64, P, I64, F32, P, P, F32, I32, P, I64,
+                                     P, I64, P, P, P]),
     "gmr_layernorm_parts_floats": (I64, [I64, I32]),
     "gmr_layernorm_bwd": (I32, [I64, I32, P, I64, P, P, P, P, I32, P, I64, P, I64, I32, P, P, P, I32, P]),
     "gmr_adaln_fwd": (I32, [I64, I32, P, I64, P, I32, P, I64, P, I64, P]),

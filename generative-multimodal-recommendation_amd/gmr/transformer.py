@@ -326,9 +326,12 @@ class TransformerDenoiser:
             given = masks.get(site) if masks else None
             if given is not None:
                 mbuf.copy_(given[l])
-            else:  # draw the residual-branch dropout mask (mask only: the LN kernel applies it)
-                _lib.call("gmr_keep_mask_u8", B * D, keep, seed, self._site_step(step, l, site), int(row0) * D, ptr(mbuf),
-                          stream())
+            else:  # the residual-branch dropout mask drawn by the LN kernel itself (gmr_keep_mask_u8's keys)
+                assert mbuf.stride(0) == D and ldb > 0
+                _lib.call("gmr_layernorm_drop_fwd", B, D, ptr(a), K._ld(a), ptr(b), ldb, keep, seed,
+                          self._site_step(step, l, site), int(row0) * D, ptr(mbuf), D, 1.0 / keep, ptr(wt), ptr(bs),
+                          1e-5, 0, ptr(y), K._ld(y), ptr(s), D, ptr(mean), ptr(rstd), stream())
+                return
         _lib.call("gmr_layernorm_fwd", B, D, ptr(a), K._ld(a), ptr(b), ldb, ptr(mbuf), mbuf.stride(0) if mbuf is not None
                   else 0, 1.0 / keep, ptr(wt), ptr(bs), 1e-5, 0, ptr(y), K._ld(y), ptr(s), D, ptr(mean), ptr(rstd),
                   stream())

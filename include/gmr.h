@@ -594,6 +594,15 @@ int gmr_layernorm_fwd(int64_t rows, int32_t D, const float* a, int64_t lda, cons
                       const uint8_t* keep, int64_t ld_keep, float keep_scale, const float* w, const float* bias,
                       float eps, int32_t gelu, float* y, int64_t ldy, float* s_out, int64_t lds, float* mean,
                       float* rstd, void* stream);
+/* The same with the residual-branch dropout drawn in the kernel (nn.Dropout on the decoder layer's branch,
+ * :650-710): keep_out[r][c] = (Philox(seed, step, ctr0 + r D + c).x >> 8) / 2^24 < p_keep (gmr_keep_mask_u8's
+ * key, so the bytes equal a gmr_keep_mask_u8 draw of rows x D at ctr0) is stored and applied; one launch
+ * instead of the mask launch + gmr_layernorm_fwd.  b must be a matrix (ldb > 0). */
+int gmr_layernorm_drop_fwd(int64_t rows, int32_t D, const float* a, int64_t lda, const float* b, int64_t ldb,
+                           float p_keep, uint64_t seed, uint64_t step, uint64_t ctr0, uint8_t* keep_out,
+                           int64_t ld_keep, float keep_scale, const float* w, const float* bias, float eps,
+                           int32_t gelu, float* y, int64_t ldy, float* s_out, int64_t lds, float* mean, float* rstd,
+                           void* stream);
 int64_t gmr_layernorm_parts_floats(int64_t rows, int32_t D);
 int gmr_layernorm_bwd(int64_t rows, int32_t D, const float* s, int64_t lds, const float* mean, const float* rstd,
                       const float* w, const float* bias, int32_t gelu, const float* dy, int64_t lddy, float* dx,

@@ -94,3 +94,33 @@ def test_fused_training_forward_feeds_the_backward(train, B, monkeypatch):
     np.testing.assert_allclose(res[1][0], res[0][0], rtol=1e-4, atol=1e-5)
     g0, g1 = res[0][1], res[1][1]
     np.testing.assert_allclose(g1, g0, rtol=1e-3, atol=1e-4 * np.abs(g0).max())
+
+
+@pytest.mark.parametrize("B,row0,keep", [(300, 0, 0.8), (37, 1000, 0.5), (2048, 5, 0.9)])
+def test_layernorm_drop_fwd_equals_mask_then_layernorm(B, row0, keep):
+    """gmr_layernorm_drop_fwd (the residual-branch dropout drawn inside the LayerNorm kernel) against
+    gmr_keep_mask_u8 + gmr_layernorm_fwd with the same Philox key: keep bytes, y, s, mean and rstd bit for bit."""
+    from gmr import _lib
+    from gmr.kernels import ptr, stream
+    D = 512
+    rng = np.random.default_rng(B)
+    a = torch.as_tensor(rng.standard_normal((B, D)).astype(np.float32), device=DEV)
+    b = torch.as_tensor(rng.standard_normal((B, D)).astype(np.float32), device=DEV)
+    w = torch.as_tensor(rng.standard_normal(D).astype(np.float32), device=DEV)
+    bs = torch.as_tensor(rng.standard_normal(D).astype(np.float32), device=DEV)
+    res = []
+    for fused in (False, True):
+        m = torch.full((B, D), 7, dtype=torch.uint8, device=DEV)
+        y, s = torch.empty((B, D), device=DEV), torch.empty((B, D), device=DEV)
+        mean, rstd = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+        if fused:
+            _lib.call("gmr_layernorm_drop_fwd", B, D, ptr(a), D, ptr(b), D, keep, 11, 1234, row0 * D, ptr(m), D,
+                      1.0 / keep, ptr(w), ptr(bs), 1e-5, 0, ptr(y), D, ptr(s), D, ptr(mean), ptr(rstd), stream())
+        else:
+            _lib.call("gmr_keep_mask_u8", B * D, keep, 11, 1234, row0 * D, ptr(m), stream())
+            _lib.call("gmr_layernorm_fwd", B, D, ptr(a), D, ptr(b), D, ptr(m), D, 1.0 / keep, ptr(w), ptr(bs), 1e-5, 0,
+                      ptr(y), D, ptr(s), D, ptr(mean), ptr(rstd), stream())
+        res.append([t.cpu() for t in (m, y, s, mean, rstd)])
+    assert 0.3 < res[0][0].float().mean().item() / keep < 1.7
+    for x0, x1 in zip(*res):
+        assert torch.equal(x0, x1)
