@@ -1,19 +1,11 @@
 #!/bin/bash
-# r04g: class plan with the ballot class lookup and the prefetched hub loop: isolation probe, SpMM kernel
-# tests (both plan forms), then the DiffMM phase / baby parity tests on the new default.
+# r04g: DiffMM epoch with the rec step replayed from a HIP graph (GMR_GRAPHS=1) vs eager, alternating, 5 steps
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-python scripts/micro/dump_graph.py baby norm_adj /tmp/na.bin > gpurun_out/r04g_probe.txt || exit 1
-python scripts/micro/dump_graph.py baby ui_top1 /tmp/ui.bin >> gpurun_out/r04g_probe.txt || exit 1
-timeout -k 10 240 scripts/micro/side_iso /tmp/na.bin >> gpurun_out/r04g_probe.txt 2>&1 || { tail -20 gpurun_out/r04g_probe.txt; exit 1; }
-timeout -k 10 240 scripts/micro/side_iso /tmp/ui.bin >> gpurun_out/r04g_probe.txt 2>&1 || { tail -20 gpurun_out/r04g_probe.txt; exit 1; }
-grep -E 'full|user side only|item side only|classes|T=' gpurun_out/r04g_probe.txt | head -120
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider \
-  tests/test_kernels_gpu.py -k "spmm" > gpurun_out/r04g_spmm_tests.log 2>&1 || { tail -30 gpurun_out/r04g_spmm_tests.log; exit 1; }
-tail -3 gpurun_out/r04g_spmm_tests.log
-timeout -k 10 900 python -u -m pytest -x -v --timeout 420 --timeout-method thread -p no:cacheprovider \
-  tests/test_diffmm_gpu.py tests/test_phases_gpu.py tests/test_baby_gpu.py tests/test_sports_gpu.py > gpurun_out/r04g_tests.log 2>&1
-rc=$?
-tail -5 gpurun_out/r04g_tests.log
-exit $rc
+for r in a b c; do
+  for g in 0 1; do
+    GMR_GRAPHS=$g timeout -k 10 300 python bench.py --model diffmm --no-legs --steps 5 --warmup 2 --no-cpu-baseline --no-probe > gpurun_out/r04g_g${g}_$r.json 2> gpurun_out/r04g_g${g}_$r.err || { tail -20 gpurun_out/r04g_g${g}_$r.err; exit 1; }
+    echo "GMR_GRAPHS=$g ($r) $(python -c "import json; d=json.load(open('gpurun_out/r04g_g${g}_$r.json')); print(d['value'], d['ms_per_step'], d['eval_recall@20'])")"
+  done
+done | tee gpurun_out/r04g_ab.txt
