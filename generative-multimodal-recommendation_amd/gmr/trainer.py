@@ -86,7 +86,8 @@ class Trainer:
         # GMR_GRAPHS=1: full-size BPR steps of models that expose graph_key() (DiffMM) replay a HIP
         # graph of the whole rec step, side streams included (torch.cuda.CUDAGraph; captured on the
         # first step and again when the model's device graphs change, i.e. after each rebuild).
-        # Off by default: the step is GPU-bound, so replay saves only launch gaps.
+        # Off by default: measured slower in the epoch (104-106 vs 95-97 ms, profiles/r04g_graphs_ab.txt;
+        # the replay appears to lose the three-stream overlap of the eager step).
         self._use_graphs = os.environ.get("GMR_GRAPHS", "0") == "1" and hasattr(model, "graph_key")
         self._graph = None
         self.fused_eval = FUSED_EVAL  # per trainer, so a test can run both eval paths in one process
