@@ -158,6 +158,26 @@ def test_forward_train_and_bn_stats(G, M):
         np.testing.assert_allclose(model.bn_state[n][1].cpu().numpy(), m[f"fwd_bn_{n}_var"], rtol=1e-5, atol=1e-7)
 
 
+def test_rec_step_unfused_nce_matches_golden(G, M, monkeypatch):
+    """GMR_NCE_FUSED=0 (the in-batch InfoNCE terms through the B x B logit GEMMs instead of the fused contrast
+    kernel): the same loss and gradients as the reference (the default fused form is checked below)."""
+    from gmr import genrecv1 as gv
+    monkeypatch.setattr(gv, "NCE_FUSED", False)
+    m = G["m"]
+    model, _ = M
+    for n in BN_NAMES:
+        model.bn_state[n][0].zero_()
+        model.bn_state[n][1].fill_(1.0)
+    model._forward(model._work(24), True, _inject_masks(m, "fwd"))
+    t = lambda k: _dev(m[k].astype(np.int32))  # noqa: E731
+    loss = model.rec_step(t("bpr_users"), t("bpr_pos"), t("bpr_neg"), masks=_inject_masks(m, "loss"))
+    np.testing.assert_allclose(loss.item(), float(m["loss"]), rtol=1e-5)
+    for n in [str(s) for s in m["g_names"]]:
+        k = n.replace(".", "_")
+        np.testing.assert_allclose(model.grad_view(k).cpu().numpy().reshape(m["g_" + k].shape), m["g_" + k],
+                                   rtol=2e-4, atol=2e-7, err_msg=n)
+
+
 def test_rec_step_loss_grads_and_eval(G, M):
     m = G["m"]
     model, _ = M
