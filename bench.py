@@ -398,7 +398,9 @@ def main():
     ap.add_argument("--scoring-dtype", default=None, choices=["fp32", "fp16"],
                     help="GenRecV1 full-catalog scoring precision (config 5's fp16 MFMA scoring GEMM)")
     args = ap.parse_args()
-    legs = args.model is None and not args.no_legs
+    # the DiffRec / GenRecV1 legs at N = 1 only: under data parallelism an exception in one rank's leg would leave
+    # the others waiting in a collective, and the scaling line is the DiffMM headline's
+    legs = args.model is None and not args.no_legs and int(os.environ.get("WORLD_SIZE", "1")) == 1
     args.model = args.model or "diffmm"
     args.shape = args.shape or DEFAULT_SHAPE[args.model]
 
