@@ -8,20 +8,46 @@
 
 namespace {
 
+// one element's update (torch.optim.Adam's arithmetic, every product and sum rounded on its own): FMA
+// contraction is off here because the float4 kernel's packed instructions (v_pk_fma_f32) would otherwise
+// contract differently from the scalar kernel's, and the two paths must agree bit for bit
+__device__ __forceinline__ float adam_one(float gi, float pi, float& mi, float& vi, float b1, float b2, float eps,
+                                          float wd, float step_size, float bc2_sqrt) {
+#pragma clang fp contract(off)
+  if (wd != 0.f) gi = gi + wd * pi;
+  mi = mi + (1.f - b1) * (gi - mi);
+  vi = vi * b2 + (1.f - b2) * gi * gi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  return pi - step_size * (mi / denom);
+}
 __global__ void adam_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, float b1, float b2, float eps, float wd, float step_size,
                             float bc2_sqrt) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float gi = g[i];
-  const float pi = p[i];
-  if (wd != 0.f) gi = gi + wd * pi;
-  const float mi = m[i] + (1.f - b1) * (gi - m[i]);
-  const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+  float mi = m[i], vi = v[i];
+  const float po = adam_one(g[i], p[i], mi, vi, b1, b2, eps, wd, step_size, bc2_sqrt);
   m[i] = mi;
   v[i] = vi;
-  const float denom = sqrtf(vi) / bc2_sqrt + eps;
-  p[i] = pi - step_size * (mi / denom);
+  p[i] = po;
+}
+
+// the same update, four elements per thread (16-byte aligned slabs; each lane's arithmetic is the scalar
+// kernel's, so the results are bit-identical): one 16-byte load / store per operand instead of four
+__global__ void adam4_kernel(int64_t n4, float4* __restrict__ p, const float4* __restrict__ g, float4* __restrict__ m,
+                             float4* __restrict__ v, float b1, float b2, float eps, float wd, float step_size,
+                             float bc2_sqrt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const float4 gi = g[i], pi = p[i];
+  float4 mi = m[i], vi = v[i], po;
+  po.x = adam_one(gi.x, pi.x, mi.x, vi.x, b1, b2, eps, wd, step_size, bc2_sqrt);
+  po.y = adam_one(gi.y, pi.y, mi.y, vi.y, b1, b2, eps, wd, step_size, bc2_sqrt);
+  po.z = adam_one(gi.z, pi.z, mi.z, vi.z, b1, b2, eps, wd, step_size, bc2_sqrt);
+  po.w = adam_one(gi.w, pi.w, mi.w, vi.w, b1, b2, eps, wd, step_size, bc2_sqrt);
+  m[i] = mi;
+  v[i] = vi;
+  p[i] = po;
 }
 
 }  // namespace
@@ -31,9 +57,22 @@ extern "C" int gmr_adam_f32(int64_t n, float* param, const float* grad, float* e
                             void* stream) {
   GMR_ARG(param && grad && exp_avg && exp_avg_sq && n >= 0, "bad args");
   if (n == 0) return GMR_OK;
-  hipLaunchKernelGGL(adam_kernel, dim3(gmr::grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, param, grad, exp_avg,
-                     exp_avg_sq, beta1, beta2, eps, weight_decay, step_size, bias_correction2_sqrt);
-  GMR_LAUNCHED();
+  hipStream_t st = (hipStream_t)stream;
+  const bool al = (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) == 0;
+  const int64_t n4 = al ? n / 4 : 0;
+  if (n4 > 0) {
+    hipLaunchKernelGGL(adam4_kernel, dim3(gmr::grid_for(n4, 256)), dim3(256), 0, st, n4,
+                       reinterpret_cast<float4*>(param), reinterpret_cast<const float4*>(grad),
+                       reinterpret_cast<float4*>(exp_avg), reinterpret_cast<float4*>(exp_avg_sq), beta1, beta2, eps,
+                       weight_decay, step_size, bias_correction2_sqrt);
+    GMR_LAUNCHED();
+  }
+  const int64_t t0 = 4 * n4;  // scalar tail (or the whole range when a pointer is not 16-byte aligned)
+  if (t0 < n) {
+    hipLaunchKernelGGL(adam_kernel, dim3(gmr::grid_for(n - t0, 256)), dim3(256), 0, st, n - t0, param + t0, grad + t0,
+                       exp_avg + t0, exp_avg_sq + t0, beta1, beta2, eps, weight_decay, step_size, bias_correction2_sqrt);
+    GMR_LAUNCHED();
+  }
   return GMR_OK;
 }
 

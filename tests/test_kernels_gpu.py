@@ -369,6 +369,28 @@ def test_adam_vs_torch(K):
     np.testing.assert_allclose(p.cpu().numpy(), want, rtol=3e-7, atol=1e-7)  # fp32 contraction: <= 1 ulp
 
 
+@pytest.mark.parametrize("n", [1003, 4096, 3])
+def test_adam_vector_path_bit_exact(K, n):
+    """gmr_adam_f32's float4 kernel (16-byte aligned operands) against its scalar kernel (the same buffers
+    offset by one element, so unaligned): p, m and v bit for bit over a few steps with weight decay; n not a
+    multiple of four exercises the scalar tail."""
+    rng = _rng(9)
+    p0 = rng.standard_normal(n).astype(np.float32)
+    gs = [rng.standard_normal(n).astype(np.float32) for _ in range(3)]
+    out = []
+    for off in (0, 1):  # the same n values at element offset 0 (aligned) and 1 (unaligned)
+        sl = slice(off, off + n)
+        p, m, v = (torch.zeros(n + 1, device=DEV) for _ in range(3))
+        p[sl] = _dev(p0)
+        for i, g in enumerate(gs):
+            gd = torch.zeros(n + 1, device=DEV)
+            gd[sl] = _dev(g)
+            K.adam(p[sl], gd[sl], m[sl], v[sl], 1e-3, 0.9, 0.999, 1e-8, 0.01, i + 1)
+        out.append([t[sl].cpu() for t in (p, m, v)])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 def test_normalize_rows_and_bwd(K):
     torch.manual_seed(3)
     x = torch.randn(333, 128)
