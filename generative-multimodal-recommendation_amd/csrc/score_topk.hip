@@ -133,7 +133,7 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
   // the lane's output rows are row0 + 4 grp + e (MFMA C/D map: row = 4 (lane >> 4) + reg, col = lane & 15)
   int64_t mc[4], me[4];
   int nm[4];
-  float tau[4];  // per row: the k-th best score so far (-inf until k entries are held)
+  float tau[4];  // per row: the k-th best score so far (NaN until the first compaction: every item enters)
   int cnt[4];  // entries in the buffers of the lane's rows (the same in the 16 lanes of a row group)
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -141,7 +141,9 @@ __device__ __forceinline__ void score_topk_wave(int64_t n_rows, int64_t row0, in
     mc[e] = r < n_rows ? mptr[r] : 0;
     me[e] = r < n_rows ? mptr[r + 1] : 0;
     nm[e] = mc[e] < me[e] ? mask_at(mc[e]) : 0x7fffffff;
-    tau[e] = -__builtin_inff();
+    // NaN, not -inf: !(s <= NaN) admits every item, a -inf score (a caller's -inf fill) included, until
+    // the first compaction has k entries and sets tau to the k-th of them
+    tau[e] = __builtin_nanf("");
     cnt[e] = 0;
   }
   // items [c0, c0 + 64): this lane's 16 consecutive k of item c0 + 16 t + col (clamped: the loads of

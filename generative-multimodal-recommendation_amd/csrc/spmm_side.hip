@@ -544,7 +544,9 @@ SideLayout side_layout(const SidePlanHost& p, int64_t nnz) {
   l.perm = l.cls + 4 * (int64_t)p.cls.size();
   l.dsto = l.perm + (int64_t)p.perm.size();
   l.packb = r4(l.dsto + (int64_t)p.dsto.size());
-  l.words = l.packb + 2 * p.short_entries;
+  // 4 zero words past the packed entries: the degree-class job loader issues its perm / packedB loads
+  // from clamped indices even when the plan has no class rows (H_NSR == 0), and then they land here
+  l.words = l.packb + 2 * p.short_entries + 4;
   return l;
 }
 
@@ -660,6 +662,7 @@ extern "C" int gmr_spmm_side_plan_build(const int32_t* rowptr_host, int64_t n_ro
   for (size_t i = 0; i < p.dsto.size(); ++i) h[l.dsto + i] = p.dsto[i];
   for (int64_t i = l.packed + 2 * nnz; i < l.cls; ++i) h[i] = 0;
   for (int64_t i = l.dsto + (int64_t)p.dsto.size(); i < l.packb; ++i) h[i] = 0;
+  for (int64_t i = l.packb + 2 * p.short_entries; i < l.words; ++i) h[i] = 0;
   int4* t = reinterpret_cast<int4*>(h + l.task);
   for (int s = 0; s < 2; ++s)
     for (const int4& x : p.tasks[s]) *t++ = x;

@@ -397,7 +397,7 @@ class CSR:
         # the 64-column products fill the XCDs with 128, the wider norm_adj products with 256
         short = self.nnz < 4 * self.n_rows
         self.side_wpx = {1: 128, 2: 128, 4: 128 if short else 256}
-        self.side_hdr = tuple(int(x) for x in host[:16])
+        self.side_hdr = tuple(int(x) for x in host[:27])  # csrc/spmm_side.hip H_MAGIC .. H_NSE
         self.partial = torch.zeros(max(nsc, self.partial.numel()), dtype=torch.float32, device=dev)
 
     def spmm(self, out, blocks, split=None, alpha=1.0, beta=0.0, partial=None):

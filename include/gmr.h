@@ -489,6 +489,8 @@ int gmr_nce_rows_f32(int64_t B, float* L, int64_t ld, float coef, float* loss, v
 /* the same for a data-parallel rank's block: rows [diag_off, diag_off + rows) of the global batch
  * against all cols keys (row r's positive at column diag_off + r; genrecv1.py:407-414 over the
  * global batch) */
+int gmr_nce_rows_off_f32(int64_t rows, int64_t cols, float* L, int64_t ld, int64_t diag_off, float coef, float* loss,
+                         void* stream);
 /* GenRecV1's in-batch InfoNCE terms through gmr_contrast_fused_f32 (round 4; genrecv1.py:389-397): term k
  * pairs the normalised query table i1[k] with key table i2[k] of nv [4][tab][64] (i1 / i2: host arrays of
  * nterms <= 4 entries; Bg rows used per table).  gmr_nce_pairs_f32 writes the (query, positive) pair rows
@@ -500,8 +502,6 @@ int gmr_nce_pairs_f32(int32_t nterms, int64_t B, int64_t Bg, int64_t row0, const
 int gmr_nce_combine_f32(int32_t nterms, int64_t B, int64_t Bg, int64_t row0, const int32_t* i1, const int32_t* i2,
                         const float* contrib, int64_t ct, const float* dT, int64_t dts, float* g, int64_t tab,
                         void* stream);
-int gmr_nce_rows_off_f32(int64_t rows, int64_t cols, float* L, int64_t ld, int64_t diag_off, float coef, float* loss,
-                         void* stream);
 /* BPR with log-sigmoid (:377-380) over one (U + I) x 64 table; contrib = [dU; dP; dN] */
 int gmr_bpr_logsigmoid_f32(int32_t B, int64_t U, const float* C, const int32_t* users, const int32_t* pos,
                            const int32_t* neg, float* loss, float* contrib, float inv_norm, void* stream);

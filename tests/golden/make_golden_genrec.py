@@ -531,9 +531,66 @@ def main_tiktok():
     print("wrote", os.path.join(OUT, "genrecv1_tiktok.npz"), meta["valid"]["rounded"])
 
 
+def label_inertia(Z, labels):
+    """Sum over points of the squared distance to their cluster's mean (fp64): the K-means objective of a
+    partition, the same figure for the reference's labels and the device K-means' labels."""
+    Z = np.asarray(Z, np.float64)
+    tot = 0.0
+    for c in np.unique(labels):
+        P = Z[labels == c]
+        tot += float(((P - P.mean(0)) ** 2).sum())
+    return tot
+
+
+def main_kmeans():
+    """G6 / (f)3 K-means on the configuration's own data (VERDICT r4 missing #4): the reference's
+    MultimodalCluster.multimodal_specific_cluster (common/interest_cluster.py:60-79: StandardScaler, then
+    sklearn KMeans(n_clusters=k).fit(...).labels_) on the TikTok-shaped item features of
+    test_genrec_tiktok_gpu.py (gmr/synthetic.py 'tiktok', seed 0: image 6,710 x 128, text 6,710 x 768) with
+    the TikTok cluster counts of GenRecV1Trainer._init_interest_clustering (common/trainer.py:611-671:
+    image 18, text 59).  The reference's KMeans is unseeded (random_state None: numpy's global RNG), so
+    the clustering is run under five global seeds (np.random.seed(999 + s)); stored: the labels of seed
+    999 and, per seed, the partition's inertia (sum of squared distances to the cluster means of the
+    standardized features).  The device K-means is pinned statistically: its partition's inertia must fall
+    within 1 % of the reference's range."""
+    ref = _import_reference()
+    import sklearn
+    import torch
+    ROOT = os.path.dirname(os.path.dirname(HERE))
+    sys.path.insert(0, os.path.join(ROOT, "generative-multimodal-recommendation_amd"))
+    from gmr.synthetic import SHAPES, make_features
+    import common.interest_cluster as ic
+    U, I, n, dv, dt = SHAPES["tiktok"]
+    v, t = make_features(I, dv, dt, 0, gaussian=True)
+    mc = ic.MultimodalCluster(num_cluster_visual_modal=20, num_cluster_text_modal=20, num_cluster_audio_modal=20,
+                              num_cluster_fusion_modal=20, kmeans_cluster_num=20, spectral_cluster_num=20,
+                              sim_top_k=20, use_auto_optimal_k=False, kmeans_cluster_num_min=3,
+                              kmeans_cluster_num_mean=7, kmeans_cluster_num_max=237, kmeans_stride=10)
+    meta = {"I": I, "numpy": np.__version__, "sklearn": sklearn.__version__, "torch": torch.__version__,
+            "generator": "tests/golden/make_golden_genrec.py kmeans", "reference": REF_SRC, "modal": {}}
+    out = {}
+    for key, feats, k in (("image", v, 18), ("text", t, 59)):
+        Z = mc.stand_norm.fit_transform(np.asarray(feats, np.float32))
+        inert = []
+        for s in range(5):
+            np.random.seed(999 + s)
+            lab = mc.multimodal_specific_cluster(torch.from_numpy(np.asarray(feats, np.float32)), key + "_modal", k)
+            inert.append(label_inertia(Z, lab))
+            if s == 0:
+                out[f"{key}_labels"] = lab.astype(np.int8)
+        meta["modal"][key] = {"k": k, "inertia": inert, "n_clusters_used": int(len(np.unique(out[f"{key}_labels"])))}
+        print(key, k, inert)
+    np.savez_compressed(os.path.join(OUT, "kmeans_tiktok.npz"), **out)
+    with open(os.path.join(OUT, "kmeans_tiktok_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1, default=float)
+    print("wrote", os.path.join(OUT, "kmeans_tiktok.npz"))
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "tiktok":
         return main_tiktok()
+    if len(sys.argv) > 1 and sys.argv[1] == "kmeans":
+        return main_kmeans()
     ref = _import_reference()
     import torch
     import sklearn

@@ -963,6 +963,48 @@ def test_spmm_side_vs_fp64_and_lane(K, nb, self_loops, classes):
     assert torch.equal(y2.view(torch.int32), ys.view(torch.int32))
 
 
+@pytest.mark.parametrize("classes", [True, False])
+def test_spmm_side_all_hub_rows_split_blocks(K, classes):
+    """Every row a hub row: users of degree 17-40 (one wave block each)
+    and item rows of degree ~400-550, split into 2-3 wave blocks of 8 TW = 256 entries whose partial sums
+    meet through the relaxed agent-scope counter hand-off (csrc/spmm_side.hip, hub publish / last-block
+    sum); d = 64 and d = 128.  The degree-class plan then holds no class rows (H_NSR = 0: the job
+    loader's clamped loads land in the plan's zero pad).  Checked: fp64 within 1e-6, and bit-identical
+    across four launches and with a second scratch (the counters re-arm, the block order is fixed)."""
+    rng = _rng(47)
+    U, I = 2000, 120
+    N = U + I
+    deg = rng.integers(17, 41, size=U)
+    rows = np.repeat(np.arange(U), deg)
+    cols = np.concatenate([rng.choice(I, size=d, replace=False) for d in deg])
+    rp, col, val = graph_ref.norm_adj_csr(U, I, rows, cols)
+    d_all = np.diff(rp)
+    assert d_all.min() > 16 and d_all[U:].min() > 256  # every item row spans >= 2 wave blocks
+    gs = K.CSR(_dev(rp), _dev(col), _dev(val), class_split=U, side=True)
+    gs.build_side_plan(U, classes=classes)
+    assert gs.side_hdr[24] == 0  # H_NSR: no short rows in the plan
+    a = np.zeros((N, N))
+    a[np.repeat(np.arange(N), d_all), col] = val
+    for nb in (1, 2):
+        X = rng.standard_normal((N, 64 * nb)).astype(np.float32)
+        Xd = _dev(X)
+        blocks = [(Xd[:, 64 * b:64 * (b + 1)],) for b in range(nb)]
+        outs = []
+        for _ in range(4):
+            y = torch.empty((N, 64 * nb), device=DEV)
+            gs.spmm(y, blocks)
+            outs.append(y)
+        want = a @ X.astype(np.float64)
+        scale = np.abs(a) @ np.abs(X.astype(np.float64)) + 1e-6
+        err = np.abs(outs[0].cpu().numpy() - want) / scale
+        assert err.max() <= 1e-6, err.max()
+        for y in outs[1:]:
+            assert torch.equal(y.view(torch.int32), outs[0].view(torch.int32))
+        y2 = torch.empty((N, 64 * nb), device=DEV)
+        gs.spmm(y2, blocks, partial=torch.zeros_like(gs.partial))
+        assert torch.equal(y2.view(torch.int32), outs[0].view(torch.int32))
+
+
 def test_spmm_side_multi_outputs_and_jobs(K):
     """spmm_multi / spmm_jobs on side plans: per-block outputs equal the one-output product, and a
     jobs launch mixing a side-plan matrix with a lane-plan one equals the separate calls."""

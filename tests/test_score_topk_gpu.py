@@ -45,14 +45,14 @@ def _expected(scores, rows, k, fill=-1e10):
     return out, s
 
 
-def _run(U, I, users, ptr, cols, k, want_val=False):
+def _run(U, I, users, ptr, cols, k, want_val=False, fill=-1e10):
     from gmr import kernels as K
     n = len(users) if users is not None else U.shape[0]
     out = torch.full((n, k), -7, dtype=torch.int32, device=DEV)
     val = torch.zeros((n, k), dtype=torch.float32, device=DEV) if want_val else None
     ut = torch.as_tensor(users, dtype=torch.int32, device=DEV) if users is not None else None
     K.score_topk(torch.as_tensor(U, device=DEV), torch.as_tensor(I, device=DEV), ut,
-                 torch.as_tensor(ptr, device=DEV), torch.as_tensor(cols, device=DEV), k, out, val)
+                 torch.as_tensor(ptr, device=DEV), torch.as_tensor(cols, device=DEV), k, out, val, fill=fill)
     torch.cuda.synchronize()
     return out.cpu().numpy(), (val.cpu().numpy() if want_val else None)
 
@@ -72,6 +72,27 @@ def test_integer_embeddings_exact(D, n_items, k, n_rows):
     got, val = _run(U, I, users, ptr, cols, k, want_val=True)
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(val, np.take_along_axis(s, want, 1).astype(np.float32))
+
+
+@pytest.mark.parametrize("D,n_items,k", [(64, 1000, 50), (128, 300, 64), (64, 7050, 50)])
+def test_minus_inf_fill_with_rows_short_of_k(D, n_items, k):
+    """fill = -inf (torch's usual masking value): masked items score -inf and must still reach
+    the top-k of a row that has fewer than k unmasked items (row 1: n_items - 10 masked), ties among them
+    to the lowest index, with every returned index valid and the value -inf."""
+    rng = np.random.default_rng(D + n_items)
+    n_rows = 37
+    U = rng.integers(-3, 4, size=(n_rows, D)).astype(np.float32)
+    I = rng.integers(-3, 4, size=(n_items, D)).astype(np.float32)
+    rows, ptr, cols = _mask(rng, n_rows, n_items, min(40, n_items - k), full_row=1)
+    rows[3] = np.arange(n_items, dtype=np.int32)  # a row with every item masked
+    ptr = np.concatenate([[0], np.cumsum([len(x) for x in rows])]).astype(np.int64)
+    cols = np.concatenate(rows).astype(np.int32)
+    want, s = _expected(U.astype(np.int64) @ I.T.astype(np.int64), rows, k, fill=-np.inf)
+    got, val = _run(U, I, None, ptr, cols, k, want_val=True, fill=float("-inf"))
+    assert got.min() >= 0 and got.max() < n_items
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(val, np.take_along_axis(s, want, 1).astype(np.float32))
+    assert np.isneginf(val[1, 10:]).all() and np.isneginf(val[3]).all()
 
 
 def test_users_none_and_empty_masks():
