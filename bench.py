@@ -54,8 +54,8 @@ FP32_MFMA_PEAK_TFS = 157.3
 # 1,024 flop/clk x 2.4 GHz = 2,516.6 TF/s, MI355X_MICROARCH.md) / 6
 X6_PEAK_TFS = round(2516.6 / 6, 1)
 KERNEL_NAMES = {"gemm": "gemm_glds_kernel (fp32 MFMA v_mfma_f32_32x32x2_f32, global_load_lds staging, XCD-aware tiles)",
-                "gemm_x6": "gemm_x6_kernel + gemm_p3_kernel (fp32 operands split exactly into three bf16 terms - on the "
-                           "way into LDS, or once by their producers for the rebuild's p_sample products - six "
+                "gemm_x6": "gemm_x6_kernel (fp32 operands split exactly into three bf16 terms on the "
+                           "way into LDS, six "
                            "v_mfma_f32_32x32x16_bf16 products accumulated in fp32: fp32-accurate NT products)",
                 "infonce": "cl6_kernel rows + table passes (fused InfoNCE on the split-bf16 pipe: fp32 operands split "
                            "exactly into three bf16 terms, six v_mfma_f32_32x32x16_bf16 products, fp32 accumulation)",

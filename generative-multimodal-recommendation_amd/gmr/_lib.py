@@ -64,8 +64,6 @@ SIGNATURES = {
     "gmr_gemm_f32": (I32, [I32, I32, I64, I64, I64, F32, P, I64, P, I64, F32, P, I64, I32, P, P, I64, P, I64, P, P,
                            F32, I32, I32, P, I64, P]),
     "gmr_split3_planes": (I32, [I64, I64, P, I64, P, I64, I64, P]),
-    "gmr_gemm_p3_f32": (I32, [I64, I64, I64, F32, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, I32, P, P, I64, P,
-                              I64, I64, F32, F32, I32, P]),
     "gmr_dmm_combine_fwd": (I32, [I64, P, P, P, P, P, F32, P, P]),
     "gmr_dmm_final_fwd": (I32, [I64, P, P, F32, P, P, P]),
     "gmr_dmm_cl_fwd": (I32, [I64, P, P, P, P, P, P]),

@@ -24,14 +24,6 @@ def _r4(n):
     return (n + 3) // 4 * 4
 
 
-# GMR_P3=1: the graph rebuild's p_sample products from pre-split operands (gmr_gemm_p3_f32: the weights split
-# once per rebuild, x and h carried as bf16 plane sets by the products' epilogues).  Opt-in: faster alone
-# (hidden product 1.70 -> 1.52 ms) but the plane sets carry 6 bytes per element where fp32 carries 4, and
-# with the image and text sweeps running concurrently the rebuild phase takes 37.3 ms vs 33.0 ms for the
-# default split-bf16 GEMM that splits fp32 operands on the fly (gemm_x6; profiles/r04j_ab.txt)
-P3 = os.environ.get("GMR_P3", "0") != "0"
-
-
 class _Linear(nn.Module):
     def __init__(self, weight, bias):
         super().__init__()
@@ -105,24 +97,7 @@ class Denoiser(nn.Module):
             self._w1t = torch.empty((self.I, _r4(self.H)), device=self.device)[:, :self.H]
         _lib.call("gmr_transpose_f32", self.H, self.I, ptr(self.slab.view("W1")), self.ld_w1, ptr(self._w1t),
                   self._w1t.stride(0), stream())
-        if P3:
-            if getattr(self, "_w1p", None) is None:
-                self._w1p = K.Planes(self.H, self.I, self.device)
-                self._w2p = K.Planes(self.I, self.H, self.device)
-            self._w1p.load(self.W1x())
-            self._w2p.load(self.slab.view("W2"))
         return self._w1t
-
-    def hidden_p3(self, xp, B, hp, eb_row):
-        """h = tanh(x @ W1[:, :I]^T + eb_row) from the plane set of x into the plane set of h."""
-        K.gemm_p3(xp, self._w1p, B, C_planes=hp, epi=K.EPI_BIAS_TANH, bias=eb_row)
-        return hp
-
-    def posterior_p3(self, hp, B, c1, c2, x=None, xp_in=None, x_out=None, xp_out=None):
-        """x <- c1 * (h @ W2^T + b2) + c2 * x from the plane set of h; x read as fp32 (x) or planes (xp_in),
-        written as fp32 (x_out) and / or planes (xp_out) — in place allowed."""
-        K.gemm_p3(hp, self._w2p, B, C=x_out, C_planes=xp_out, epi=K.EPI_POSTERIOR, bias=self.slab.view("b2"),
-                  aux=x, aux_planes=xp_in, slope=c1, beta=c2)
 
     def hidden_sparse(self, users, user_ptr, user_items, h, eb_row):
         """h = tanh(x0 @ W1[:, :I]^T + eb_row) for binary x0 rows given as the users' item lists

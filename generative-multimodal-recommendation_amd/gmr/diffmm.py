@@ -601,23 +601,7 @@ class DiffMM(GeneralRecommender):
         if not w1t_fresh:
             den.refresh_w1t()
         xi = x[:, :I]
-        if dn.P3:
-            # pre-split products: x and h travel as bf16 plane sets between the steps (gmr_gemm_p3_f32);
-            # the first posterior reads the binary x0 (fp32), the last one writes fp32 x for the top-k
-            if "xp" not in w:
-                w["xp"] = K.Planes(w["B"], I, self.device)
-                w["hp"] = K.Planes(w["B"], den.H, self.device)
-            xp, hp = w["xp"], w["hp"]
-            for i in reversed(range(T)):
-                c1, c2 = float(np.float32(self.tables["c1"][i])), float(np.float32(self.tables["c2"][i]))
-                if i == T - 1:
-                    den.hidden_sparse(users, self.user_ptr, self.user_items, h, EB[i])
-                    hp.load(h)
-                else:
-                    den.hidden_p3(xp, B, hp, EB[i])
-                den.posterior_p3(hp, B, c1, c2, x=xi if i == T - 1 else None, xp_in=xp if i < T - 1 else None,
-                                 x_out=xi if i == 0 else None, xp_out=xp if i > 0 else None)
-        for i in reversed(range(T)) if not dn.P3 else ():
+        for i in reversed(range(T)):
             if i == T - 1:  # the first model call sees the binary history: sparse hidden layer
                 den.hidden_sparse(users, self.user_ptr, self.user_items, h, EB[i])
             else:

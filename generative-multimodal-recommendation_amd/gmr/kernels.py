@@ -242,7 +242,7 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
 class Planes:
     """A plane set (include/gmr.h gmr_split3_planes): an fp32 matrix of `rows` x `cols` held as three bf16
     planes [3][rows][ld] (x = hi + mid + lo exactly), ld = cols rounded up to 32, pad columns zero.  The
-    operand / output form of the pre-split GEMM (gmr_gemm_p3_f32)."""
+    item-table form of the split-bf16 fused eval (gmr_score_topk_x6)."""
 
     def __init__(self, rows, cols, device):
         self.rows, self.cols = int(rows), int(cols)
@@ -267,29 +267,6 @@ class Planes:
         p = self.t[:, :, :self.cols].to(torch.int32) << 16
         f = p.view(torch.float32) if p.is_contiguous() else p.contiguous().view(torch.float32)
         return (f[0] + f[1]) + f[2]
-
-
-def gemm_p3(A, B, M, C=None, C_planes=None, alpha=1.0, epi=EPI_NONE, bias=None, aux=None, aux_planes=None,
-            slope=0.0, beta=0.0, tile=0):
-    """C[:M] = epi(alpha * A[:M] @ B^T) from plane sets A (M rows used) and B (N = B.rows), fp32 C and / or
-    output planes (include/gmr.h gmr_gemm_p3_f32)."""
-    N = B.rows
-    if A.ld != B.ld:
-        raise ValueError(f"plane sets of different padded k: {A.ld} vs {B.ld}")
-    if M > A.rows or (C_planes is not None and (C_planes.rows < M or C_planes.cols != N)):
-        raise ValueError("gemm_p3: row / column counts do not match")
-    if C is not None and (C.shape[0] < M or C.shape[1] != N or C.dtype != torch.float32):
-        raise ValueError("gemm_p3: C must be fp32 with >= M rows and N columns")
-    if aux_planes is not None and (aux_planes.rows < M or aux_planes.cols != N):
-        raise ValueError("gemm_p3: aux planes must be M x N")
-    with _Probe("gemm_x6" if _probe is not None else "gemm", (M, N, A.cols, 0, 1, epi)):
-        _lib.call("gmr_gemm_p3_f32", M, N, A.ld, float(alpha), A.ptr(), A.ld, A.ps, B.ptr(), B.ld, B.ps, ptr(C),
-                  _ld(C) if C is not None else 0, C_planes.ptr() if C_planes is not None else None,
-                  C_planes.ld if C_planes is not None else 0, C_planes.ps if C_planes is not None else 0, epi,
-                  ptr(bias), ptr(aux), _ld(aux) if aux is not None else 0,
-                  aux_planes.ptr() if aux_planes is not None else None, aux_planes.ld if aux_planes is not None else 0,
-                  aux_planes.ps if aux_planes is not None else 0, float(slope), float(beta), int(tile), stream())
-    return C
 
 
 # ----------------------------------------------------------------------------- SpMM

@@ -243,23 +243,13 @@ int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t
                  const float* rowvec1, const float* rowvec2, float slope, int32_t tile, int32_t split_k,
                  float* workspace, int64_t workspace_floats, void* stream);
 
-/* Pre-split operands (csrc/gemm_p3.hip; the graph rebuild's p_sample products, models/diffmm.py:352-358,
- * 408-451, common/trainer.py:529-546).  A plane set is three bf16 matrices (uint16 storage) [3][rows][ld]
- * with plane stride ps: x = hi + mid + lo exactly for every fp32 x (the split of GMR_GEMM_X6); ld is a
- * multiple of 32 and the columns [cols, ld) are zero.  gmr_split3_planes writes one from an fp32 matrix.
- * gmr_gemm_p3_f32: C[M,N] = epilogue(alpha * A B^T) with A (M x Kp) and B (N x Kp) given as plane sets
- * (Kp = their padded k, a multiple of 32, 16-byte aligned planes, ld % 8 == 0), six bf16 MFMA products
- * per 32x32x16 block (fp32-accurate, as GMR_GEMM_X6); output as fp32 C (ldc % 4 == 0, 16-byte aligned)
- * and / or as a plane set C_planes (ldcp % 4 == 0: a later product's operand).  Epilogues NONE, BIAS,
- * BIAS_TANH, POSTERIOR (c1 = slope, c2 = beta; aux as fp32 or as planes aux_planes — in place over
- * C_planes is allowed).  tile: 0 = by shape, 1 = 256 x 128, 2 = 128^2 double-buffered, 3 = 128^2. */
+/* bf16 plane sets (csrc/planes.hip): an fp32 matrix as three bf16 matrices (uint16 storage) [3][rows][ld]
+ * with plane stride ps, x = hi + mid + lo exactly for every fp32 x (the split of GMR_GEMM_X6); ld is a
+ * multiple of 32 and the columns [cols, ld) are zero.  gmr_split3_planes writes one from an fp32 matrix
+ * (the item table of gmr_score_topk_x6).  (Round 4's pre-split GEMM gmr_gemm_p3_f32 was removed in round 5:
+ * slower in the epoch and less accurate at K = 7,050 than the on-the-fly split of gmr_gemm_f32.) */
 int gmr_split3_planes(int64_t rows, int64_t cols, const float* src, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
                       int64_t plane_stride, void* stream);
-int gmr_gemm_p3_f32(int64_t M, int64_t N, int64_t Kp, float alpha, const uint16_t* A, int64_t lda, int64_t psa,
-                    const uint16_t* B, int64_t ldb, int64_t psb, float* C, int64_t ldc, uint16_t* C_planes,
-                    int64_t ldcp, int64_t pscp, int32_t epilogue, const float* bias, const float* aux, int64_t ld_aux,
-                    const uint16_t* aux_planes, int64_t ld_auxp, int64_t ps_auxp, float slope, float beta,
-                    int32_t tile, void* stream);
 
 /* ---------------------------------------------------------------- DiffMM rec step (diffmm.py:129-258)
  * Fused row kernels of forward_MM / forward_cl_MM / calculate_loss and their backward
@@ -420,7 +410,7 @@ int gmr_score_topk_f32(int64_t n_rows, const int32_t* users, const float* user_t
                        float* out_val, void* stream);
 /* The same with the scores on the bf16 matrix cores (round 4): the item table as a plane set
  * (gmr_split3_planes: item_planes[p * plane_stride + i * ld_plane + c], x = hi + mid + lo exactly) and
- * the six-product split of gmr_gemm_p3_f32 (fp32-accurate sums, 2.7x the fp32 MFMA rate); the user
+ * the six-product split of GMR_GEMM_X6 (fp32-accurate sums, 2.7x the fp32 MFMA rate); the user
  * table stays fp32 and is split in registers.  dim 64; ld_plane a multiple of 8. */
 int gmr_score_topk_x6(int64_t n_rows, const int32_t* users, const float* user_table, int64_t ld_user, int64_t n_items,
                       const uint16_t* item_planes, int64_t ld_plane, int64_t plane_stride, int64_t dim,

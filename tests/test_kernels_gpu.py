@@ -753,89 +753,6 @@ def test_split3_planes_exact(K):
     assert (p.t[:, :, 70:] == 0).all() and (p.t[:, 37:] == 0).all()
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
-def test_gemm_p3_fp32_accuracy_and_bits(K, tile):
-    """Pre-split products (gmr_gemm_p3_f32): the same six bf16 MFMA products per 32x32x16 block as the
-    split-bf16 kernel on operands the producers split once.  Accuracy against fp64 <= 6e-7 (and within 1.25x
-    the fp32-MFMA kernel's error up to K ~ 1,000: one unsplit chain) on ragged M / N (N % 4 != 0), K not a
-    multiple of 32 (zero pad columns), values spanning 2^-20 .. 2^20; on the same tile the sums are the
-    split-bf16 kernel's (without split-K) bit for bit (same split, same MFMA order, zero-padded last k tile)."""
-    rng = _rng(41)
-    for M, N, Kd in ((300, 200, 1000), (517, 262, 70), (19, 34, 7), (1000, 702, 7050), (600, 1000, 1001)):
-        a = (rng.standard_normal((M, Kd)) * np.exp2(rng.integers(-20, 21, size=(M, 1)))).astype(np.float32)
-        b = rng.standard_normal((N, Kd)).astype(np.float32)
-        pad4 = lambda x: np.pad(x, ((0, 0), (0, (-x.shape[1]) % 4)))  # noqa: E731
-        A, B = _dev(pad4(a))[:, :Kd], _dev(pad4(b))[:, :Kd]
-        Ap, Bp = K.Planes(M, Kd, DEV).load(A), K.Planes(N, Kd, DEV).load(B)
-        a64, b64 = A.double(), B.double()
-        ref, scale = a64 @ b64.t(), a64.abs() @ b64.abs().t()
-        C = torch.empty(M, (N + 3) // 4 * 4, device=DEV)[:, :N]
-        Cp = K.Planes(M, N, DEV)
-        K.gemm_p3(Ap, Bp, M, C=C, C_planes=Cp, tile=tile)
-        e_p3 = ((C.double() - ref).abs() / scale).max().item()
-        Cf = torch.empty(M, N, device=DEV)
-        K.gemm(A, B, Cf, trans_b=True, tile=F32)
-        e_f32 = ((Cf.double() - ref).abs() / scale).max().item()
-        # one unsplit accumulation chain over K (the split kernel's tests run K = 7,050 with split-K slabs): the
-        # fp32-MFMA ratio bar holds to K ~ 1,000; at K = 7,050 the absolute fp32-accuracy bar
-        assert e_p3 <= X6_ABS, (M, N, Kd, e_p3, e_f32)
-        if Kd <= 1001:
-            assert e_p3 <= X6_RATIO * e_f32 + X6_FLOOR, (M, N, Kd, e_p3, e_f32)
-        assert torch.equal(Cp.to_float(), C)  # the planes output is the fp32 output, split exactly
-        if tile in (1, 3):  # the split kernel on the same tile: identical sums
-            x6t = 256128 if tile == 1 else 128
-            Cx = torch.empty(M, N, device=DEV)
-            K.gemm(A, B, Cx, trans_b=True, tile=x6t | X6, split_k=1)
-            assert torch.equal(Cx, C), (M, N, Kd, (Cx - C).abs().max().item())
-
-
-def test_gemm_p3_epilogues(K):
-    """The p_sample chain on plane sets: BIAS_TANH into planes, then POSTERIOR reading its x from planes IN
-    PLACE (and from fp32 x), writing planes or fp32 — each equal, bit for bit, to the split-bf16 kernel's
-    fp32 epilogue on the same tile."""
-    rng = _rng(42)
-    M, H, I = 700, 1000, 1502
-    x = (rng.random((M, I)) < 0.01).astype(np.float32)
-    W1 = (rng.standard_normal((H, I)) * 0.03).astype(np.float32)
-    W2 = (rng.standard_normal((I, H)) * 0.03).astype(np.float32)
-    eb = _dev(rng.standard_normal(H).astype(np.float32))
-    b2 = _dev(rng.standard_normal(I).astype(np.float32))
-    # 16-byte rows (ld % 4 == 0) so the reference calls take the split-bf16 kernel, not the fp32 fallback
-    X, W1d, W2d = _dev(np.pad(x, ((0, 0), (0, 2))))[:, :I], _dev(np.pad(W1, ((0, 0), (0, 2))))[:, :I], _dev(W2)
-    Xp, W1p, W2p = K.Planes(M, I, DEV).load(X), K.Planes(H, I, DEV).load(W1d), K.Planes(I, H, DEV).load(W2d)
-    for tile, x6t in ((1, 256128), (3, 128)):
-        hp = K.Planes(M, H, DEV)
-        K.gemm_p3(Xp, W1p, M, C_planes=hp, epi=K.EPI_BIAS_TANH, bias=eb, tile=tile)
-        h_ref = torch.empty(M, H, device=DEV)
-        K.gemm(X, W1d, h_ref, trans_b=True, epi=K.EPI_BIAS_TANH, bias=eb, tile=x6t | X6, split_k=1)
-        assert torch.equal(hp.to_float(), h_ref)
-        # posterior from fp32 x into planes, then from planes in place, then into fp32
-        xp = K.Planes(M, I, DEV)
-        K.gemm_p3(hp, W2p, M, C_planes=xp, epi=K.EPI_POSTERIOR, bias=b2, aux=X, slope=0.3, beta=0.6, tile=tile)
-        x_ref = X.clone()
-        K.gemm(h_ref, W2d, x_ref, trans_b=True, epi=K.EPI_POSTERIOR, bias=b2, aux=x_ref, slope=0.3, beta=0.6,
-               tile=x6t | X6, split_k=1)
-        assert torch.equal(xp.to_float(), x_ref)
-        K.gemm_p3(hp, W2p, M, C_planes=xp, epi=K.EPI_POSTERIOR, bias=b2, aux_planes=xp, slope=0.2, beta=0.7,
-                  tile=tile)
-        K.gemm(h_ref, W2d, x_ref, trans_b=True, epi=K.EPI_POSTERIOR, bias=b2, aux=x_ref, slope=0.2, beta=0.7,
-               tile=x6t | X6, split_k=1)
-        assert torch.equal(xp.to_float(), x_ref)
-        out = torch.empty(M, I + 2, device=DEV)[:, :I]
-        K.gemm_p3(hp, W2p, M, C=out, epi=K.EPI_POSTERIOR, bias=b2, aux_planes=xp, slope=0.5, beta=0.4, tile=tile)
-        K.gemm(h_ref, W2d, x_ref, trans_b=True, epi=K.EPI_POSTERIOR, bias=b2, aux=x_ref, slope=0.5, beta=0.4,
-               tile=x6t | X6, split_k=1)
-        assert torch.equal(out, x_ref)
-
-
-def test_gemm_p3_bad_arguments(K):
-    from gmr import _lib
-    a = K.Planes(64, 64, DEV)
-    with pytest.raises(RuntimeError):
-        _lib.call("gmr_gemm_p3_f32", 64, 64, 48, 1.0, a.ptr(), a.ld, a.ps, a.ptr(), a.ld, a.ps, None, 0, None, 0, 0,
-                  0, None, None, 0, None, 0, 0, 0.0, 0.0, 0, None)  # no output, Kp not a multiple of 32
-
-
 def test_gemm_x6_edge_values(K):
     """Split of edge values: |x| near FLT_MAX (where rounding hi to bf16 would overflow)
     splits by truncation and stays finite and accurate; inf / NaN operands give non-finite results
