@@ -553,7 +553,67 @@ __global__ void __launch_bounds__(256) sparse_hidden_kernel(int B, int H, const 
   }
 }
 
+// the same gather, keeping the pre-activation a = x0 W1[:, :I]^T (no bias) beside h = tanh(a + eb): the
+// first step of the folded p_sample chain (Denoiser.p_sample_fold).  The sum runs in the same order as
+// sparse_hidden_kernel, so h is bit-identical to it.
+__global__ void __launch_bounds__(256) sparse_pre_kernel(int B, int H, const int* __restrict__ users,
+                                                         const int* __restrict__ uptr, const int* __restrict__ uitems,
+                                                         const float* __restrict__ W1T, int64_t ldw,
+                                                         const float* __restrict__ eb, float* __restrict__ a,
+                                                         int64_t lda, float* __restrict__ h, int64_t ldh) {
+  const int b = blockIdx.x;
+  const int u = users[b];
+  const int beg = uptr[u], end = uptr[u + 1];
+  for (int c = threadIdx.x * 4; c < H; c += 1024) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e = beg; e < end; ++e) acc = gmr::f4_add(acc, *reinterpret_cast<const float4*>(W1T + (int64_t)uitems[e] * ldw + c));
+    const float4 bb = *reinterpret_cast<const float4*>(eb + c);
+    *reinterpret_cast<float4*>(a + (int64_t)b * lda + c) = acc;
+    float4 o = make_float4(tanhf(acc.x + bb.x), tanhf(acc.y + bb.y), tanhf(acc.z + bb.z), tanhf(acc.w + bb.w));
+    *reinterpret_cast<float4*>(h + (int64_t)b * ldh + c) = o;
+  }
+}
+
+// h = tanh(a + bias) (rows x cols, cols % 4 == 0), float4 per thread
+__global__ void __launch_bounds__(256) tanh_bias_kernel(int64_t rows, int cols, const float* __restrict__ a,
+                                                        int64_t lda, const float* __restrict__ bias,
+                                                        float* __restrict__ h, int64_t ldh) {
+  const int c4 = cols / 4;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < rows * c4; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = g / c4;
+    const int c = (int)(g % c4) * 4;
+    const float4 x = *reinterpret_cast<const float4*>(a + r * lda + c);
+    const float4 bb = *reinterpret_cast<const float4*>(bias + c);
+    *reinterpret_cast<float4*>(h + r * ldh + c) =
+        make_float4(tanhf(x.x + bb.x), tanhf(x.y + bb.y), tanhf(x.z + bb.z), tanhf(x.w + bb.w));
+  }
+}
+
 }  // namespace
+
+extern "C" int gmr_diff_sparse_pre(int32_t B, int32_t H, const int32_t* users, const int32_t* user_ptr,
+                                   const int32_t* user_items, const float* W1T, int64_t ldw, const float* eb, float* a,
+                                   int64_t lda, float* h, int64_t ldh, void* stream) {
+  GMR_ARG(users && user_ptr && user_items && W1T && eb && a && h && B > 0 && H > 0, "bad args");
+  GMR_ARG(H % 4 == 0 && ldw % 4 == 0 && lda % 4 == 0 && ldh % 4 == 0, "H and the leading dims must be multiples of 4");
+  GMR_ARG((((uintptr_t)W1T | (uintptr_t)eb | (uintptr_t)a | (uintptr_t)h) & 15) == 0, "16-byte alignment");
+  hipLaunchKernelGGL(sparse_pre_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, H, users, user_ptr, user_items,
+                     W1T, ldw, eb, a, lda, h, ldh);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_tanh_bias_f32(int64_t rows, int32_t cols, const float* a, int64_t lda, const float* bias, float* h,
+                                 int64_t ldh, void* stream) {
+  GMR_ARG(a && bias && h && rows >= 0 && cols > 0, "bad args");
+  GMR_ARG(cols % 4 == 0 && lda % 4 == 0 && ldh % 4 == 0, "cols and the leading dims must be multiples of 4");
+  GMR_ARG((((uintptr_t)a | (uintptr_t)bias | (uintptr_t)h) & 15) == 0, "16-byte alignment");
+  if (rows == 0) return GMR_OK;
+  hipLaunchKernelGGL(tanh_bias_kernel, dim3(gmr::grid_for(rows * (cols / 4), 256, 16384)), dim3(256), 0,
+                     (hipStream_t)stream, rows, cols, a, lda, bias, h, ldh);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
 
 extern "C" int gmr_diff_sample_t(int32_t B, int32_t T, uint64_t seed, uint64_t step, int64_t row0, int32_t* t,
                                  void* stream) {

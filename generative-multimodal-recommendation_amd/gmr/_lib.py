@@ -100,6 +100,8 @@ SIGNATURES = {
     "gmr_fill2d_f32": (I32, [I64, I64, P, I64, F32, P]),
     "gmr_transpose_f32": (I32, [I64, I64, P, I64, P, I64, P]),
     "gmr_diff_sparse_hidden": (I32, [I32, I32, P, P, P, P, I64, P, P, I64, P]),
+    "gmr_diff_sparse_pre": (I32, [I32, I32, P, P, P, P, I64, P, P, I64, P, I64, P]),
+    "gmr_tanh_bias_f32": (I32, [I64, I32, P, I64, P, P, I64, P]),
     "gmr_diff_sample_t_importance": (I32, [I32, I32, I32, P, P, F64, U64, U64, I64, P, P, P]),
     "gmr_diff_history_update": (I32, [I32, I32, I32, P, P, P, P, P]),
     "gmr_diff_gc_rows": (I32, [I32, P, P, P, P, I64, P, I64, F32, P, I64, P, P]),

@@ -24,6 +24,12 @@ def _r4(n):
     return (n + 3) // 4 * 4
 
 
+# GMR_PSAMPLE_FOLD (default 1): p_sample chains (the DiffMM graph rebuild, DiffRec's prediction) carry the
+# hidden pre-activation a = x_t W1[:, :I]^T instead of x_t (p_sample_fold): every step but the last is one
+# B x H x H product instead of a B x H x I and a B x I x H one.  0 restores the step-by-step chain.
+PSAMPLE_FOLD = os.environ.get("GMR_PSAMPLE_FOLD", "1") != "0"
+
+
 class _Linear(nn.Module):
     def __init__(self, weight, bias):
         super().__init__()
@@ -97,7 +103,44 @@ class Denoiser(nn.Module):
             self._w1t = torch.empty((self.I, _r4(self.H)), device=self.device)[:, :self.H]
         _lib.call("gmr_transpose_f32", self.H, self.I, ptr(self.slab.view("W1")), self.ld_w1, ptr(self._w1t),
                   self._w1t.stride(0), stream())
+        if PSAMPLE_FOLD:
+            self.refresh_fold()
         return self._w1t
+
+    def refresh_fold(self):
+        """P = W1[:, :I] @ W2 (H x H) and v = W1[:, :I] @ b2 (H) for p_sample_fold; recomputed with W1T."""
+        H = self.H
+        if getattr(self, "_fold", None) is None:
+            self._fold = (torch.empty((H, _r4(H)), device=self.device)[:, :H],
+                          torch.empty((1, _r4(H)), device=self.device)[:, :H])
+        P, v = self._fold
+        K.gemm(self.W1x(), self.slab.view("W2"), P)                                  # (H x I) (I x H)
+        K.gemm(self.slab.view("b2")[None, :], self.W1x(), v, trans_b=True)          # b2 W1[:, :I]^T
+        return self._fold
+
+    def p_sample_fold(self, users, user_ptr, user_items, EB, c1, c2, x, a, h):
+        """p_sample(x0, steps = 0, sampling_noise = False) of binary histories (models/diffmm.py:408-426,
+        models/diffrec.py:291-310), exact algebra of the same chain carried in the hidden pre-activation.
+
+        The step-by-step chain is h_i = tanh(x_{i+1} W1x^T + EB[i]), x_i = c1_i (h_i W2^T + b2) + c2_i x_{i+1}
+        (x_T = x0, W1x = W1[:, :I]).  With a_j = x_j W1x^T that is a_i = c1_i (h_i P^T + v) + c2_i a_{i+1}
+        (P = W1x W2, v = W1x b2: refresh_fold), so the chain needs x only at the end: for i = T-1 .. 1 one
+        B x H x H product with the posterior epilogue (in place over a) and h_{i-1} = tanh(a_i + EB[i-1]);
+        the last step (t = 0) is x_0 = c1_0 (h_0 W2^T + b2) + c2_0 x_1 with c2_0 = 0 exactly (the posterior
+        at t = 0 is the x0 prediction: alphas_cumprod_prev[0] = 1), i.e. ONE B x I x H product over the
+        densified x0 that x holds on entry (0 * x0 = 0).  c1 / c2: the fp32 coefficient per t (len = T).
+        Work for the DiffMM rebuild (T = 5, H = 1,000, I = 7,050): 4 B H^2 + B I H instead of 9 B I H."""
+        T = len(c1)
+        if c2[0] != 0.0:
+            raise ValueError("p_sample_fold needs c2[0] == 0 (the posterior mean at t = 0 is the x0 prediction)")
+        P, v = self._fold
+        B, H = users.numel(), self.H
+        _lib.call("gmr_diff_sparse_pre", B, H, ptr(users), ptr(user_ptr), ptr(user_items), ptr(self._w1t),
+                  self._w1t.stride(0), ptr(EB[T - 1]), ptr(a), a.stride(0), ptr(h), h.stride(0), stream())
+        for i in range(T - 1, 0, -1):
+            K.gemm(h, P, a, trans_b=True, epi=K.EPI_POSTERIOR, bias=v[0], aux=a, slope=c1[i], beta=c2[i])
+            _lib.call("gmr_tanh_bias_f32", B, H, ptr(a), a.stride(0), ptr(EB[i - 1]), ptr(h), h.stride(0), stream())
+        return self.posterior_step(h, x, c1[0], 0.0)
 
     def hidden_sparse(self, users, user_ptr, user_items, h, eb_row):
         """h = tanh(x0 @ W1[:, :I]^T + eb_row) for binary x0 rows given as the users' item lists

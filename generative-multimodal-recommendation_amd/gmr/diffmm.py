@@ -544,7 +544,7 @@ class DiffMM(GeneralRecommender):
         self._dw[slot] = {"B": B, "x": f(B, Ip), "h": f(B, H), "out": f(B, Ip), "dpre": f(B, H), "Z": f(B, 64),
                           "Gc": f(B, 64), "S": f(self.steps, H), "t": f(B, dt=torch.int32),
                           "mse": f(B, dt=torch.float64), "diff": f(B, dt=torch.float64),
-                          "gc": f(B, dt=torch.float64),
+                          "gc": f(B, dt=torch.float64), "a": f(B, (H + 3) // 4 * 4)[:, :H],
                           "users": torch.arange(self.n_users, dtype=torch.int32, device=dev)}
         return self._dw[slot]
 
@@ -601,7 +601,11 @@ class DiffMM(GeneralRecommender):
         if not w1t_fresh:
             den.refresh_w1t()
         xi = x[:, :I]
-        for i in reversed(range(T)):
+        c1 = [float(np.float32(c)) for c in self.tables["c1"]]
+        c2 = [float(np.float32(c)) for c in self.tables["c2"]]
+        if dn.PSAMPLE_FOLD:  # the chain in the hidden pre-activation (Denoiser.p_sample_fold)
+            den.p_sample_fold(users, self.user_ptr, self.user_items, EB, c1, c2, xi, w["a"][:B], h)
+        for i in reversed(range(T)) if not dn.PSAMPLE_FOLD else ():
             if i == T - 1:  # the first model call sees the binary history: sparse hidden layer
                 den.hidden_sparse(users, self.user_ptr, self.user_items, h, EB[i])
             else:

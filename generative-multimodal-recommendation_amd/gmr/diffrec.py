@@ -10,8 +10,9 @@ one fused step per batch:
   loss       per row w[t] * mean_I (x0 - f)^2 / pt, gradient written in place (gmr_diff_loss_rows)
   backward   hand-derived (Denoiser.backward), gradients straight into the flat parameter slab
   history    Lt_history / Lt_count updated on the device in batch order (:279-286)
-Prediction (full_sort_predict, :372-388) is p_sample over all `steps` with the posterior mean
-fused into the output GEMM's epilogue.
+Prediction (full_sort_predict, :372-388) is p_sample over all `steps`, carried in the hidden
+pre-activation (Denoiser.p_sample_fold: 99 B x 300 x 300 products and one B x I x 300 output product
+instead of 100 pairs of B x 300 x I products), the posterior mean in the GEMM epilogues.
 
 Data parallel (gmr/dist.py): each loader batch is split over the ranks (rank r holds rows
 [row0, row0 + n) of it); t, pt, noise and the dropout mask are drawn per global row, and the
@@ -24,6 +25,7 @@ import torch
 from . import _lib
 from . import dist
 from .abstract_recommender import GeneralRecommender
+from . import denoise as dn
 from .denoise import Denoiser
 from .kernels import ptr, stream
 
@@ -230,6 +232,13 @@ class DiffRec(GeneralRecommender):
         EB, _, _ = den.time_bias(T)
         den.refresh_w1t()
         xi = x[:, :I]
+        if dn.PSAMPLE_FOLD:  # the chain in the hidden pre-activation: 99 B x H x H products + one output product
+            if "a" not in w:
+                w["a"] = torch.empty((w["B"], (den.H + 3) // 4 * 4), device=self.device)[:, :den.H]
+            den.p_sample_fold(users, self.user_ptr, self.user_items, EB,
+                              [float(np.float32(c)) for c in self.tables["c1"]],
+                              [float(np.float32(c)) for c in self.tables["c2"]], xi, w["a"][:B], h)
+            return xi
         for i in reversed(range(T)):
             if i == T - 1:  # binary history input: sparse hidden layer
                 den.hidden_sparse(users, self.user_ptr, self.user_items, h, EB[i])

@@ -203,6 +203,8 @@ def zero_(t):
 
 # ----------------------------------------------------------------------------- GEMM
 _gemm_kinds = {}
+# tile flags OR-ed into every gemm() call (tests: GMR_GEMM_F32 = 1 << 27 runs a whole path on the fp32-input MFMA)
+GEMM_TILE_FLAGS = 0
 
 
 def _gemm_tag(A, B, trans_a, trans_b, M, N, K, tile, split_k):
@@ -228,6 +230,7 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
     for t in (A, B, C):
         if t.dtype != torch.float32:
             raise TypeError("gemm is fp32")
+    tile |= GEMM_TILE_FLAGS
     need = _lib.load().gmr_gemm_workspace_floats(int(trans_a), int(trans_b), M, N, K, tile, split_k)
     ws = workspace(need, C.device) if need > 0 else None  # split-K partials only when this call splits
     with _Probe(_gemm_tag(A, B, trans_a, trans_b, M, N, K, tile, split_k) if _probe is not None else "gemm",

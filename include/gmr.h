@@ -377,6 +377,17 @@ int gmr_transpose_f32(int64_t rows, int64_t cols, const float* in, int64_t ldi, 
 int gmr_diff_sparse_hidden(int32_t B, int32_t H, const int32_t* users, const int32_t* user_ptr,
                            const int32_t* user_items, const float* W1T, int64_t ldw, const float* eb, float* h,
                            int64_t ldh, void* stream);
+/* Folded p_sample chain (round 5; the same p_sample, models/diffmm.py:408-451 and models/diffrec.py:291-310,
+ * carried as the hidden pre-activation a = x_t W1[:, :I]^T instead of x_t: a_i = c1_i (h_i P^T + v) +
+ * c2_i a_{i+1} with P = W1[:, :I] W2 (H x H), v = W1[:, :I] b2; gmr/denoise.py p_sample_fold).
+ * gmr_diff_sparse_pre: the first step from binary x0 rows, a[b] = sum over the user's items of W1T[i, :]
+ * and h[b] = tanh(a[b] + eb) (h bit-identical to gmr_diff_sparse_hidden).
+ * gmr_tanh_bias_f32: h = tanh(a + bias) per row (rows x cols, cols % 4 == 0, 16-byte aligned). */
+int gmr_diff_sparse_pre(int32_t B, int32_t H, const int32_t* users, const int32_t* user_ptr, const int32_t* user_items,
+                        const float* W1T, int64_t ldw, const float* eb, float* a, int64_t lda, float* h, int64_t ldh,
+                        void* stream);
+int gmr_tanh_bias_f32(int64_t rows, int32_t cols, const float* a, int64_t lda, const float* bias, float* h,
+                      int64_t ldh, void* stream);
 /* DiffRec importance sampling of t (models/diffrec.py:234-250): uniform t and pt = 1 until every
  * t has hist_len recorded losses, then t ~ (1-up) sqrt(mean(hist^2))/sum + up/T, pt = p[t]*T. */
 int gmr_diff_sample_t_importance(int32_t B, int32_t T, int32_t hist_len, const double* hist, const int32_t* count,
