@@ -22,7 +22,7 @@ Reference code exercised (paths relative to GenMMRec/src):
                                  with pop / niche, warm / cold and coverage / gini / tail extras)
   utils/quick_start.py:46-102    pop_items (top 20 % train items) and warm users (> 5 train inter.)
 
-Usage:  python tests/golden/make_golden_baby.py [baby|sports|diffrec|diffrec_train]
+Usage:  python tests/golden/make_golden_baby.py [baby|sports|diffrec|diffrec_train|diffmm_train|vbpr]
   baby   (default) -> diffmm_baby.npz / diffmm_baby_meta.json, about a minute on 8 cores
   sports (config 4: 35,598 users x 18,357 items) -> diffmm_sports.npz / _meta.json:
          the same checks on the valid split only (the is_test extras are pinned at baby), a few
@@ -33,6 +33,10 @@ Usage:  python tests/golden/make_golden_baby.py [baby|sports|diffrec|diffrec_tra
          about two minutes on 8 cores
   diffrec_train -> diffrec_baby_train.npz / _meta.json: three training calls at the baby shape
          (main_diffrec_train's docstring)
+  diffmm_train -> diffmm_baby_train.npz / _meta.json: one diffusion step per denoiser and one rec step at
+         the baby shape with the reference's draws / batch (main_diffmm_train's docstring), ~30 s
+  vbpr   (config 1) -> vbpr_baby.npz / _meta.json: VBPR init digests, one loss + backward, valid top-50 +
+         metrics, each also in fp64 (main_vbpr's docstring), about a minute
 """
 import hashlib
 import json
@@ -482,26 +486,50 @@ def main_vbpr():
         _grad_record(out, "g_" + n.replace(".", "_"), g, pk)
     ev = ref["topk_evaluator"].TopKEvaluator(cfg)
     kmax = max(cfg["topk"])
-    model.eval()
-    mats, vals = [], []
-    with torch.no_grad():
-        for b in vl:
-            scores = model.full_sort_predict(b)
-            m = b[1]
-            scores[m[0], m[1]] = -1e10
-            v, ix = torch.topk(scores, kmax, dim=-1)
-            mats.append(ix)
-            vals.append(v)
-    topk = torch.cat(mats).numpy()
-    out["valid_top50"] = topk.astype(np.int16)
-    out["valid_top50_val_sample"] = torch.cat(vals)[:SAMPLE].numpy().astype(np.float32)
-    res = ev.evaluate([torch.as_tensor(topk)], vl, is_test=False)
-    pos = vl.get_eval_items()
-    bool_rec = np.asarray([[i in p for i in row] for p, row in zip(pos, topk)])
-    raw = ev._calculate_metrics(vl.get_eval_len_list(), bool_rec)
-    meta["valid"] = {"n_users": int(len(topk)), "rounded": res,
-                     "raw": {mname: np.asarray(raw[j], np.float64).tolist()
-                             for j, mname in enumerate(["recall", "ndcg", "precision", "map"])}}
+
+    def valid_eval(tag):
+        model.eval()
+        mats, vals = [], []
+        with torch.no_grad():
+            for b in vl:
+                scores = model.full_sort_predict(b)
+                m = b[1]
+                scores[m[0], m[1]] = -1e10
+                v, ix = torch.topk(scores, kmax, dim=-1)
+                mats.append(ix)
+                vals.append(v)
+        topk = torch.cat(mats).numpy()
+        out[f"valid_top50{tag}"] = topk.astype(np.int16)
+        out[f"valid_top50_val_sample{tag}"] = torch.cat(vals)[:SAMPLE].numpy().astype(np.float32)
+        res = ev.evaluate([torch.as_tensor(topk)], vl, is_test=False)
+        pos = vl.get_eval_items()
+        bool_rec = np.asarray([[i in p for i in row] for p, row in zip(pos, topk)])
+        raw = ev._calculate_metrics(vl.get_eval_len_list(), bool_rec)
+        meta[f"valid{tag}"] = {"n_users": int(len(topk)), "rounded": res,
+                               "raw": {mname: np.asarray(raw[j], np.float64).tolist()
+                                       for j, mname in enumerate(["recall", "ndcg", "precision", "map"])}}
+        return res
+    res = valid_eval("")
+    # the same reference calls in fp64 (model.double(): the same parameters, widened): the reference's fp32
+    # loss is 2.1e-5 off its own fp64 value (EmbLoss's fp32 torch.norm over 2,048 x 128-wide rows of the
+    # 4,480-term item projection), so the HIP path is pinned to the fp64 values, the fp32 ones recorded beside
+    model.double()
+    model.item_raw_features = model.item_raw_features.double()
+    model.train()
+    model.zero_grad()
+    loss64 = model.calculate_loss(batch)
+    loss64.backward()
+    meta["loss64"] = float(loss64.item())
+    for n, p in model.named_parameters():
+        g = p.grad.detach().numpy()
+        k = n.replace(".", "_")
+        _grad_record(out, "g64_" + k, g, out.get("pick_" + k))
+    valid_eval("64")
+    # the fp32 top-50 kept as its differences from the fp64 one (54 positions; the fixture stays small)
+    t32, t64 = out.pop("valid_top50").reshape(-1), out["valid_top5064"].reshape(-1)
+    dpos = np.nonzero(t32 != t64)[0]
+    out["valid_top50_fp32_diff_pos"] = dpos.astype(np.int32)
+    out["valid_top50_fp32_diff_val"] = t32[dpos]
     np.savez_compressed(os.path.join(HERE, "vbpr_baby.npz"), **out)
     with open(os.path.join(HERE, "vbpr_baby_meta.json"), "w") as f:
         json.dump(meta, f, indent=1, default=float)

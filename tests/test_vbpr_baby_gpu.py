@@ -1,16 +1,22 @@
 """Config 1 - VBPR at the Amazon-baby shape (19,445 users x 7,050 items, 4,096-d image + 384-d text
 features, VBPR.yaml: embedding 64, reg_weight 2.0; VERDICT r4 missing #2) against the reference's own
 outputs on the same inputs (tests/golden/vbpr_baby.npz + vbpr_baby_meta.json, made by
-`make_golden_baby.py vbpr`, which ran the reference in the build container).  Through the HIP path:
+`make_golden_baby.py vbpr`, which ran the reference in the build container, in fp32 AND - model.double(),
+the same parameters widened - in fp64).  The reference's fp32 CPU path is itself 2.1e-5 off its fp64 loss
+(EmbLoss takes fp32 torch.norm's of 2,048 x 128-wide rows whose item half is a 4,480-term projection) and
+its fp32 top-50 differs from its fp64 top-50 at 54 positions, so the HIP path is pinned to the fp64 run at
+the north-star bars, and to the fp32 run within that run's own measured distance from fp64.  Through the
+HIP path:
   * init     SHA-256 of every parameter equals the reference's after init_seed(999) (models/vbpr.py:31-45
              + xavier_normal_initialization: the CPU RNG order) - bit-exact;
   * loss     calculate_loss + backward (vbpr.py:76-97) on the reference loader's first 2,048-row batch:
-             loss rtol 1e-5, every gradient rtol 1e-4 (whole when small, else row / column sums and
-             4,096 sampled entries);
-  * D19      Trainer.topk_all (score -> mask -> top-50; the 128-wide user rows of VBPR) on the valid
-             split through both eval paths: by position except inside 1e-6 near ties of the path's own
-             scores; the reference's top-50 scores of the stored user sample within fp32 tolerance;
-  * D21      Recall/NDCG/Precision/MAP@{5,10,20,50} unrounded within 1e-4.
+             loss within 1e-5 of the fp64 reference (and of the fp32 one within its own error + 1e-5), every
+             gradient rtol 1e-4 vs fp64 (whole when small, else row / column sums and 4,096 sampled entries);
+  * D19      Trainer.topk_all (score -> mask -> top-50; the 128-wide user rows of VBPR) on the valid split
+             through both eval paths: by position vs the fp64 reference except inside 1e-6 near ties of the
+             path's own scores; the fp64 reference's top-50 scores of the stored user sample within fp32
+             tolerance;
+  * D21      Recall/NDCG/Precision/MAP@{5,10,20,50} unrounded within 1e-4 of the fp64 AND the fp32 reference.
 """
 import hashlib
 import json
@@ -72,20 +78,27 @@ def test_vbpr_baby_init_bit_exact(vb):
 
 
 def test_vbpr_baby_loss_and_grads(vb):
-    m, g = vb["model"], vb["g"]
+    m, g, meta = vb["model"], vb["g"], vb["meta"]
     inter = torch.as_tensor(g["inter"]).to(DEV)
-    loss = m.rec_step(inter[0].contiguous(), inter[1].contiguous(), inter[2].contiguous())
-    np.testing.assert_allclose(loss.item(), vb["meta"]["loss"], rtol=1e-5)
+    loss = m.rec_step(inter[0].contiguous(), inter[1].contiguous(), inter[2].contiguous()).item()
+    l64, l32 = meta["loss64"], meta["loss"]
+    np.testing.assert_allclose(loss, l64, rtol=1e-5)
+    assert abs(loss - l32) <= abs(l32 - l64) + 1e-5 * abs(l64), (loss, l32, l64)
     for name, gv in zip(["u_embedding", "i_embedding", "item_linear.weight", "item_linear.bias"], m.grad_views()):
         k = name.replace(".", "_")
-        _check_grad(gv.cpu().numpy(), g, "g_" + k, "pick_" + k, name)
+        _check_grad(gv.cpu().numpy(), g, "g64_" + k, "pick_" + k, name)
     m.slab.zero_grad()
 
 
 @pytest.mark.parametrize("path", EVAL_PATHS)
 def test_vbpr_baby_valid_topk_and_metrics(vb, path):
-    m, g = vb["model"], vb["g"]
+    m, g, meta = vb["model"], vb["g"], vb["meta"]
     m.eval()
-    out = check_topk_vs_reference(m, vb["trainer"], vb["vl"], g["valid_top50"].astype(np.int64),
-                                  g["valid_top50_val_sample"], path)
-    check_metrics_vs_reference(vb["trainer"], vb["vl"], out, vb["meta"]["valid"])
+    out = check_topk_vs_reference(m, vb["trainer"], vb["vl"], g["valid_top5064"].astype(np.int64),
+                                  g["valid_top50_val_sample64"], path)
+    check_metrics_vs_reference(vb["trainer"], vb["vl"], out, meta["valid64"])
+    # the reference's fp32 run: its top-50 (stored as differences from the fp64 one) gives the same metrics
+    t32 = g["valid_top5064"].astype(np.int64).reshape(-1)
+    t32[g["valid_top50_fp32_diff_pos"]] = g["valid_top50_fp32_diff_val"]
+    assert len(g["valid_top50_fp32_diff_pos"]) < 0.001 * t32.size
+    check_metrics_vs_reference(vb["trainer"], vb["vl"], out, meta["valid"])
