@@ -371,9 +371,9 @@ __global__ void cl_bwd_kernel(int64_t n, const float* __restrict__ dK, const flo
   st4(Rt + r * 128 + 64 + c, dct);
 }
 
-// gradient assembly:
-//   dE0[:U]  += T3u_img + T3u_txt + Ri[:U, :64] + Ri[:U, 64:] + Rt[:U, :64] + Rt[:U, 64:] + 2 reg uE
-//   dE0[U:]  += T2i_img + T2i_txt + Ri[U:, :64] + Rt[U:, :64] + 2 reg iE
+// gradient assembly (dE0 is written, not accumulated: the rec step's slab gradient needs no zeroing pass):
+//   dE0[:U]  = T3u_img + T3u_txt + Ri[:U, :64] + Ri[:U, 64:] + Rt[:U, :64] + Rt[:U, 64:] + 2 reg uE
+//   dE0[U:]  = T2i_img + T2i_txt + Ri[U:, :64] + Rt[U:, :64] + 2 reg iE
 //   dNF[:, :64] = T3[U:, :64] + Ri[U:, 64:] ;  dNF[:, 64:] = T3[U:, 64:] + Rt[U:, 64:]
 // T2 = adj@dE (its item rows feed diE), T3 = adj@dG.
 __global__ void assemble_kernel(int64_t n, int64_t U, const float* __restrict__ T2, const float* __restrict__ T3,
@@ -398,8 +398,7 @@ __global__ void assemble_kernel(int64_t n, int64_t U, const float* __restrict__ 
     st4(dNF + ri * 128 + 64 + c, gmr::f4_add(ld4(T3 + o + 64), ld4(Rt + o + 64)));
   }
   g = gmr::f4_fma(reg2, ld4(E0 + r * 64 + c), g);
-  float* d = dE0 + r * 64 + c;
-  st4(d, gmr::f4_add(ld4(d), g));
+  st4(dE0 + r * 64 + c, g);
 }
 
 // sum of a float vector into out[0] (single block, deterministic); optional scale and accumulation

@@ -318,7 +318,8 @@ class DiffMM(GeneralRecommender):
         K.zero_(dEmb)
         _lib.call("gmr_scatter_sorted_f32", plan_bpr.numel(), 64, ptr(plan_bpr), ptr(w["contrib_bpr"]), 64,
                   ptr(dEmb), 64, stream())
-        s.zero_grad()
+        # (no slab zeroing: every rec gradient segment is written, not accumulated - E0 by gmr_dmm_assemble,
+        # the projections by their GEMMs, modal_weight by gmr_dmm_mw_grad)
         if SPMM_FUSE & FUSE_BWD_CL:  # Tcl = adj^T dK and T1 = adj^T dEmb (adj symmetric) in one launch
             st.join(0)
             K.spmm_jobs([(adj, w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], None, w["part_cl"]),
