@@ -163,7 +163,7 @@ def summarize_probe(p, model="diffmm", shape=None):
             # (a multi-job launch, key ("jobs", job, ...), moves the sum of its jobs' bytes)
             byts = 0.0
             for key in (r[2] for r in recs):
-                for nnz, nr, nc, nb, has_beta in (key[1:] if key[0] == "jobs" else (key,)):
+                for nnz, nr, nc, nb, has_beta in (key[1:] if key[0] in ("jobs", "side_jobs") else (key,)):
                     d = 64 * nb
                     byts += 8.0 * nnz + 4.0 * (nr + 1) + 4.0 * d * nc + 4.0 * d * nr * (2 if has_beta else 1)
             achieved = byts / (tot_ms * 1e-3) / 1e9

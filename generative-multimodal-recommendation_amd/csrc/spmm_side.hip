@@ -105,11 +105,11 @@ __device__ __forceinline__ int grp_bcast(int x, int j) {  // j is a constant aft
   }
 }
 
-// NS = 32-column slices of the product (d = 32 NS), EB = entries in flight per lane group
+// NS = 32-column slices of the product (d = 32 NS), EB = entries in flight per lane group.  The body of one
+// product; spmm_side_kernel runs one, spmm_side_jobs_kernel up to four independent ones (blockIdx.y)
 template <int EB, int NS>
-__global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __restrict__ plan, SideSrc src,
-                                                                  float alpha, float beta, SideDst dst,
-                                                                  float* __restrict__ scratch, int wpx, int nt) {
+__device__ __forceinline__ void side_body(const int* __restrict__ plan, const SideSrc& src, float alpha, float beta,
+                                          const SideDst& dst, float* __restrict__ scratch, int wpx, int nt) {
   constexpr int G = 2 * NS;                    // (side, slice) groups
   constexpr int PHASES = G > 8 ? G / 8 : 1;    // groups per XCD, one after the other
   constexpr int P = G >= 8 ? 1 : 8 / G;        // XCDs per group
@@ -432,6 +432,35 @@ __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __re
   }
 }
 
+template <int EB, int NS>
+__global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __restrict__ plan, SideSrc src,
+                                                                  float alpha, float beta, SideDst dst,
+                                                                  float* __restrict__ scratch, int wpx, int nt) {
+  side_body<EB, NS>(plan, src, alpha, beta, dst, scratch, wpx, nt);
+}
+
+// Multi-job launch (round 5, gmr_spmm_side_jobs_f32): independent side-split products of the same width in one
+// grid, job = blockIdx.y.  gridDim.x = 8 wpx is a multiple of 8, so a workgroup's XCD (its linear id mod 8) is
+// blockIdx.x mod 8 in every job: each job keeps the (side, slice) -> XCD map of its own launch.  Each job has
+// its own plan and hub scratch, so the sums are those of separate launches bit for bit.
+struct SideJob {
+  const int* plan;
+  float* scratch;
+  SideSrc src;
+  SideDst dst;
+};
+struct SideJobs {
+  SideJob j[4];
+};
+template <int EB, int NS>
+__global__ void __launch_bounds__(kSideThreads) spmm_side_jobs_kernel(SideJobs jobs, float alpha, float beta, int wpx,
+                                                                       int nt) {
+  const int y = blockIdx.y;
+  const SideJob& J = jobs.j[y];
+  side_body<EB, NS>(J.plan, J.src, alpha, beta, J.dst, J.scratch, wpx, nt);
+}
+
+
 // packed entries: {col | (last entry of its row) << 31, val}: one thread per entry (coalesced), then one
 // per row sets its last entry's bit (a per-row loop serialised the hub rows of a rebuilt graph: 790 us)
 __global__ void __launch_bounds__(256) side_pack_kernel(const int* __restrict__ col, const float* __restrict__ val,
@@ -589,7 +618,70 @@ void side_launch(int eb, const int* plan, const SideSrc& src, float alpha, float
                        dst, scratch, wpx, nt);
 }
 
+template <int NS>
+void side_jobs_launch(int eb, int njobs, const SideJobs& jobs, float alpha, float beta, int wpx, int nt,
+                      hipStream_t st) {
+  const dim3 grid((unsigned)(8 * wpx), (unsigned)njobs);
+  if (eb == 8)
+    hipLaunchKernelGGL((spmm_side_jobs_kernel<8, NS>), grid, dim3(kSideThreads), 0, st, jobs, alpha, beta, wpx, nt);
+  else
+    hipLaunchKernelGGL((spmm_side_jobs_kernel<16, NS>), grid, dim3(kSideThreads), 0, st, jobs, alpha, beta, wpx, nt);
+}
+
+// one job's block pointers / strides from the C-ABI arrays (entries [4 q, 4 q + n_blocks) of job q)
+int side_fill(int n_blocks, const float* const* x_lo, const int64_t* ld_lo, const float* const* x_hi,
+              const int64_t* ld_hi, int64_t split, float* const* y, const int64_t* ld_y, SideSrc& s, SideDst& d) {
+  for (int b = 0; b < 4; ++b) {
+    const bool on = b < n_blocks;
+    s.lo[b] = on ? x_lo[b] : nullptr;
+    s.hi[b] = on ? x_hi[b] : nullptr;
+    s.ld_lo[b] = on ? ld_lo[b] : 0;
+    s.ld_hi[b] = on ? ld_hi[b] : 0;
+    d.y[b] = on ? y[b] : nullptr;
+    d.ld[b] = on ? ld_y[b] : 0;
+    if (on) {
+      GMR_ARG(s.lo[b] && s.hi[b] && d.y[b], "null block pointer");
+      GMR_ARG(((uintptr_t)s.lo[b] | (uintptr_t)s.hi[b] | (uintptr_t)d.y[b]) % 16 == 0, "blocks must be 16-byte aligned");
+      GMR_ARG(s.ld_lo[b] % 4 == 0 && s.ld_hi[b] % 4 == 0 && d.ld[b] % 4 == 0 && d.ld[b] >= 64,
+              "leading dimensions must be multiples of 4");
+    }
+  }
+  s.split = split;
+  return GMR_OK;
+}
+
 }  // namespace
+
+extern "C" int gmr_spmm_side_jobs_f32(int32_t njobs, const int32_t* const* plans, float* const* scratch,
+                                      int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
+                                      const float* const* x_hi, const int64_t* ld_hi, const int64_t* split,
+                                      float alpha, float beta, float* const* y, const int64_t* ld_y, int32_t wpx,
+                                      void* stream) {
+  GMR_ARG(njobs >= 1 && njobs <= 4, "1 to 4 jobs");
+  GMR_ARG(plans && scratch && x_lo && ld_lo && x_hi && ld_hi && split && y && ld_y, "null argument");
+  GMR_ARG(wpx >= 0 && wpx <= 1024, "wpx in [0, 1024] (0 = default)");
+  GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "1, 2 or 4 blocks of 64 columns");
+  SideJobs jobs{};
+  for (int q = 0; q < njobs; ++q) {
+    GMR_ARG(plans[q] && scratch[q], "null plan / scratch");
+    jobs.j[q].plan = plans[q];
+    jobs.j[q].scratch = scratch[q];
+    if (side_fill(n_blocks, x_lo + 4 * q, ld_lo + 4 * q, x_hi + 4 * q, ld_hi + 4 * q, split[q], y + 4 * q, ld_y + 4 * q,
+                  jobs.j[q].src, jobs.j[q].dst) != GMR_OK)
+      return GMR_ERR_ARG;
+  }
+  const hipStream_t st = (hipStream_t)stream;
+  const int eb = side_eb(), nt = side_nt();
+  if (wpx == 0 || getenv("GMR_SPMM_SIDE_WPX") || g_side_tuned) wpx = side_wpx();
+  if (n_blocks == 1)
+    side_jobs_launch<2>(eb, njobs, jobs, alpha, beta, wpx, nt, st);
+  else if (n_blocks == 2)
+    side_jobs_launch<4>(eb, njobs, jobs, alpha, beta, wpx, nt, st);
+  else
+    side_jobs_launch<8>(eb, njobs, jobs, alpha, beta, wpx, nt, st);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
 
 extern "C" int gmr_spmm_side_tune(int32_t wpx, int32_t eb) {
   GMR_ARG(wpx > 0 && wpx <= 1024 && (eb == 8 || eb == 16), "wpx in [1, 1024], eb 8 or 16");

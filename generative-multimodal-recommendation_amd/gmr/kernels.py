@@ -466,6 +466,38 @@ def spmm_multi(a, outs, blocks, split=None, alpha=1.0, beta=0.0, partial=None):
     return outs
 
 
+# side-plan products of a jobs call in one launch (gmr_spmm_side_jobs_f32; GMR_SPMM_SIDE_JOBS=0: one per job)
+SIDE_JOBS = os.environ.get("GMR_SPMM_SIDE_JOBS", "1") != "0"
+
+
+def _side_jobs(jobs, alpha, beta):
+    """Side-plan products [(a, outs, blocks, split, partial), ...] of one width in one gmr_spmm_side_jobs_f32."""
+    n, nb = len(jobs), len(jobs[0][2])
+    PA, LA = ctypes.c_void_p * (4 * n), ctypes.c_int64 * (4 * n)
+    plans, scr = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)()
+    lo, hi, ys = PA(), PA(), PA()
+    ldl, ldh, ldy = LA(), LA(), LA()
+    splits = (ctypes.c_int64 * n)()
+    key = []
+    for q, (a, outs, blocks, split, partial) in enumerate(jobs):
+        if isinstance(outs, torch.Tensor):
+            outs = [outs[:, 64 * b:64 * (b + 1)] for b in range(nb)]
+        if len(outs) != nb or any(o.shape != (a.n_rows, 64) for o in outs):
+            raise ValueError("one n_rows x 64 output per block")
+        plans[q] = a.side[0].data_ptr()
+        scr[q] = (a.partial if partial is None else partial).data_ptr()
+        splits[q] = a.n_cols if split is None else int(split)
+        for b in range(nb):
+            lo[4 * q + b], ldl[4 * q + b] = blocks[b][0].data_ptr(), _ld(blocks[b][0])
+            src_hi = blocks[b][1] if split is not None else blocks[b][0]
+            hi[4 * q + b], ldh[4 * q + b] = src_hi.data_ptr(), _ld(src_hi)
+            ys[4 * q + b], ldy[4 * q + b] = outs[b].data_ptr(), _ld(outs[b])
+        key.append((a.nnz, a.n_rows, a.n_cols, nb, beta != 0.0))
+    with _Probe("spmm", ("side_jobs",) + tuple(key)):
+        _lib.call("gmr_spmm_side_jobs_f32", n, plans, scr, nb, lo, ldl, hi, ldh, splits, float(alpha), float(beta), ys,
+                  ldy, jobs[0][0].side_wpx[nb], stream())
+
+
 def spmm_jobs(jobs, alpha=1.0, beta=0.0):
     """One launch for up to 4 independent lane-plan products (gmr_spmm_jobs_f32).
 
@@ -475,10 +507,16 @@ def spmm_jobs(jobs, alpha=1.0, beta=0.0):
     n = len(jobs)
     if not 1 <= n <= 4:
         raise ValueError("1 to 4 jobs")
-    if any(j[0].side is not None for j in jobs):  # side-plan products launch on their own (in job order)
+    if any(j[0].side is not None for j in jobs):
+        # side-plan products of one width go out as one multi-job launch (gmr_spmm_side_jobs_f32; SIDE_JOBS=0:
+        # one launch each, in job order); lane-plan products as a lane multi-job launch
         lane = [j for j in jobs if j[0].side is None]
-        for a, outs, blocks, split, partial in jobs:
-            if a.side is not None:
+        side = [j for j in jobs if j[0].side is not None]
+        if SIDE_JOBS and len(side) > 1 and len({len(j[2]) for j in side}) == 1 and \
+                len({j[0].side_wpx[len(j[2])] for j in side}) == 1:
+            _side_jobs(side, alpha, beta)
+        else:
+            for a, outs, blocks, split, partial in side:
                 if isinstance(outs, torch.Tensor):
                     outs = [outs[:, 64 * b:64 * (b + 1)] for b in range(len(blocks))]
                 spmm_multi(a, outs, blocks, split=split, alpha=alpha, beta=beta, partial=partial)

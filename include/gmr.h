@@ -183,6 +183,14 @@ int gmr_spmm_side_tune(int32_t wpx, int32_t eb);
 int gmr_spmm_side_f32(const int32_t* plan, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
                       const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
                       float* const* y_blocks, const int64_t* ld_y, float* scratch, int32_t wpx, void* stream);
+/* Up to 4 independent side-split products of the same width (n_blocks) in ONE launch (round 5; the forward's
+ * Qi / Qt / G and the backward's UI-graph transposes, models/diffmm.py:129-195): job q has its own plan,
+ * hub scratch, split and block arrays at entries [4 q, 4 q + n_blocks) of x_lo / ld_lo / x_hi / ld_hi / y /
+ * ld_y.  Each job's sums are those of its own gmr_spmm_side_f32 call, bit for bit. */
+int gmr_spmm_side_jobs_f32(int32_t njobs, const int32_t* const* plans, float* const* scratch, int32_t n_blocks,
+                           const float* const* x_lo, const int64_t* ld_lo, const float* const* x_hi,
+                           const int64_t* ld_hi, const int64_t* split, float alpha, float beta, float* const* y,
+                           const int64_t* ld_y, int32_t wpx, void* stream);
 
 int gmr_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n_rows, int64_t nnz,
                      const int32_t* plan, int32_t seg_nnz, float* partial, int32_t n_blocks,

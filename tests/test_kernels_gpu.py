@@ -922,6 +922,36 @@ def test_spmm_side_all_hub_rows_split_blocks(K, classes):
         assert torch.equal(y2.view(torch.int32), outs[0].view(torch.int32))
 
 
+@pytest.mark.parametrize("nb", [1, 2, 4])
+def test_spmm_side_jobs_one_launch_bit_exact(K, nb):
+    """gmr_spmm_side_jobs_f32 (round 5): up to four side-plan products of different graphs (a norm_adj-like
+    graph, a rebuilt-UI-like graph with self loops, a second norm_adj) with split sources in ONE launch equal
+    their separate launches bit for bit (own plans and hub scratches, the same XCD map), with beta too."""
+    U, I = 3000, 500
+    N = U + I
+    graphs = []
+    for seed, loops in ((41, 0), (42, 1), (43, 0)):
+        rp, col, val = _side_graph(loops, seed=seed)
+        g = K.CSR(_dev(rp), _dev(col), _dev(val), class_split=U, side=True)
+        graphs.append(g)
+    rng = _rng(9)
+    X = _dev(rng.standard_normal((N, 64 * nb)).astype(np.float32))
+    E = _dev(rng.standard_normal((I, 64 * nb)).astype(np.float32))
+    Y0 = _dev(rng.standard_normal((N, 64 * nb)).astype(np.float32))
+    blocks = [(X[:, 64 * b:64 * (b + 1)], E[:, 64 * b:64 * (b + 1)]) for b in range(nb)]
+    for beta in (0.0, 0.5):
+        sep = []
+        for g in graphs:
+            y = Y0.clone()
+            g.spmm(y, blocks, split=U, alpha=0.9, beta=beta)
+            sep.append(y)
+        outs = [Y0.clone() for _ in graphs]
+        assert K.SIDE_JOBS
+        K.spmm_jobs([(g, o, blocks, U, None) for g, o in zip(graphs, outs)], alpha=0.9, beta=beta)
+        for a, b in zip(sep, outs):
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
 def test_spmm_side_multi_outputs_and_jobs(K):
     """spmm_multi / spmm_jobs on side plans: per-block outputs equal the one-output product, and a
     jobs launch mixing a side-plan matrix with a lane-plan one equals the separate calls."""
