@@ -31,7 +31,10 @@ from .slab import Slab
 #   FUSE_BWD3  OutI / OutT / T2 (main stream)       FUSE_UI_T    OutI / OutT (cl side stream, T2 on main)
 # GMR_SPMM_FUSE overrides (0 = one launch per product, on side streams as before), for A/B runs
 FUSE_FWD, FUSE_BWD_CL, FUSE_BWD3, FUSE_UI_T = 1, 2, 4, 8
-SPMM_FUSE = int(os.environ.get("GMR_SPMM_FUSE", str(FUSE_FWD | FUSE_UI_T)))
+# Since the side-split products take multi-job launches too (round 5, gmr_spmm_side_jobs_f32), OutI / OutT / T2
+# in one main-stream launch beats OutI / OutT on the side stream beside T2: epoch 68.5 / 69.0 vs 69.3 / 70.0 ms
+# (profiles/r05k_spmm_side_jobs_ab.txt; 70.9 / 70.4 with one launch per side-split product)
+SPMM_FUSE = int(os.environ.get("GMR_SPMM_FUSE", str(FUSE_FWD | FUSE_BWD3)))
 # users per p_sample launch chain of the graph rebuild: the whole baby user set in one chain
 # (−1.5 ms per rebuild vs 8,192-user chunks: fewer, fuller GEMM waves; 1.3 GB of buffers per
 # denoiser, profiles/r02m_knobs_ab.txt); GMR_REBUILD_CHUNK overrides, for tuning
