@@ -55,6 +55,10 @@ SIGNATURES = {
     "gmr_spmm_side_pack_classes": (I32, [P, P, P, P, P, P]),
     "gmr_spmm_side_tune": (I32, [I32, I32]),
     "gmr_spmm_side_f32": (I32, [P, I32, P, P, P, P, I64, F32, F32, P, P, P, I32, P]),
+    "gmr_graph_exec_create": (I32, [P, I32, P]),
+    "gmr_graph_exec_info": (I32, [P, P, P, P, P]),
+    "gmr_graph_exec_launch": (I32, [P, P]),
+    "gmr_graph_exec_destroy": (I32, [P]),
     "gmr_spmm_side_jobs_f32": (I32, [I32, P, P, I32, P, P, P, P, P, F32, F32, P, P, I32, P]),
     "gmr_bipartite_nnz": (I64, [I64, I64, I64, I32]),
     "gmr_bipartite_workspace_ints": (I64, [I64, I64]),

@@ -427,6 +427,35 @@ def _side_call(self, nb, lo, ldl, hi, ldh, split, alpha, beta, ys, ldy, partial)
 CSR._side_call = _side_call
 
 
+class GraphExec:
+    """Native multi-stream executor of a captured step (include/gmr.h gmr_graph_exec_*): `graph` is a
+    torch.cuda.CUDAGraph captured with keep_graph=True (kept referenced here: its nodes own the kernel arguments);
+    launch() re-issues every node from C++ on the executor's streams, forked from and joined into the current
+    stream."""
+
+    def __init__(self, graph, max_streams=4):
+        self.graph = graph
+        h = ctypes.c_void_p()
+        _lib.call("gmr_graph_exec_create", ctypes.c_void_p(graph.raw_cuda_graph()), int(max_streams), ctypes.byref(h))
+        self.handle = h
+
+    def info(self):
+        v = [ctypes.c_int64() for _ in range(4)]
+        _lib.call("gmr_graph_exec_info", self.handle, *[ctypes.byref(x) for x in v])
+        return dict(zip(("nodes", "kernels", "streams", "cross_edges"), (x.value for x in v)))
+
+    def launch(self):
+        _lib.call("gmr_graph_exec_launch", self.handle, stream())
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().gmr_graph_exec_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+
+
 def score_f16(a, b, out):
     """out = fp16(a) @ fp16(b)^T with fp32 accumulation (gmr_score_f16; a: E x 64, b: I x 64)."""
     E, d = a.shape

@@ -28,6 +28,10 @@ from .utils import dict2str, early_stopping
 # full-rank eval through the fused score -> mask -> top-k kernel (gmr_score_topk_f32); GMR_EVAL_FUSED=0
 # keeps the score GEMM + mask + radix top-k over an E x I buffer (A/B)
 FUSED_EVAL = os.environ.get("GMR_EVAL_FUSED", "1") != "0"
+# graphed BPR steps (GMR_GRAPHS=1) re-issue the captured step through the native multi-stream executor
+# (K.GraphExec, csrc/graph_exec.hip) unless GMR_GRAPH_EXEC=0 (then hipGraphLaunch); GMR_GRAPH_STREAMS: its streams
+GRAPH_EXEC = os.environ.get("GMR_GRAPH_EXEC", "1") != "0"
+GRAPH_EXEC_STREAMS = int(os.environ.get("GMR_GRAPH_STREAMS", "4"))
 
 
 def reduce_slab_grads(model, slabs):
@@ -159,15 +163,23 @@ class Trainer:
             self._graph = None
             static = [t.clone() for t in (u, p, ng, pb, pc)]
             torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
+            g = torch.cuda.CUDAGraph(keep_graph=True)
             with torch.cuda.graph(g):
                 loss = self.model.rec_step(*static, norm_rows=norm, reg_share=share)
                 _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
-            self._graph = (key, g, static)
-        _, g, static = self._graph
+            runner = None
+            if GRAPH_EXEC:  # the native multi-stream executor (csrc/graph_exec.hip); else hipGraphLaunch
+                runner = K.GraphExec(g, max_streams=GRAPH_EXEC_STREAMS)
+            else:
+                g.instantiate()
+            self._graph = (key, g, static, runner)
+        _, g, static, runner = self._graph
         for dst, src in zip(static, (u, p, ng, pb, pc)):
             dst.copy_(src)
-        g.replay()
+        if runner is not None:
+            runner.launch()
+        else:
+            g.replay()
 
     def _generate_train_loss_output(self, epoch_idx, s_time, e_time, losses):
         out = "epoch %d training [time: %.2fs, " % (epoch_idx, e_time - s_time)
