@@ -335,7 +335,8 @@ class DiffMM(GeneralRecommender):
                   ptr(s.gview("modal_weight")), 0, stream())
         if SPMM_FUSE & FUSE_BWD3:
             # the UI-graph transposes of the contrastive/ris branch and the first GCN hop adj^T dE
-            # are independent: one launch; then the second hop
+            # are independent: one launch; then the second hop.  cl_bwd reads dK / Tcl of the side stream.
+            st.join(0)
             _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
                       ptr(w["Rt"]), stream())
             K.spmm_jobs([(self._transpose_of(iadj), w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)], None, None),
