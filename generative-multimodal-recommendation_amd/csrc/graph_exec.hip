@@ -8,10 +8,12 @@
 // executor keeps both: the step is captured once into a hipGraph (torch.cuda.CUDAGraph, keep_graph), its
 // nodes are read back (kernel / memset / memcpy / empty nodes and their edges), put in a topological order
 // and given streams - a node continues the stream of a predecessor it is the first successor of, else takes
-// a new stream (up to max_streams, then the stream whose last node is earliest) - and every edge that crosses
-// streams becomes an event record + wait.  gmr_graph_exec_launch then issues the whole step from C++ in one
-// call: each kernel through hipLaunchKernel with the node's own argument block (owned by the graph, which the
-// caller keeps alive), forked from and joined back into the caller's stream.  The same kernels with the same
+// a new stream (up to 1 + n_side, then the stream whose last node is earliest) - and every edge that crosses
+// streams becomes an event record + wait.  Stream 0 is the launch stream itself; streams 1.. are the caller's
+// side streams (the ones its eager step uses, so the hardware-queue mapping is the eager step's) or, when none
+// are given, the executor's own.  gmr_graph_exec_launch then issues the whole step from C++ in one call: each
+// kernel through hipLaunchKernel with the node's own argument block (owned by the graph, which the caller keeps
+// alive), the side streams forked from and joined back into the launch stream.  The same kernels with the same
 // arguments in a dependency-respecting order: results equal the captured step's bit for bit.
 #include <algorithm>
 #include <new>
@@ -46,7 +48,8 @@ struct ExecNode {
 
 struct GraphExec {
   std::vector<ExecNode> nodes;  // in issue (topological) order; ids below index this vector
-  std::vector<hipStream_t> streams;
+  std::vector<hipStream_t> streams;  // [0] unused (the launch stream); [1..] side streams
+  bool own_streams = false;
   std::vector<hipEvent_t> events;  // per node id (null where no cross-stream successor)
   hipEvent_t fork = nullptr;
   std::vector<hipEvent_t> joins;  // per stream
@@ -56,7 +59,9 @@ struct GraphExec {
     for (hipEvent_t e : joins)
       if (e) (void)hipEventDestroy(e);
     if (fork) (void)hipEventDestroy(fork);
-    for (hipStream_t s : streams) (void)hipStreamDestroy(s);
+    if (own_streams)
+      for (size_t i = 1; i < streams.size(); ++i)
+        if (streams[i]) (void)hipStreamDestroy(streams[i]);
   }
 };
 
@@ -77,8 +82,9 @@ int issue_memset(const hipMemsetParams& m, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int gmr_graph_exec_create(void* graph, int32_t max_streams, void** exec_out) {
-  GMR_ARG(graph && exec_out && max_streams >= 1 && max_streams <= 16, "graph, exec_out, max_streams in [1, 16]");
+extern "C" int gmr_graph_exec_create(void* graph, int32_t n_side, void* const* side_streams, void** exec_out) {
+  GMR_ARG(graph && exec_out && n_side >= 0 && n_side <= 15, "graph, exec_out, n_side in [0, 15]");
+  const int max_streams = 1 + n_side;
   *exec_out = nullptr;
   hipGraph_t g = static_cast<hipGraph_t>(graph);
   size_t n = 0;
@@ -187,8 +193,16 @@ extern "C" int gmr_graph_exec_create(void* graph, int32_t max_streams, void** ex
   for (auto& nd : ex->nodes)
     for (int& w : nd.waits) w = pos[w];
   bool ok = true;
-  ex->streams.resize(tail.size(), nullptr);
-  for (auto& s : ex->streams) ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+  ex->streams.assign(tail.size(), nullptr);
+  ex->own_streams = side_streams == nullptr;
+  for (size_t i = 1; i < ex->streams.size(); ++i) {
+    if (side_streams) {
+      ex->streams[i] = static_cast<hipStream_t>(side_streams[i - 1]);
+      ok = ok && ex->streams[i] != nullptr;
+    } else {
+      ok = ok && hipStreamCreateWithFlags(&ex->streams[i], hipStreamNonBlocking) == hipSuccess;
+    }
+  }
   for (size_t k = 0; k < n && ok; ++k)
     if (ex->nodes[k].record) ok = hipEventCreateWithFlags(&ex->events[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&ex->fork, hipEventDisableTiming) == hipSuccess;
@@ -222,11 +236,13 @@ extern "C" int gmr_graph_exec_launch(void* exec, void* stream) {
   GMR_ARG(exec, "null executor");
   GraphExec* ex = static_cast<GraphExec*>(exec);
   const hipStream_t s0 = (hipStream_t)stream;
-  GX_HIP(hipEventRecord(ex->fork, s0));
-  for (hipStream_t s : ex->streams) GX_HIP(hipStreamWaitEvent(s, ex->fork, 0));
+  if (ex->streams.size() > 1) {
+    GX_HIP(hipEventRecord(ex->fork, s0));
+    for (size_t q = 1; q < ex->streams.size(); ++q) GX_HIP(hipStreamWaitEvent(ex->streams[q], ex->fork, 0));
+  }
   for (size_t k = 0; k < ex->nodes.size(); ++k) {
     const ExecNode& nd = ex->nodes[k];
-    const hipStream_t st = ex->streams[nd.stream];
+    const hipStream_t st = nd.stream ? ex->streams[nd.stream] : s0;
     for (int w : nd.waits) GX_HIP(hipStreamWaitEvent(st, ex->events[w], 0));
     if (nd.kind == NK_KERNEL) {
       GX_HIP(hipLaunchKernel(nd.kp.func, nd.kp.gridDim, nd.kp.blockDim, nd.kp.kernelParams, nd.kp.sharedMemBytes, st));
@@ -238,7 +254,7 @@ extern "C" int gmr_graph_exec_launch(void* exec, void* stream) {
     }
     if (nd.record) GX_HIP(hipEventRecord(ex->events[k], st));
   }
-  for (size_t q = 0; q < ex->streams.size(); ++q) {
+  for (size_t q = 1; q < ex->streams.size(); ++q) {
     GX_HIP(hipEventRecord(ex->joins[q], ex->streams[q]));
     GX_HIP(hipStreamWaitEvent(s0, ex->joins[q], 0));
   }

@@ -55,7 +55,7 @@ SIGNATURES = {
     "gmr_spmm_side_pack_classes": (I32, [P, P, P, P, P, P]),
     "gmr_spmm_side_tune": (I32, [I32, I32]),
     "gmr_spmm_side_f32": (I32, [P, I32, P, P, P, P, I64, F32, F32, P, P, P, I32, P]),
-    "gmr_graph_exec_create": (I32, [P, I32, P]),
+    "gmr_graph_exec_create": (I32, [P, I32, P, P]),
     "gmr_graph_exec_info": (I32, [P, P, P, P, P]),
     "gmr_graph_exec_launch": (I32, [P, P]),
     "gmr_graph_exec_destroy": (I32, [P]),

@@ -88,8 +88,10 @@ class Streams:
 
     SERIAL = False
 
+    PRIORITY = int(os.environ.get("GMR_SIDE_PRIO", "0"))  # torch stream priority of the side streams (-1: high)
+
     def __init__(self, n):
-        self.side = [torch.cuda.Stream() for _ in range(n)]
+        self.side = [torch.cuda.Stream(priority=Streams.PRIORITY) for _ in range(n)]
         self._raw = [ctypes.c_void_p(s.cuda_stream) for s in self.side]
         self._ids = [(s.stream_id, s.device_index, s.device_type) for s in self.side]
         self._dev = torch.cuda.current_device()
@@ -431,12 +433,18 @@ class GraphExec:
     """Native multi-stream executor of a captured step (include/gmr.h gmr_graph_exec_*): `graph` is a
     torch.cuda.CUDAGraph captured with keep_graph=True (kept referenced here: its nodes own the kernel arguments);
     launch() re-issues every node from C++ on the executor's streams, forked from and joined into the current
-    stream."""
+    stream.  `side`: a Streams whose side streams the executor issues on (the eager step's, so the hardware-queue
+    mapping is the same), else up to `n_side` streams of its own."""
 
-    def __init__(self, graph, max_streams=4):
+    def __init__(self, graph, side=None, n_side=2):
         self.graph = graph
         h = ctypes.c_void_p()
-        _lib.call("gmr_graph_exec_create", ctypes.c_void_p(graph.raw_cuda_graph()), int(max_streams), ctypes.byref(h))
+        arr = None
+        if side is not None:
+            n_side = len(side._raw)
+            arr = (ctypes.c_void_p * n_side)(*[r.value for r in side._raw])
+            self._side = side  # keep the streams alive
+        _lib.call("gmr_graph_exec_create", ctypes.c_void_p(graph.raw_cuda_graph()), int(n_side), arr, ctypes.byref(h))
         self.handle = h
 
     def info(self):

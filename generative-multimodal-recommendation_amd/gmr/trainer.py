@@ -29,9 +29,34 @@ from .utils import dict2str, early_stopping
 # keeps the score GEMM + mask + radix top-k over an E x I buffer (A/B)
 FUSED_EVAL = os.environ.get("GMR_EVAL_FUSED", "1") != "0"
 # graphed BPR steps (GMR_GRAPHS=1) re-issue the captured step through the native multi-stream executor
-# (K.GraphExec, csrc/graph_exec.hip) unless GMR_GRAPH_EXEC=0 (then hipGraphLaunch); GMR_GRAPH_STREAMS: its streams
+# (K.GraphExec, csrc/graph_exec.hip, on the model's own side streams) unless GMR_GRAPH_EXEC=0 (then hipGraphLaunch)
 GRAPH_EXEC = os.environ.get("GMR_GRAPH_EXEC", "1") != "0"
-GRAPH_EXEC_STREAMS = int(os.environ.get("GMR_GRAPH_STREAMS", "4"))
+
+
+_CAPTURE = {}
+
+
+def capture_graph(body, keep_graph=False):
+    """Capture body()'s launches into a torch.cuda.CUDAGraph on a side capture stream (the graph's own private
+    memory pool).  torch.cuda.graph() would also empty the allocator's cache on every
+    capture (each rebuilt epoch recaptures), so every later allocation of the epoch would go back to
+    hipMalloc; this does only what capture needs: the capture stream waits for the current one, and the
+    current one for the capture."""
+    dev = torch.cuda.current_device()
+    if dev not in _CAPTURE:
+        _CAPTURE[dev] = torch.cuda.Stream()
+    cs = _CAPTURE[dev]
+    g = torch.cuda.CUDAGraph(keep_graph=keep_graph)
+    cur = torch.cuda.current_stream()
+    cs.wait_stream(cur)
+    with torch.cuda.stream(cs):
+        g.capture_begin()
+        try:
+            body()
+        finally:
+            g.capture_end()
+    cur.wait_stream(cs)
+    return g
 
 
 def reduce_slab_grads(model, slabs):
@@ -162,14 +187,14 @@ class Trainer:
         if self._graph is None or self._graph[0] != key:
             self._graph = None
             static = [t.clone() for t in (u, p, ng, pb, pc)]
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph(keep_graph=True)
-            with torch.cuda.graph(g):
+
+            def body():
                 loss = self.model.rec_step(*static, norm_rows=norm, reg_share=share)
                 _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
+            g = capture_graph(body, keep_graph=True)
             runner = None
             if GRAPH_EXEC:  # the native multi-stream executor (csrc/graph_exec.hip); else hipGraphLaunch
-                runner = K.GraphExec(g, max_streams=GRAPH_EXEC_STREAMS)
+                runner = K.GraphExec(g, side=getattr(self.model, "_streams", None))
             else:
                 g.instantiate()
             self._graph = (key, g, static, runner)

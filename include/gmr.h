@@ -686,10 +686,11 @@ int gmr_adam_f32(int64_t n, float* param, const float* grad, float* exp_avg, flo
 
 /* ---------------------------------------------------------------- native graph executor (round 5)
  * A captured HIP graph (the BPR rec step, common/trainer.py:144-208; csrc/graph_exec.hip) re-issued from C++ on
- * up to max_streams internal streams: kernel / memset / memcpy / empty nodes in a topological order, each node
- * on the stream of a predecessor it continues, cross-stream edges as events; the launch forks from and joins
- * back into `stream`.  The graph must outlive the executor (its nodes own the kernel argument blocks). */
-int gmr_graph_exec_create(void* graph, int32_t max_streams, void** exec_out);
+ * the launch stream plus up to n_side side streams (the caller's `side_streams[0..n_side)`, or the executor's
+ * own when that is NULL): kernel / memset / memcpy / empty nodes in a topological order, each node on the stream
+ * of a predecessor it continues, cross-stream edges as events; the side streams fork from and join back into
+ * the launch `stream`.  The graph must outlive the executor (its nodes own the kernel argument blocks). */
+int gmr_graph_exec_create(void* graph, int32_t n_side, void* const* side_streams, void** exec_out);
 int gmr_graph_exec_info(const void* exec, int64_t* nodes, int64_t* kernels, int64_t* streams, int64_t* cross_edges);
 int gmr_graph_exec_launch(void* exec, void* stream);
 int gmr_graph_exec_destroy(void* exec);

@@ -44,11 +44,11 @@ def test_captured_rec_step_replays_eager(golden):
     assert torch.equal(m.rec_slab.grad.view(torch.int32), grad_e.view(torch.int32))
 
 
-@pytest.mark.parametrize("streams", [1, 2, 4])
+@pytest.mark.parametrize("streams", [0, 1, 3, "model"])
 def test_graph_executor_replays_eager(golden, streams):
-    """The native executor (gmr_graph_exec_*, csrc/graph_exec.hip) re-issues the captured step from C++ on its
-    own streams: loss and gradients equal the eager step's bit for bit for 1, 2 and 4 executor streams, and
-    repeated launches stay identical."""
+    """The native executor (gmr_graph_exec_*, csrc/graph_exec.hip) re-issues the captured step from C++ on the
+    launch stream plus side streams: loss and gradients equal the eager step's bit for bit with 0, 1 and 3 side
+    streams of its own and with the model's two side streams, and repeated launches stay identical."""
     from gmr import kernels as K
     g = golden("diffmm_tiny")
     m = build_model(g)
@@ -62,9 +62,10 @@ def test_graph_executor_replays_eager(golden, streams):
     graph = torch.cuda.CUDAGraph(keep_graph=True)
     with torch.cuda.graph(graph):
         loss_g = m.rec_step(*static)
-    ex = K.GraphExec(graph, max_streams=streams)
+    ex = K.GraphExec(graph, side=m._streams) if streams == "model" else K.GraphExec(graph, n_side=streams)
     info = ex.info()
-    assert info["kernels"] >= 30 and 1 <= info["streams"] <= streams, info
+    n_side = 2 if streams == "model" else streams
+    assert info["kernels"] >= 30 and 1 <= info["streams"] <= 1 + n_side, info
     for dst, src in zip(static, (*b1, *pl1)):
         dst.copy_(src)
     for _ in range(3):
