@@ -220,9 +220,13 @@ def _gemm_tag(A, B, trans_a, trans_b, M, N, K, tile, split_k):
     return "gemm_x6" if kind == 6 else "gemm"
 
 
-def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NONE, bias=None, bias_row=None,
-         ld_bias=0, aux=None, rv1=None, rv2=None, slope=0.0, tile=0, split_k=0):
-    """C = epi(alpha * op(A) @ op(B) ...), see include/gmr.h gmr_gemm_f32."""
+# gemm() call plans by (shapes, leading dimensions, dtypes, flags): the shape checks and the workspace size
+# are worked out once per call site.  GenRecV1 issues ~2,400 GEMMs per epoch and is host-issue-bound, so the
+# per-call Python work (~13 us before this cache) is kept to the pointer reads and the one ctypes call.
+_gemm_plans = {}
+
+
+def _gemm_plan(A, B, C, trans_a, trans_b, tile, split_k):
     M, N = C.shape
     K = A.shape[0] if trans_a else A.shape[1]
     if (A.shape[1] if trans_a else A.shape[0]) != M:
@@ -232,15 +236,32 @@ def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NON
     for t in (A, B, C):
         if t.dtype != torch.float32:
             raise TypeError("gemm is fp32")
+        if not t.is_cuda:
+            raise ValueError("gmr kernels take device tensors only (no CPU fallback)")
     tile |= GEMM_TILE_FLAGS
-    need = _lib.load().gmr_gemm_workspace_floats(int(trans_a), int(trans_b), M, N, K, tile, split_k)
+    need = int(_lib.load().gmr_gemm_workspace_floats(int(trans_a), int(trans_b), M, N, K, tile, split_k))
+    return M, N, K, tile, need, _ld(A), _ld(B), _ld(C)
+
+
+def gemm(A, B, C, trans_a=False, trans_b=False, alpha=1.0, beta=0.0, epi=EPI_NONE, bias=None, bias_row=None,
+         ld_bias=0, aux=None, rv1=None, rv2=None, slope=0.0, tile=0, split_k=0):
+    """C = epi(alpha * op(A) @ op(B) ...), see include/gmr.h gmr_gemm_f32."""
+    key = (A.shape, A.stride(), B.shape, B.stride(), C.shape, C.stride(), A.dtype, B.dtype, C.dtype, A.device,
+           trans_a, trans_b, tile, split_k, GEMM_TILE_FLAGS)
+    pl = _gemm_plans.get(key)
+    if pl is None:
+        pl = _gemm_plans[key] = _gemm_plan(A, B, C, trans_a, trans_b, tile, split_k)
+    M, N, K, tile, need, lda, ldb, ldc = pl
     ws = workspace(need, C.device) if need > 0 else None  # split-K partials only when this call splits
-    with _Probe(_gemm_tag(A, B, trans_a, trans_b, M, N, K, tile, split_k) if _probe is not None else "gemm",
-                (M, N, K, int(trans_a), int(trans_b), epi)):
-        _lib.call("gmr_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), ptr(A), _ld(A), ptr(B), _ld(B),
-                  float(beta), ptr(C), _ld(C), epi, ptr(bias), ptr(bias_row), ld_bias, ptr(aux),
-                  _ld(aux) if aux is not None else 0, ptr(rv1), ptr(rv2), float(slope), tile, split_k, ptr(ws),
-                  ws.numel() if ws is not None else 0, stream())
+    args = (int(trans_a), int(trans_b), M, N, K, float(alpha), A.data_ptr(), lda, B.data_ptr(), ldb, float(beta),
+            C.data_ptr(), ldc, epi, ptr(bias), ptr(bias_row), ld_bias, ptr(aux), _ld(aux) if aux is not None else 0,
+            ptr(rv1), ptr(rv2), float(slope), tile, split_k, ws.data_ptr() if ws is not None else None,
+            ws.numel() if ws is not None else 0, stream())
+    if _probe is None:
+        _lib.call("gmr_gemm_f32", *args)
+    else:
+        with _Probe(_gemm_tag(A, B, trans_a, trans_b, M, N, K, tile, split_k), (M, N, K, int(trans_a), int(trans_b), epi)):
+            _lib.call("gmr_gemm_f32", *args)
     return C
 
 

@@ -43,11 +43,21 @@ class Slab:
             return buf.as_strided(shape, (ld, 1), off)
         return buf[off:off + int(math.prod(shape))].view(shape)
 
+    # views are cached per name (GenRecV1's step reads ~8,000 parameter views per epoch and is host-issue-bound;
+    # building one costs ~2 us); a cached view is dropped when its buffer is no longer the slab's
     def view(self, name):
-        return self._view(self.data, name)
+        c = self.__dict__.setdefault("_vcache", {})
+        v = c.get(name)
+        if v is None or v[0] is not self.data:
+            v = c[name] = (self.data, self._view(self.data, name))
+        return v[1]
 
     def gview(self, name):
-        return self._view(self.grad, name)
+        c = self.__dict__.setdefault("_gcache", {})
+        v = c.get(name)
+        if v is None or v[0] is not self.grad:
+            v = c[name] = (self.grad, self._view(self.grad, name))
+        return v[1]
 
     def parameter(self, name):
         p = nn.Parameter(self.view(name))

@@ -1,7 +1,7 @@
-"""Host-side cost of the DiffMM BPR step: wall time of issuing N rec_steps without synchronising
-vs with, and a cProfile of the issuing loop (top entries by total time).
+"""Host-side profile (cProfile) of one warm epoch: where the host issue time goes (Python wrappers vs the
+ctypes calls into libgmr_hip.so, which include the HIP launch).
 
-python scripts/host_profile.py [--steps 30]
+python scripts/host_profile.py [--model genrecv1|diffmm] [--top 45]
 """
 import argparse
 import cProfile
@@ -21,34 +21,25 @@ import bench  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--model", default="genrecv1")
+    ap.add_argument("--top", type=int, default=45)
     a = ap.parse_args()
-    args = argparse.Namespace(model="diffmm", shape="baby", scoring_dtype=None)
+    args = argparse.Namespace(model=a.model, shape="tiktok" if a.model == "genrecv1" else "baby", scoring_dtype=None)
     cfg, ds, tr, tl, vl, model, trainer = bench.setup(args)
-    trainer._train_epoch(tl, 0)  # builds the UI graphs, warms every kernel
+    trainer._train_epoch(tl, 0)
     torch.cuda.synchronize()
-    d = tl.epoch()
-    batches = list(tl.batches(d))[:a.steps]
-
-    def run():
-        for _, _, u, p, ng, pb, pc in batches:
-            model.rec_step(u, p, ng, pb, pc)
-
-    run()
+    t = time.perf_counter()
+    trainer._train_epoch(tl, 1)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run()
-    t_issue = time.perf_counter() - t0
-    torch.cuda.synchronize()
-    t_all = time.perf_counter() - t0
-    print(f"{len(batches)} rec_steps: host issue {1e3 * t_issue / len(batches):.3f} ms/step, "
-          f"issue+drain {1e3 * t_all / len(batches):.3f} ms/step")
+    print(f"epoch (no profiler) {1e3 * (time.perf_counter() - t):.2f} ms", flush=True)
     pr = cProfile.Profile()
     pr.enable()
-    run()
-    pr.disable()
+    trainer._train_epoch(tl, 2)
     torch.cuda.synchronize()
-    pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+    pr.disable()
+    st = pstats.Stats(pr)
+    st.sort_stats("tottime").print_stats(a.top)
+    st.sort_stats("cumulative").print_stats(25)
 
 
 if __name__ == "__main__":
