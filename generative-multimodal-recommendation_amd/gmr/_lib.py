@@ -170,6 +170,8 @@ SIGNATURES = {
     "gmr_time_embedding": (I32, [I32, I32, P, P]),
     "gmr_silu_f32": (I32, [I64, P, P, P, P]),
     "gmr_xattn_table_f32": (I32, [I32, I32, I32, P, P, I64, F32, P, P]),
+    "gmr_decoder_layers_fwd_f32": (I32, [I64, I64, I32, I32, I32, P, P, I64, I32, F32, U64, U64, I64, I32, P, P, I32, P,
+                                         I64, P]),
     "gmr_xattn_fwd_f32": (I32, [I64, I32, I32, P, P, F32, P, P, I64, U64, U64, I64, P, I64, P]),
     "gmr_xattn_bwd_workspace_floats": (I64, [I64, I32, I32]),
     "gmr_xattn_bwd_f32": (I32, [I64, I32, I32, P, I64, P, I64, P, P, F32, P, P, P, I64, P]),

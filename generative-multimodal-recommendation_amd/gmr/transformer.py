@@ -35,6 +35,16 @@ def _round4(n):
 # fills 64 of 256 CUs and re-streams every weight plane per 32-row block, 1.49 ms per call vs ~0.7 ms for the
 # tiled GEMMs + row kernels (epoch 165 vs 121 ms, profiles/r04s_genrecv1_ab.txt)
 DEC_FUSED = os.environ.get("GMR_DEC_FUSED", "0") != "0"
+# the layer-by-layer decoder issued from C++ (gmr_decoder_layers_fwd_f32, csrc/decoder_host.hip): the same kernels
+# and arguments as the Python loop below (bit-identical), without its ~7 us of Python per launch; GMR_DEC_NATIVE=0
+# keeps the Python loop (A/B, and the path that takes injected masks)
+DEC_NATIVE = os.environ.get("GMR_DEC_NATIVE", "1") != "0"
+_DEC_OFFSETS = ("self_attn_in_proj_weight", "self_attn_in_proj_bias", "self_attn_out_proj_weight",
+                "self_attn_out_proj_bias", "norm1_weight", "norm1_bias", "multihead_attn_in_proj_bias",
+                "multihead_attn_out_proj_weight", "multihead_attn_out_proj_bias", "norm2_weight", "norm2_bias",
+                "linear1_weight", "linear1_bias", "linear2_weight", "linear2_bias", "norm3_weight", "norm3_bias")
+_DEC_BUFS = ("h", "V", "SAin", "SA", "s1", "h1", "m1", "CA", "s2", "h2", "F1", "F2", "s3", "m2", "m3", "cav",
+             "mask_a", "mask_c", "mask_1", "mask_2", "mask_3", "mask_f")
 
 
 class TransformerDenoiser:
@@ -90,6 +100,12 @@ class TransformerDenoiser:
                 "self_attn_in_proj_bias", "self_attn_out_proj_bias", "norm1_weight", "norm1_bias",
                 "multihead_attn_out_proj_bias", "norm2_weight", "norm2_bias", "linear1_bias", "linear2_bias",
                 "norm3_weight", "norm3_bias")])
+        # layer 0's slab offsets for gmr_decoder_layers_fwd_f32 (value rows / bias of in_proj: + 2 D)
+        p0 = "transformer_decoder_layers_0_"
+        self._lay_off = (ctypes.c_int64 * len(_DEC_OFFSETS))(*[
+            o[p0 + n] + (2 * D * D if n == "self_attn_in_proj_weight" else 2 * D if n.endswith("in_proj_bias") else 0)
+            for n in _DEC_OFFSETS])
+        self._lay_bufs = None
         self.training = True
         self._ws = None
         self._temb = None
@@ -207,9 +223,12 @@ class TransformerDenoiser:
         h = w["h"][0, :B]
         _lib.call("gmr_adaln_fwd", B, D, ptr(h0), D, ptr(t_rows), -1 if t_rows is not None else int(t_const), ptr(S),
                   2 * D, ptr(h), D, stream())
+        native = DEC_NATIVE and not fused and masks is None
         if fused:
             h = self._decoder_fused(w, B, h, train_drop, keep, seed, step, row0, keep_acts)
-        for l in range(L if not fused else 0):
+        elif native:
+            h = self._decoder_native(w, B, train_drop, keep, seed, step, row0, reuse)
+        for l in range(L if not (fused or native) else 0):
             p = f"transformer_decoder_layers_{l}_"
             wv = self.v(p + "self_attn_in_proj_weight")[2 * D:]
             bv = self.v(p + "self_attn_in_proj_bias")[2 * D:]
@@ -302,6 +321,23 @@ class TransformerDenoiser:
                   m1.stride(0), ctypes.cast(acts, ctypes.c_void_p) if acts is not None else None, D, w["h"].stride(0),
                   w["B"], stream())
         return out
+
+    def _decoder_native(self, w, B, train_drop, keep, seed, step, row0, reuse):
+        """The L decoder layers issued from C++ (gmr_decoder_layers_fwd_f32): the Python loop of forward()
+        with the same kernels and arguments.  Returns the last layer's rows w['h'][L, :B]."""
+        D, L = self.D, self.L
+        if self._lay_bufs is None or self._lay_bufs[0] is not w:
+            self._lay_bufs = (w, (ctypes.c_void_p * len(_DEC_BUFS))(*[w[k].data_ptr() for k in _DEC_BUFS]))
+        tile = K.GEMM_TILE_FLAGS
+        lib = _lib.load()
+        need = max(lib.gmr_gemm_workspace_floats(0, 1, B, D, D, tile, 0), lib.gmr_gemm_workspace_floats(0, 1, 1, D, D,
+                                                                                                        tile, 0))
+        ws = K.workspace(need, self.device) if need > 0 else None
+        _lib.call("gmr_decoder_layers_fwd_f32", B, w["B"], L, D, self.nhead, ptr(self.slab.data),
+                  ctypes.cast(self._lay_off, ctypes.c_void_p), self.layer_stride, int(train_drop), keep, seed, step,
+                  int(row0), int(bool(reuse)), ptr(w["xP"]), ctypes.cast(self._lay_bufs[1], ctypes.c_void_p), tile,
+                  ptr(ws), ws.numel() if ws is not None else 0, stream())
+        return w["h"][L, :B]
 
     def _drop(self, x, y, site, l, masks, keep, seed, step, row0, group, ldx=None):
         w = self._ws

@@ -674,6 +674,20 @@ int gmr_decoder_fwd_f32(int64_t B, int32_t L, int32_t D, int32_t nhead, const fl
                         const uint8_t* mask_1, const uint8_t* mask_2, const uint8_t* mask_3, const uint8_t* mask_f,
                         int64_t msd, float* const* acts, int64_t act_ld, int64_t act_stride, int64_t stat_rows,
                         void* stream);
+/* The same L decoder layers layer by layer, issued from C++ (csrc/decoder_host.hip, round 5): the kernels and
+ * arguments of gmr/transformer.py's Python layer loop (gmr_gemm_f32 NT products with `tile`, gmr_dropout_f32,
+ * gmr_layernorm_[drop_]fwd, gmr_xattn_fwd_f32 in train mode; the constant cross-attention row cav = b_v' Wo^T +
+ * b_o, recomputed unless reuse_cav, in eval mode), bit-identical to it, without its per-launch Python cost.
+ * offsets: 17 slab offsets of layer 0 (Wv = in_proj rows 2D..3D, bv, Wo, bo, norm1 w/b, b_v' = cross in_proj
+ * bias + 2D, Wo', bo', norm2 w/b, W1, b1, W2, b2, norm3 w/b), layer l at + l * layer_stride.  bufs: 22 device
+ * pointers of the activation workspace with Bmax rows per layer (h [L+1], V, SAin, SA, s1, h1, LN1 stats
+ * [L][3][Bmax], CA, s2, h2, F1, F2, s3, LN2 / LN3 stats, cav [L][D], masks a / c [L][Bmax][nhead], masks
+ * 1 / 2 / 3 / f [L][Bmax][D]; SAin, CA and the masks may be NULL in eval mode); h[0] is the input, h[L] the
+ * output.  gemm_ws: >= gmr_gemm_workspace_floats of the B x D x D and 1 x D x D products (zeroed counters). */
+int gmr_decoder_layers_fwd_f32(int64_t B, int64_t Bmax, int32_t L, int32_t D, int32_t nhead, const float* slab,
+                               const int64_t* offsets, int64_t layer_stride, int32_t train_drop, float p_keep,
+                               uint64_t seed, uint64_t step, int64_t row0, int32_t reuse_cav, const float* xP,
+                               void* const* bufs, int32_t tile, float* gemm_ws, int64_t gemm_ws_floats, void* stream);
 /* sinusoidal time embedding table T x E (:692-696); SiLU (dy == NULL) or its backward */
 int gmr_time_embedding(int32_t T, int32_t E, float* out, void* stream);
 int gmr_silu_f32(int64_t n, const float* x, const float* dy, float* y, void* stream);

@@ -124,3 +124,43 @@ def test_layernorm_drop_fwd_equals_mask_then_layernorm(B, row0, keep):
     assert 0.3 < res[0][0].float().mean().item() / keep < 1.7
     for x0, x1 in zip(*res):
         assert torch.equal(x0, x1)
+
+
+@pytest.mark.parametrize("train,B,L,row0", [(True, 300, 6, 0), (False, 300, 6, 0), (True, 37, 2, 1000),
+                                            (True, 2048, 6, 5), (False, 2048, 6, 0)])
+def test_native_layer_issue_bit_identical(train, B, L, row0, monkeypatch):
+    """The decoder layers issued from C++ (gmr_decoder_layers_fwd_f32, csrc/decoder_host.hip) against the
+    Python layer loop of transformer.forward: the same kernels with the same arguments, so the logits, every
+    stored activation and mask, the parameter gradients of the backward that reads them, and an eval-mode
+    forward reusing its tables (the p_sample steps) are equal bit for bit."""
+    from gmr import transformer as tr
+    I = 501
+    x = _x(B, I, B + L + 1)
+    t_rows = torch.as_tensor(np.random.default_rng(B).integers(0, 5, B).astype(np.int32)).to(DEV)
+    runs = []
+    for native in (False, True):
+        monkeypatch.setattr(tr, "DEC_NATIVE", native)
+        den = _den(I, 0.2, L)
+        den.train(train)
+        out = den.forward(x, t_rows=t_rows, T=5, seed=7, step=11, row0=row0)
+        r = {"out": out.cpu().numpy().copy()}
+        w = den._ws
+        for k in ("h", "V", "SA", "s1", "h1", "m1", "s2", "h2", "F1", "F2", "s3", "m2", "m3"):
+            # LayerNorm statistics (L, 3, Bmax): rows 0 / 1 = mean / rstd (row 2 is not written by the forward)
+            r[k] = w[k][:, :2, :B].cpu().numpy().copy() if k[0] == "m" else w[k][:, :B].cpu().numpy().copy()
+        if train:
+            for k in ("SAin", "CA"):
+                r[k] = w[k][:, :B].cpu().numpy().copy()
+            for k in ("a", "c", "1", "2", "3", "f"):
+                r["mask_" + k] = w["mask_" + k][:, :B].cpu().numpy().copy()
+        den.slab.grad.zero_()
+        dz = torch.ones_like(out) * 1e-3
+        den.backward(dz)
+        r["grad"] = den.slab.grad.cpu().numpy().copy()
+        if not train:
+            again = den.forward(x, t_rows=t_rows, T=5, seed=7, step=11, row0=row0, reuse_tables=True)
+            r["reuse"] = again.cpu().numpy().copy()
+        torch.cuda.synchronize()
+        runs.append(r)
+    for k in runs[0]:
+        np.testing.assert_array_equal(runs[1][k].view(np.uint8), runs[0][k].view(np.uint8), err_msg=k)
