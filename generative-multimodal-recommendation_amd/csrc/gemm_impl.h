@@ -361,6 +361,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const floatx16 (&acc)[BM / WGM
 
 // split-bf16 products (gemm_x6.hip) of an NT call with 16-byte aligned operands on a BM x BN tile
 // (128 x 128, 256 x 128 or 128 x 256); same grid, workspace and epilogue conventions as gemm.hip
+int x6_ring();  // gemm_x6.hip: the register-ring 64^2 split-bf16 kernel is on (GMR_X6_RING, default 1)
 int x6_launch(int bm, int bn, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
               const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n, int64_t kps, float* ws);
 

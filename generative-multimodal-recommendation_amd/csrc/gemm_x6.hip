@@ -145,6 +145,30 @@ __device__ __forceinline__ void x6_store_part(const float4 (&r)[N4], __bf16* s) 
   }
 }
 
+// one k tile of a k-contiguous operand straight into ring registers d (KcTile's offsets; full tile or the
+// zero-padded last one): the loads of later ring slots stay in flight while earlier slots are split
+template <int R, int NT, int N4>
+__device__ __forceinline__ void kc_fetch(float4 (&d)[N4], const KcTile<R, NT>& tl, const float* __restrict__ base,
+                                         bool full, int kleft) {
+  if (full) {
+#pragma unroll
+    for (int i = 0; i < N4; ++i) d[i] = *reinterpret_cast<const float4*>(base + tl.off[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N4; ++i) {
+      const int k4 = ((threadIdx.x + NT * i) % (BK / 4)) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k4 < kleft) {
+        v = *reinterpret_cast<const float4*>(base + tl.off[i]);
+        if (k4 + 1 >= kleft) v.y = 0.f;
+        if (k4 + 2 >= kleft) v.z = 0.f;
+        if (k4 + 3 >= kleft) v.w = 0.f;
+      }
+      d[i] = v;
+    }
+  }
+}
+
 // instruction order of one pipelined MFMA step: its NR fragment reads, then NM MFMAs, each followed
 // by NV VALU instructions of the next tile's split and, for the first NW, one of its LDS writes
 // (sched_group_barrier masks: 0x008 MFMA, 0x002 VALU, 0x100 DS read, 0x200 DS write)
@@ -245,7 +269,42 @@ __global__ void __launch_bounds__(64 * WGM * WGN, OCC) gemm_x6_kernel(int64_t M,
       rb.load_tail(b0 + k0, kl);
     }
   };
-  if constexpr (PIPE == 0) {
+  if constexpr (PIPE == 2) {
+    // register ring of PF k tiles (the small 64^2 tiles: one 4-wave block per CU at the 2,048-row GenRecV1
+    // products, 12 MFMAs per wave per k tile - one tile of prefetch left every k step waiting on its loads):
+    // tile t is split into LDS buffer t & 1, then the slot refills with tile t + PF while t is computed.
+    // One barrier per tile: a wave storing tile t has passed tile t - 1's barrier, which every wave reaches
+    // only after its compute of tile t - 2 (the previous user of buffer t & 1).
+    constexpr int PF = 4;
+    constexpr int NA = KcTile<BM, NT>::N4, NB = KcTile<BN, NT>::N4;
+    float4 qa[PF][NA], qb[PF][NB];
+    auto fetch_slot = [&](float4 (&da)[NA], float4 (&db)[NB], int t) {
+      if (t < nk) {
+        const int64_t k0 = kbeg + (int64_t)t * BK;
+        const bool full = t + 1 < nk || kl == BK;
+        kc_fetch<BM, NT, NA>(da, ra, a0 + k0, full, kl);
+        kc_fetch<BN, NT, NB>(db, rb, b0 + k0, full, kl);
+      }
+    };
+#pragma unroll
+    for (int q = 0; q < PF; ++q) fetch_slot(qa[q], qb[q], q);
+    for (int t0 = 0; t0 < nk; t0 += PF) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int t = t0 + q;
+        if (t < nk) {
+          __bf16* buf = smem + (t & 1) * STAGE;
+          x6_store<BM, true, NT>(qa[q], buf);
+          x6_store<BN, true, NT>(qb[q], buf + 3 * APL);
+          __syncthreads();
+          fetch_slot(qa[q], qb[q], t + PF);
+          mstep(buf, 0);
+          mstep(buf, 1);
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with the buffers before an LDS epilogue reuses them
+  } else if constexpr (PIPE == 0) {
   int cur = 0;
   if (nk > 0) {
     fetch(0);
@@ -374,6 +433,15 @@ static int x6_pipe() {
   return v;
 }
 
+// GMR_X6_RING = 0 turns off the register-ring 64^2 kernel (PIPE 2) and its unsplit plans (A/B)
+int x6_ring() {
+  static const int v = [] {
+    const char* e = getenv("GMR_X6_RING");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 static int x6_nb128() {
   static const int v = [] {
     const char* e = getenv("GMR_GEMM_X6_NB128");
@@ -399,6 +467,11 @@ int x6_launch(int bm, int bn, dim3 grid, hipStream_t st, int64_t M, int64_t N, i
   // the others' MFMA steps (GMR_GEMM_X6_NB128 = 1 / 3: always two / three single-buffered blocks,
   // = 2: one double-buffered block per CU; for A/B runs)
   // 64^2 (4 waves of 32^2, LDS double-buffered, 48 KiB: three blocks per CU) for the small products
+  if (bm == 64 && bn == 64 && x6_ring()) {
+    hipLaunchKernelGGL((gemm_x6_kernel<64, 64, 2, 2, 2, 3, 2>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C,
+                       ldc, epi, tiles_n, kps, ws);
+    return 0;
+  }
   if (bm == 64 && bn == 64) GMR_X6(64, 64, 2, 2, 2, 3)
   if (bm == 256 && bn == 128) GMR_X6(256, 128, 4, 2, 2, 1)
   if (bm == 128 && bn == 256) GMR_X6(128, 256, 2, 4, 2, 1)
