@@ -639,9 +639,10 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
       const int v = e ? atoi(e) : 0;
       return (int64_t)(v >= 64 ? v : 0);
     }();
-    // with the register-ring 64^2 kernel (gemm_x6.hip PIPE 2) the 64^2 plans keep >= 1024-deep slabs: the
-    // 2048 x 512 x 512 decoder products run unsplit (no partial slabs, no reduce launch)
-    const int64_t min_slab = min_slab_env ? min_slab_env : p.bm == 64 ? (x6_ring() ? 1024 : 256) : 512;
+    // with the register-ring 64^2 kernel (gemm_x6.hip PIPE 2) 64^2 products of K <= 1024 run unsplit (the
+    // 2048 x 512 x 512 decoder products: no partial slabs, no reduce launch); longer ones keep 256-deep slabs
+    // (their sums - e.g. VBPR's K = 4,480 item projection - stay the ones the parity tests pinned)
+    const int64_t min_slab = min_slab_env ? min_slab_env : p.bm == 64 ? (x6_ring() && K <= 1024 ? K : 256) : 512;
     const int64_t slots = p.bm == 64 ? 768 : p.bm * p.bn == 128 * 128 ? 512 : 256;
     splits = 1;
     while (p.tm * p.tn * splits * 5 < slots * 4 && K / (splits * 2) >= min_slab && splits < 16) splits *= 2;
