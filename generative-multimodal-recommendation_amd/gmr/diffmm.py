@@ -31,6 +31,12 @@ from .slab import Slab
 #   FUSE_BWD3  OutI / OutT / T2 (main stream)       FUSE_UI_T    OutI / OutT (cl side stream, T2 on main)
 # GMR_SPMM_FUSE overrides (0 = one launch per product, on side streams as before), for A/B runs
 FUSE_FWD, FUSE_BWD_CL, FUSE_BWD3, FUSE_UI_T = 1, 2, 4, 8
+# GMR_BWD_EARLY=1 (with FUSE_BWD3 and not FUSE_BWD_CL): the BPR branch of the backward (dEmb scatter, T1 =
+# adj^T dEmb, final_bwd, the modal-weight gradient) is issued on the main stream BEFORE the join with the two
+# InfoNCE passes, so it runs beside their tail instead of after it; the contrastive branch then runs on the
+# main stream after the join (no fork / join of its own).  Epoch 69.2 -> 67.7 ms, BPR phase 38.8 -> 37.5 ms
+# (three same-box pairs, profiles/r05z_bwd_early_ab.txt)
+BWD_EARLY = os.environ.get("GMR_BWD_EARLY", "1") != "0"
 # Since the side-split products take multi-job launches too (round 5, gmr_spmm_side_jobs_f32), OutI / OutT / T2
 # in one main-stream launch beats OutI / OutT on the side stream beside T2: epoch 68.5 / 69.0 vs 69.3 / 70.0 ms
 # (profiles/r05k_spmm_side_jobs_ab.txt; 70.9 / 70.4 with one launch per side-split product)
@@ -300,6 +306,8 @@ class DiffMM(GeneralRecommender):
                   ptr(w["contrib_bpr"]), 1.0 / nr, stream())
         loss = w["loss"][:1]
         _lib.call("gmr_sqnorm_part_f32", N * 64, ptr(E0), ptr(w["sqws"]), stream())
+        if BWD_EARLY and SPMM_FUSE & FUSE_BWD3 and not SPMM_FUSE & FUSE_BWD_CL:
+            return self._rec_bwd_early(w, users, plan_bpr, plan_cl, loss, nr, reg_share)
         st.join(0, 1)
         # BPR mean + regulariser + both InfoNCE means in one ordered reduction (calculate_loss, :243-249)
         _lib.call("gmr_dmm_loss_total", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(w["sqws"]), self._sq_parts,
@@ -364,6 +372,46 @@ class DiffMM(GeneralRecommender):
         _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
         adj.spmm(w["T3"], [(w["DG"][:, :64],), (w["DG"][:, 64:],)])
         st.join(0)
+        return self._rec_tail(w, loss, reg_share)
+
+    def _rec_bwd_early(self, w, users, plan_bpr, plan_cl, loss, nr, reg_share):
+        """The backward of rec_step with the BPR branch issued before the InfoNCE join (GMR_BWD_EARLY): the same
+        kernels and arguments as the FUSE_BWD3 path, in an order whose only cross-stream dependency is the join
+        before the contrastive branch (dCLN is written by the InfoNCE passes and the sorted scatter below)."""
+        N, U = self.N, self.n_users
+        B = users.numel()
+        s = self.rec_slab
+        st = self._streams
+        adj, iadj, tadj = self.norm_adj, self.image_UI_matrix, self.text_UI_matrix
+        dEmb, dCLN = w["dEmb"], w["dCLN"]
+        dK = dCLN
+        # BPR branch (main), beside the InfoNCE passes on the side streams
+        K.zero_(dEmb)
+        _lib.call("gmr_scatter_sorted_f32", plan_bpr.numel(), 64, ptr(plan_bpr), ptr(w["contrib_bpr"]), 64,
+                  ptr(dEmb), 64, stream())
+        adj.spmm(w["T1"], [(dEmb,)])                                            # adj^T dEmb (adj symmetric)
+        _lib.call("gmr_dmm_final_bwd", N, ptr(dEmb), ptr(w["T1"]), ptr(w["M"]), ptr(w["nrmM"]), self.ris_lambda,
+                  ptr(w["G"]), ptr(s.view("modal_weight")), ptr(w["dE"]), ptr(w["partials"]), stream())
+        _lib.call("gmr_dmm_mw_grad", w["partials"].numel() // 2, ptr(w["partials"]), ptr(s.view("modal_weight")),
+                  ptr(s.gview("modal_weight")), 0, stream())
+        st.join(0, 1)
+        # BPR mean + regulariser + both InfoNCE means in one ordered reduction (calculate_loss, :243-249)
+        _lib.call("gmr_dmm_loss_total", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(w["sqws"]), self._sq_parts,
+                  self.reg_weight * reg_share, ptr(w["loss_cu"]), ptr(w["loss_ci"]), self.ssl_reg / nr, ptr(loss),
+                  stream())
+        # contrastive branch (main): sparse terms into dCLN, dK = normalize backward, Tcl = adj^T dK
+        _lib.call("gmr_scatter_sorted_f32", plan_cl.numel(), 128, ptr(plan_cl), ptr(w["contrib_cl"]), 128,
+                  ptr(dCLN), 128, stream())
+        K.normalize_rows_bwd(w["CLN"][:, :64], w["nrmCL"][0], dCLN[:, :64], dK[:, :64])
+        K.normalize_rows_bwd(w["CLN"][:, 64:], w["nrmCL"][1], dCLN[:, 64:], dK[:, 64:])
+        adj.spmm(w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], partial=w["part_cl"])
+        _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
+                  ptr(w["Rt"]), stream())
+        K.spmm_jobs([(self._transpose_of(iadj), w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)], None, None),
+                     (self._transpose_of(tadj), w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)], None, None),
+                     (adj, w["T2"], [(w["dE"][:, :64],), (w["dE"][:, 64:],)], None, None)])
+        _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
+        adj.spmm(w["T3"], [(w["DG"][:, :64],), (w["DG"][:, 64:],)])
         return self._rec_tail(w, loss, reg_share)
 
     def _rec_tail(self, w, loss, reg_share):
