@@ -293,11 +293,14 @@ class DiffMM(GeneralRecommender):
         st = self._streams
 
         def contrast():
-            K.zero_(w["dCLN"])  # [:, 64:] is then overwritten by the d-table GEMMs, [:, :64] by scatters
-            # the two InfoNCE terms run side by side, beside the GCN layer of forward_MM
+            # the two InfoNCE terms run side by side, beside the GCN layer of forward_MM; each zeroes its own
+            # rows of dCLN first ([:, 64:] is then written by its table pass, [:, :64] by the scatters after the
+            # join), off the main stream
             with st.on(0):
+                K.zero_(w["dCLN"][:U])
                 self._contrast(w, users, 0, U, 0, w["loss_cu"], B, nr, slot="u")
             with st.on(1):
+                K.zero_(w["dCLN"][U:])
                 self._contrast(w, pos, U, I, B, w["loss_ci"], B, nr, slot="i")
 
         self._forward_mm(w, with_cl=True, on_cl=contrast)
@@ -395,10 +398,12 @@ class DiffMM(GeneralRecommender):
         _lib.call("gmr_dmm_mw_grad", w["partials"].numel() // 2, ptr(w["partials"]), ptr(s.view("modal_weight")),
                   ptr(s.gview("modal_weight")), 0, stream())
         st.join(0, 1)
-        # BPR mean + regulariser + both InfoNCE means in one ordered reduction (calculate_loss, :243-249)
-        _lib.call("gmr_dmm_loss_total", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(w["sqws"]), self._sq_parts,
-                  self.reg_weight * reg_share, ptr(w["loss_cu"]), ptr(w["loss_ci"]), self.ssl_reg / nr, ptr(loss),
-                  stream())
+        # BPR mean + regulariser + both InfoNCE means in one ordered reduction (calculate_loss, :243-249), on
+        # side stream 1 (nothing on the main stream reads it; _rec_tail joins stream 1)
+        with st.on(1):
+            _lib.call("gmr_dmm_loss_total", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(w["sqws"]), self._sq_parts,
+                      self.reg_weight * reg_share, ptr(w["loss_cu"]), ptr(w["loss_ci"]), self.ssl_reg / nr,
+                      ptr(loss), stream())
         # contrastive branch (main): sparse terms into dCLN, dK = normalize backward, Tcl = adj^T dK
         _lib.call("gmr_scatter_sorted_f32", plan_cl.numel(), 128, ptr(plan_cl), ptr(w["contrib_cl"]), 128,
                   ptr(dCLN), 128, stream())

@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 5 (za): dCLN zeroing and the loss reduction off the main stream: tests, epochs (GMR_BWD_EARLY=0 as reference)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_diffmm_gpu.py \
+  tests/test_graph_capture_gpu.py tests/test_phases_gpu.py tests/test_diffmm_baby_train_gpu.py tests/test_dist_gpu.py \
+  > gpurun_out/r05za_tests.log 2>&1 || exit $?
+for cfg in "GMR_BWD_EARLY=0" "GMR_BWD_EARLY=1" "GMR_BWD_EARLY=0" "GMR_BWD_EARLY=1" "GMR_BWD_EARLY=0" "GMR_BWD_EARLY=1"; do
+  echo "=== $cfg" >> gpurun_out/r05za_ab.txt
+  env $cfg GMR_PHASE_TIMES=1 timeout -k 10 200 python -u bench.py --model diffmm --no-legs --no-cpu-baseline --no-probe --steps 5 --warmup 1 2>gpurun_out/r05za_err.txt | cut -c1-200 >> gpurun_out/r05za_ab.txt || exit $?
+  grep phases gpurun_out/r05za_err.txt | tail -2 >> gpurun_out/r05za_ab.txt
+done
