@@ -15,6 +15,7 @@ Layout in HBM (N = U + I, d = 64): one rec slab [E0 = user_embedding; item_id_em
 every other rec parameter under its reference name], the denoiser slab, N x 64 activation tables.
 BatchNorm running statistics are kept per module and updated in the reference's call order.
 """
+import copy
 import ctypes
 import os
 import numpy as np
@@ -629,6 +630,13 @@ class GenRecV1(GeneralRecommender):
             self.set_image_ui_matrix(mk(g), mk(t) if t is not None else None)
 
 
+# GMR_GR_OVERLAP=0: GenRecV1's training step runs its value-only p_sample after the backward on one stream, and
+# the rebuild chunks one after another (default 1: side stream 0 through a twin context, see FlipDiffusion.twin).
+# Epoch 102.0-107.5 -> 92.3-93.8 ms (diffusion phase 45.1 -> 36.9 ms, rebuild 29.6 -> 22.8 ms;
+# profiles/r05zb_genrecv1_overlap_*.txt)
+OVERLAP_PSAMPLE = os.environ.get("GMR_GR_OVERLAP", "1") != "0"
+
+
 class FlipDiffusion:
     """FlipInterestDiffusion (models/genrecv1.py:460-648) over device batches of users.
 
@@ -656,6 +664,26 @@ class FlipDiffusion:
                    "L": f(B, (B + 3) // 4 * 4), "rows": f(B), "loss": f(4, dt=torch.float64), "lossf": f(2), "lossv": f(4),
                    "topk": f(B, max(self.m.gen_topk, 1), dt=torch.int32)}
         return self._w
+
+    def twin(self, den):
+        """(FlipDiffusion, denoiser) contexts over the same model and weights with private work buffers,
+        made once per denoiser: work issued on a side stream through them touches none of this context's
+        buffers (the training step's value-only p_sample beside its backward; alternate rebuild chunks)."""
+        tw = self.__dict__.get("_tw")
+        if tw is None or tw[0] is not den:
+            d2 = copy.copy(self)
+            d2.__dict__.pop("_tw", None)
+            d2._w, d2._parts, d2._picks, d2._npicks, d2._keys = None, None, None, None, None
+            tw = self._tw = (den, d2, den.twin())
+        tw[2].training, tw[2].p = den.training, den.p
+        return tw[1], tw[2]
+
+    def side(self):
+        """The side stream of the twin-context work (K.Streams(1)), made on first use."""
+        st = self.__dict__.get("_side")
+        if st is None:
+            st = self._side = K.Streams(1)
+        return st
 
     def densify(self, users):
         B = users.numel()
@@ -728,14 +756,27 @@ class FlipDiffusion:
         den.forward(xt, t_rows=t, T=T, out=z, masks=inj.get("den_masks"), seed=seed, step=step * 16 + 14, row0=row0)
         _lib.call("gmr_flip_loss_rows", B, I, ptr(x0), x0.stride(0), ptr(z), z.stride(0), ptr(t), ptr(tab), T,
                   1.0 / (nr * I), ptr(dz), dz.stride(0), ptr(w["bce"]), ptr(w["kl"]), stream())
+        ps_inj = {"flip": inj.get("ps_flip"), "draws": inj.get("ps_draws")}
+        if OVERLAP_PSAMPLE and (rank_rows is None or len(rank_rows) == 1):
+            # the value-only p_sample + InfoNCE (:577-582) reads x0, the schedule and the weights, none of which
+            # the backward writes: it runs on side stream 0 through the twin context, beside the backward;
+            # the join below comes before the caller's Adam step
+            d2, den2 = self.twin(den)
+            d2._work(B)
+            st = self.side()
+            with st.on(0):
+                gen, _ = d2.p_sample(den2, x0, tab, seed, step + 1, inject=ps_inj, row0=row0)
+                cl = d2.infonce_value(x0, gen, item_embeds, feats, row0, rank_rows)
         den.backward(dz)
         loss = w["loss"]
         _lib.call("gmr_sum_f64", B, ptr(w["bce"]), 1.0 / (nr * I), ptr(loss[0:1]), 0, stream())
         _lib.call("gmr_sum_f64", B, ptr(w["kl"]), 1.0 / nr, ptr(loss[1:2]), 0, stream())
-        # InfoNCE(x0 (iE * feats), p_sample(x0) (iE * feats)) — value only (:577-582)
-        gen, _ = self.p_sample(den, x0, tab, seed, step + 1, inject={"flip": inj.get("ps_flip"),
-                                                                     "draws": inj.get("ps_draws")}, row0=row0)
-        cl = self.infonce_value(x0, gen, item_embeds, feats, row0, rank_rows)
+        if OVERLAP_PSAMPLE and (rank_rows is None or len(rank_rows) == 1):
+            st.join(0)
+        else:
+            # InfoNCE(x0 (iE * feats), p_sample(x0) (iE * feats)) — value only (:577-582)
+            gen, _ = self.p_sample(den, x0, tab, seed, step + 1, inject=ps_inj, row0=row0)
+            cl = self.infonce_value(x0, gen, item_embeds, feats, row0, rank_rows)
         out = w["lossv"]
         _lib.call("gmr_flip_total", ptr(loss), ptr(cl), 0.01, ptr(out), stream())
         return out

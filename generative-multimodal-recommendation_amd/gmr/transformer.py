@@ -12,6 +12,7 @@ once per call.  Forward keeps every activation the hand-derived backward needs.
 Parameters live in one Slab under the reference's parameter names ('.' -> '_'); Q/K rows of the
 in_proj matrices and the unused `time_emb` MLP are kept (zero gradient) so state dicts line up.
 """
+import copy
 import ctypes
 import math
 import os
@@ -111,6 +112,14 @@ class TransformerDenoiser:
         self._temb = None
         self._seed = 0
         self._call = 0
+
+    def twin(self):
+        """A second denoiser over the same slab (weights and gradients shared) with private work buffers and
+        table caches: a forward issued on another stream beside this one's work (GenRecV1's value-only
+        p_sample beside the training backward, the rebuild chunks) touches none of this one's buffers."""
+        t = copy.copy(self)
+        t._ws, t._cache, t._lay_bufs, t._dec_planes, t._planes_ok, t._last = None, None, None, None, False, None
+        return t
 
     # ------------------------------------------------------------------ parameters
     def v(self, name):
