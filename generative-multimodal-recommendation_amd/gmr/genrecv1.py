@@ -635,6 +635,10 @@ class GenRecV1(GeneralRecommender):
 # Epoch 102.0-107.5 -> 92.3-93.8 ms (diffusion phase 45.1 -> 36.9 ms, rebuild 29.6 -> 22.8 ms;
 # profiles/r05zb_genrecv1_overlap_*.txt)
 OVERLAP_PSAMPLE = os.environ.get("GMR_GR_OVERLAP", "1") != "0"
+# streams the rebuild chunks are dealt over (the main stream + REBUILD_STREAMS - 1 side streams, each chunk through
+# its stream's context); GMR_GR_REBUILD_STREAMS overrides, for A/B runs.  Two beat three: epoch 88.6-90.2 vs
+# 92.4 ms (profiles/r05zc_genrecv1_rebuild_streams_ab.txt)
+REBUILD_STREAMS = int(os.environ.get("GMR_GR_REBUILD_STREAMS", "2"))
 
 
 class FlipDiffusion:
@@ -665,24 +669,25 @@ class FlipDiffusion:
                    "topk": f(B, max(self.m.gen_topk, 1), dt=torch.int32)}
         return self._w
 
-    def twin(self, den):
-        """(FlipDiffusion, denoiser) contexts over the same model and weights with private work buffers,
-        made once per denoiser: work issued on a side stream through them touches none of this context's
-        buffers (the training step's value-only p_sample beside its backward; alternate rebuild chunks)."""
-        tw = self.__dict__.get("_tw")
+    def twin(self, den, k=1):
+        """The k-th (FlipDiffusion, denoiser) context (k >= 1) over the same model and weights with private work
+        buffers, made once per denoiser: work issued on side stream k - 1 through it touches none of another
+        context's buffers (the training step's value-only p_sample beside its backward; the rebuild chunks)."""
+        tws = self.__dict__.setdefault("_tw", {})
+        tw = tws.get(k)
         if tw is None or tw[0] is not den:
             d2 = copy.copy(self)
             d2.__dict__.pop("_tw", None)
             d2._w, d2._parts, d2._picks, d2._npicks, d2._keys = None, None, None, None, None
-            tw = self._tw = (den, d2, den.twin())
+            tw = tws[k] = (den, d2, den.twin())
         tw[2].training, tw[2].p = den.training, den.p
         return tw[1], tw[2]
 
     def side(self):
-        """The side stream of the twin-context work (K.Streams(1)), made on first use."""
+        """The side streams of the twin-context work (K.Streams(2)), made on first use."""
         st = self.__dict__.get("_side")
         if st is None:
-            st = self._side = K.Streams(1)
+            st = self._side = K.Streams(REBUILD_STREAMS - 1 if REBUILD_STREAMS > 1 else 1)
         return st
 
     def densify(self, users):

@@ -581,20 +581,22 @@ class GenRecV1Trainer(Trainer):
         den, diff = m.denoise_model_image, m.diffusion_model
         labels = self.multimodal_interest_space["image_modal"] if self.debias else None
         base = self._epoch_ctr * 100000 * 1000
-        from .genrecv1 import OVERLAP_PSAMPLE
-        st = diff.side()
+        from .genrecv1 import OVERLAP_PSAMPLE, REBUILD_STREAMS
+        nst = max(1, REBUILD_STREAMS) if OVERLAP_PSAMPLE else 1
+        st = diff.side() if nst > 1 else None
         for q, (j, lo) in enumerate((j, lo) for j, lo in enumerate(range(0, U, B)) if j % W == r):
             hi = min(U, lo + B)
-            if OVERLAP_PSAMPLE and q % 2 == 1:  # every other chunk on side stream 0 through the twin context
-                d2, den2 = diff.twin(den)
-                with st.on(0):
+            k = q % nst
+            if k:  # chunk q on side stream k - 1 through twin context k
+                d2, den2 = diff.twin(den, k)
+                with st.on(k - 1):
                     d2.rebuild_rows(den2, self._users[lo:hi], topk[lo:hi], labels, self.sample_ratio, m.seed,
                                     base + 4 * j)
             else:
                 diff.rebuild_rows(den, self._users[lo:hi], topk[lo:hi], labels, self.sample_ratio, m.seed,
                                   base + 4 * j)
-        if OVERLAP_PSAMPLE:
-            st.join(0)
+        if st is not None:
+            st.join(*range(nst - 1))
         dist.all_reduce_(topk)
         uptr = torch.empty(U + 1, dtype=torch.int32, device=dev)
         uitems = torch.empty(U * kr, dtype=torch.int32, device=dev)
