@@ -687,7 +687,6 @@ class DiffMM(GeneralRecommender):
         topks = [torch.zeros((W * size, k), dtype=torch.int32, device=dev) for _ in range(2)]
         uptr = torch.empty(U + 1, dtype=torch.int32, device=dev)
         uitems = torch.empty(U * k, dtype=torch.int32, device=dev)
-        graphs = []
         dens = (self.denoise_model_image, self.denoise_model_text)
 
         def sample(j):
@@ -696,13 +695,18 @@ class DiffMM(GeneralRecommender):
                 self.p_sample_topk(dens[j], lo, min(hi_r, lo + chunk), topks[j], k, w1t_fresh=True, slot=j)
 
         # the two p_sample sweeps are independent: text on a side stream beside image (own buffers);
-        # the graph builds (one host sync each, for the SpMM plan header) follow on the main stream
+        # the graph builds (one host sync each, for the SpMM plan header) follow on the main stream.  One
+        # process: the image graph is built right after its sweep, so its host sync (which waits for the main
+        # stream only) and host-side plan packing overlap the text sweep
         st = self._streams
         with st.on(1):
             sample(1)
         sample(0)
-        st.join(1)
-        for j, topk in enumerate(topks):
+        early = W == 1
+        graphs = [None, None]
+
+        def build(j):
+            topk = topks[j]
             dist.all_gather_rows_(topk, size)
             K.topk_to_user_csr(topk[:U], uptr, uitems)
             g = K.bipartite_symnorm(U, I, uptr, uitems, self_loops=True, deg_eps=0.0)
@@ -710,9 +714,16 @@ class DiffMM(GeneralRecommender):
                 # SpAdjDropEdge (diffmm.py:287-301): entry kept iff floor(u + keep) >= 1, value / keep;
                 # the same Philox draws give the transpose for the backward (same on every rank)
                 st_id = 6000 + 2 * self._rebuilds + j
-                graphs.append((K.csr_drop_edges(g, self.keepRate, seed=self.seed, step=st_id),
-                               K.csr_drop_edges(g, self.keepRate, seed=self.seed, step=st_id, transposed=True)))
+                graphs[j] = (K.csr_drop_edges(g, self.keepRate, seed=self.seed, step=st_id),
+                             K.csr_drop_edges(g, self.keepRate, seed=self.seed, step=st_id, transposed=True))
             else:
-                graphs.append((g, None))
+                graphs[j] = (g, None)
+
+        if early:
+            build(0)
+        st.join(1)
+        if not early:
+            build(0)
+        build(1)
         self._rebuilds += 1
         self.set_ui_matrices(graphs[0][0], graphs[1][0], graphs[0][1], graphs[1][1])
