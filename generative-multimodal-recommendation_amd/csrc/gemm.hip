@@ -604,6 +604,10 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
     else if (!tnm && wide256) tile = 256;
     else if (!tnm && M * N >= (int64_t)8 << 20 && K >= 512) tile = 128;
     else if (!tnm && M * N >= (int64_t)1 << 20 && K >= 4096) tile = 128;
+    // N <= 64 NN products of many rows and long K (the item-feature projections, 7050 x 64 x 4096): 128 x 64
+    // tiles, four 64 x 32 wave tiles with two accumulator chains each, 8 slabs: 54.1 -> 49.7 us
+    // (profiles/r05zp_tile12864.txt; the TN gradient moves < 1 %, so it keeps 64^2)
+    else if (!ta && !tb && N <= 64 && M >= 4096 && K >= 2048) tile = 12864;
     else tile = 64;
   }
   // split-bf16 plans take 128^2 instead of 64^2 for products of >= 4M outputs (the denoiser weight
@@ -611,7 +615,7 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
   if (x6 && tile == 64 && M * N >= ((int64_t)4 << 20) && K >= 256) tile = 128;
   // the split-bf16 kernel (gemm_x6.hip): NT products on 128^2, 256 x 128, 128 x 256 and 256^2 tiles
   // (the 256^2 tile maps to 256 x 128: a 2-wave-per-SIMD 256^2 block spills its prefetch registers)
-  if (x6 && (tile != 64 || x6_64) && !ta && tb) {
+  if (x6 && (tile != 64 || x6_64) && tile != 12864 && !ta && tb) {  // (no 128 x 64 split-bf16 tile)
     mf = 6;
     // products with >= 768 128^2 tiles run three 128^2 blocks per CU (gemm_x6.hip), which beat
     // 256 x 128 there (19445 x 1000 x 7050: 1852 -> 1605 us); smaller ones keep 256 x 128
@@ -621,8 +625,8 @@ Plan make_plan_core(int ta, int tb, int64_t M, int64_t N, int64_t K, int tile, i
   p.mf = mf;
   p.glds = glds && mf == 32;
   p.tile = tile;
-  p.bm = tile == 256128 ? 256 : tile == 128256 ? 128 : tile;
-  p.bn = tile == 256128 ? 128 : tile == 128256 ? 256 : tile;
+  p.bm = tile == 256128 ? 256 : tile == 128256 || tile == 12864 ? 128 : tile;
+  p.bn = tile == 256128 ? 128 : tile == 128256 ? 256 : tile == 12864 ? 64 : tile;
   p.tm = (M + p.bm - 1) / p.bm;
   p.tn = (N + p.bn - 1) / p.bn;
   int splits = split_k;
@@ -731,8 +735,8 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   {
     const int t = tile & ~(GMR_GEMM_MFMA16 | GMR_GEMM_MFMA32 | GMR_GEMM_GLDS | GMR_GEMM_REGSTAGE | GMR_GEMM_X6 |
                            GMR_GEMM_F32);
-    GMR_ARG(t == 0 || t == 64 || t == 128 || t == 256 || t == 256128 || t == 128256,
-            "tile must be 0 (auto), 64, 128, 256, 256128 or 128256 (| GMR_GEMM_MFMA16 / GMR_GEMM_MFMA32)");
+    GMR_ARG(t == 0 || t == 64 || t == 128 || t == 256 || t == 256128 || t == 128256 || t == 12864,
+            "tile must be 0 (auto), 64, 128, 256, 256128, 128256 or 12864 (| GMR_GEMM_MFMA16 / GMR_GEMM_MFMA32)");
   }
   Epi e;
   e.kind = epilogue;
@@ -801,6 +805,9 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
       break;
     case 128256:
       launch_tile<128, 256, 2, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
+      break;
+    case 12864:
+      launch_tile<128, 64, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
       break;
     case 128:
       launch_tile<128, 128, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);

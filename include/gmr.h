@@ -224,7 +224,7 @@ int gmr_topk_to_user_csr(int64_t n_users, int32_t k, const int32_t* topk, int64_
  * C[M,N] = epilogue(alpha * op(A) op(B)); op(A) = A (M x K, lda) or A^T (A stored K x M);
  * op(B) = B (K x N, ldb) or B^T (B stored N x K).  bias[(bias_row ? bias_row[m] : 0)*ld_bias + n].
  * Replaces nn.Linear / torch.mm / matmul: diffmm.py:117,124,277,352-358,472-473; vbpr.py:70,105.
- * tile: 0 auto, 64, 128, 256, 256128 (256 x 128) or 128256, optionally | GMR_GEMM_MFMA16 (v_mfma_f32_16x16x4_f32)
+ * tile: 0 auto, 64, 128, 256, 256128 (256 x 128), 128256 or 12864 (128 x 64, fp32 kernel only), optionally | GMR_GEMM_MFMA16 (v_mfma_f32_16x16x4_f32)
  * or | GMR_GEMM_MFMA32 (v_mfma_f32_32x32x2_f32) to force the matrix instruction, | GMR_GEMM_REGSTAGE /
  * GMR_GEMM_GLDS to force register or global_load_lds operand staging (same sums, bit for bit);
  * split_k: 0 auto, else >= 1.

@@ -637,7 +637,7 @@ def test_spmm_jobs_bit_exact(K):
                      (g3, _dev(Y3.copy()), [(X3,)], None, None)])
 
 
-@pytest.mark.parametrize("tile", [64, 128, 256, 256128, 128256])
+@pytest.mark.parametrize("tile", [64, 128, 256, 256128, 128256, 12864])
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
 def test_gemm_glds_bit_exact_vs_register_staging(K, tile, ta, tb):
     """global_load_lds operand staging (GMR_GEMM_GLDS, swizzled k-contiguous LDS images) gives the
