@@ -109,20 +109,22 @@ def setup(args):
 
 
 def pmc_summary(model="diffmm", shape=None):
-    """Per-kernel-class memory-side bytes and MFMA busy cycles of this workload from the newest
-    profiles/*_pmc_<tag>.json made by scripts/pmc_collect.sh, used only when it was measured on
-    the library now loaded (same SHA-256)."""
+    """Per-kernel-class memory-side bytes and MFMA busy cycles of this workload from the last (by name)
+    profiles/*_pmc_<tag>.json made by scripts/pmc_collect.sh that was measured on the library now loaded
+    (same SHA-256); none when no summary matches."""
     import glob
     tag = model if shape in (None, DEFAULT_SHAPE.get(model)) else f"{model}_{shape}"
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{tag}.json")))
     if not files:
         return {}, None, "no PMC summary of this workload in profiles/"
-    with open(files[-1]) as f:
-        d = json.load(f)
+    sha = lib_sha256()
+    for fn in reversed(files):  # a summary measured on the loaded library, whatever its tag sorts as
+        with open(fn) as f:
+            d = json.load(f)
+        if d.get("lib_sha256") == sha:
+            return d, os.path.relpath(fn, ROOT), None
     src = os.path.relpath(files[-1], ROOT)
-    if d.get("lib_sha256") != lib_sha256():
-        return {}, src, f"{src} measured another build (lib_sha256 differs): not used"
-    return d, src, None
+    return {}, src, f"no profiles/*_pmc_{tag}.json measured this build (lib_sha256 differs): not used"
 
 
 def summarize_probe(p, model="diffmm", shape=None):

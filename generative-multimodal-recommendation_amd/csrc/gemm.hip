@@ -428,7 +428,7 @@ void launch_t(bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t
               int64_t kps, float* ws, int* counters) {
   const dim3 blk(64 * WGM * WGN);
   if constexpr (MF == 6) {  // split-bf16 kernel (gemm_x6.hip): NT products, 16-byte aligned (make_plan)
-    x6_launch(BM, BN, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);
+    x6_launch(BM, BN, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws, AKC, BKC);
     return;
   } else {
   if constexpr (MF == 32) {
@@ -756,6 +756,11 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   // the split-bf16 kernel loads float4 granules: operands it reads in place must be 16-byte aligned
   if (pl.mf == 6 && !(((pl.xpose & 1) || a16) && ((pl.xpose & 2) || b16)))
     pl = make_plan_core(trans_a, trans_b, M, N, K, tile, split_k, false);
+  // GMR_X6_INPLACE = 1 / 2 (opt-in, gemm_x6.hip x6_inplace): TN / NN split-bf16 plans read their n- (and
+  // m-) contiguous operands in place (MnTile, single-float loads: any alignment) instead of copying them
+  // k-contiguous.  TT calls (A m-contiguous, B k-contiguous) always copy.
+  if ((pl.xpose & 2) && x6_inplace()) pl.xpose &= ~2;
+  if (pl.xpose == 1 && !trans_b && x6_inplace() == 2) pl.xpose = 0;
   const WsLayout wl = ws_layout(pl, M, N, K);
   if (pl.xpose) {
     GMR_ARG(workspace && workspace_floats >= wl.total, "needs workspace of gmr_gemm_workspace_floats(...) floats");
@@ -772,9 +777,9 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
       B = workspace + wl.bt;
       ldb = wl.kp;
     }
-    trans_a = 0;
-    trans_b = 1;
-    vec = true;
+    if (pl.xpose & 1) trans_a = 0;
+    if (pl.xpose & 2) trans_b = 1;
+    vec = (pl.xpose & 1 ? true : a16) && (pl.xpose & 2 ? true : b16);
   }
   tile = pl.tile;
   const int64_t tm = pl.tm, tn = pl.tn, kps = pl.kps;

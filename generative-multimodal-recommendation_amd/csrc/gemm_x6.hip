@@ -2,6 +2,8 @@
 // Same operand, epilogue, split-K and tile-order conventions as gemm.hip (gemm_impl.h).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "gemm_impl.h"
 
 namespace {
@@ -119,6 +121,57 @@ struct KcTile {
   }
 };
 
+// m- / n-contiguous operand tile (A stored K x M of a TN call, B stored K x N of an NN / TN call) read in place:
+// each thread owns one row of the tile and E = R x BK / NT consecutive k of it (8 or 16), loaded as single
+// floats (the 64 lanes of a load read 64 consecutive rows at one k: 256 contiguous bytes), so after the split
+// it writes 16-byte chunks of its own row: the same plane images as KcTile's, with no transposed copy in HBM,
+// and consecutive lanes write consecutive 64-byte rows (the 4-row quads of a float4 mapping all hit one half
+// of the banks and ran the TN gradients 8-10 % slower than copy + k-contiguous, profiles/r05zs_*).  Rows past
+// the operand's end load its last row (any alignment) and only reach C rows / columns the epilogue discards;
+// k past the slab's end is zeroed, never loaded.
+template <int R, int NT>
+struct MnTile {
+  static constexpr int E = R * BK / NT;  // k per thread
+  static_assert(E % 8 == 0 && NT % R == 0, "whole 8-k chunks of one row per thread");
+  int off;  // element offset of (this thread's row, its first k) from the tile's (r0, k0)
+  int rr;   // the row within the tile
+  int kt;   // its first k
+  int64_t ld;
+  float v[E];
+
+  __device__ __forceinline__ void init(int64_t r0, int64_t nrows, int64_t ld_) {
+    ld = ld_;
+    rr = threadIdx.x % R;
+    kt = (threadIdx.x / R) * E;
+    off = (int)(kt * ld + (min(r0 + rr, nrows - 1) - r0));
+  }
+  // base = element (row r0, k0); kleft = valid k of this tile (BK for a full one)
+  __device__ __forceinline__ void load(const float* __restrict__ base, int kleft) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = (kleft == BK || kt + e < kleft) ? base[off + e * ld] : 0.f;
+  }
+  // the three bf16 planes of one LDS stage (plane stride PL elements), KcTile / x6_store's image
+  __device__ __forceinline__ void store(__bf16* s) const {
+    constexpr int PL = R * BK;
+#pragma unroll
+    for (int c = 0; c < E / 8; ++c) {
+      bf16x8 h, m, l;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 a, b, d;
+        split3(v[8 * c + e], a, b, d);
+        h[e] = a;
+        m[e] = b;
+        l[e] = d;
+      }
+      const int o = rr * BK + ((((kt >> 3) + c) ^ x6_swz(rr)) << 3);
+      *reinterpret_cast<bf16x8*>(s + o) = h;
+      *reinterpret_cast<bf16x8*>(s + PL + o) = m;
+      *reinterpret_cast<bf16x8*>(s + 2 * PL + o) = l;
+    }
+  }
+};
+
 // NT products (A [M][K], B [N][K], both k-contiguous, 16-byte aligned, lda / ldb multiples of 4)
 // float4 granules [I0, I1) of a k-contiguous register tile -> the three bf16 planes (as x6_store)
 template <int R, int NT, int N4, int I0, int I1>
@@ -183,7 +236,7 @@ __device__ __forceinline__ void x6_interleave() {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int NBUF, int OCC, int PIPE>
+template <int BM, int BN, int WGM, int WGN, int NBUF, int OCC, int PIPE, bool AKC = true, bool BKC = true>
 __global__ void __launch_bounds__(64 * WGM * WGN, OCC) gemm_x6_kernel(int64_t M, int64_t N, int64_t K,
                                                                 const float* __restrict__ A, int64_t lda,
                                                                 const float* __restrict__ B, int64_t ldb,
@@ -251,23 +304,41 @@ __global__ void __launch_bounds__(64 * WGM * WGN, OCC) gemm_x6_kernel(int64_t M,
     }
   };
 
-  KcTile<BM, NT> ra;
-  KcTile<BN, NT> rb;
+  static_assert((AKC && BKC) || PIPE == 0, "m- / n-contiguous operands: the PIPE 0 loop only");
+  std::conditional_t<AKC, KcTile<BM, NT>, MnTile<BM, NT>> ra;
+  std::conditional_t<BKC, KcTile<BN, NT>, MnTile<BN, NT>> rb;
   ra.init(m0, M, lda);
   rb.init(n0, N, ldb);
-  const float* a0 = A + m0 * lda;
-  const float* b0 = B + n0 * ldb;
+  const float* a0 = AKC ? A + m0 * lda : A + m0;
+  const float* b0 = BKC ? B + n0 * ldb : B + n0;
   const int nk = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
   const int kl = (int)(kend - kbeg - (int64_t)(nk - 1) * BK);  // k in the last tile (1..32)
   auto fetch = [&](int t) {
     const int64_t k0 = kbeg + (int64_t)t * BK;
-    if (t + 1 < nk || kl == BK) {
-      ra.load(a0 + k0);
-      rb.load(b0 + k0);
+    if constexpr (AKC && BKC) {
+      if (t + 1 < nk || kl == BK) {
+        ra.load(a0 + k0);
+        rb.load(b0 + k0);
+      } else {
+        ra.load_tail(a0 + k0, kl);
+        rb.load_tail(b0 + k0, kl);
+      }
     } else {
-      ra.load_tail(a0 + k0, kl);
-      rb.load_tail(b0 + k0, kl);
+      const int kleft = t + 1 < nk ? BK : kl;
+      if constexpr (AKC) {
+        if (kleft == BK) ra.load(a0 + k0);
+        else ra.load_tail(a0 + k0, kleft);
+      } else {
+        ra.load(a0 + k0 * lda, kleft);
+      }
+      rb.load(b0 + k0 * ldb, kleft);
     }
+  };
+  auto store = [&](__bf16* s) {  // the registers of one k tile -> the planes of one LDS stage
+    if constexpr (AKC) x6_store<BM, true, NT>(ra.r, s);
+    else ra.store(s);
+    if constexpr (BKC) x6_store<BN, true, NT>(rb.r, s + 3 * APL);
+    else rb.store(s + 3 * APL);
   };
   if constexpr (PIPE == 2) {
     // register ring of PF k tiles (the small 64^2 tiles: one 4-wave block per CU at the 2,048-row GenRecV1
@@ -308,8 +379,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, OCC) gemm_x6_kernel(int64_t M,
   int cur = 0;
   if (nk > 0) {
     fetch(0);
-    x6_store<BM, true, NT>(ra.r, smem);
-    x6_store<BN, true, NT>(rb.r, smem + 3 * APL);
+    store(smem);
   }
   __syncthreads();
   for (int t = 0; t < nk; ++t) {
@@ -319,18 +389,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN, OCC) gemm_x6_kernel(int64_t M,
     mstep(a_s, 0);
     mstep(a_s, 1);
     if constexpr (NBUF == 2) {
-      if (more) {
-        x6_store<BM, true, NT>(ra.r, smem + (cur ^ 1) * STAGE);
-        x6_store<BN, true, NT>(rb.r, smem + (cur ^ 1) * STAGE + 3 * APL);
-      }
+      if (more) store(smem + (cur ^ 1) * STAGE);
       __syncthreads();
       cur ^= 1;
     } else {
       __syncthreads();
-      if (more) {
-        x6_store<BM, true, NT>(ra.r, smem);
-        x6_store<BN, true, NT>(rb.r, smem + 3 * APL);
-      }
+      if (more) store(smem);
       __syncthreads();
     }
   }
@@ -450,10 +514,34 @@ static int x6_nb128() {
   return v;
 }
 
+// GMR_X6_INPLACE = 0 (default): TN / NN split-bf16 calls copy their m- / n-contiguous operands k-contiguous
+// first; 1: B read in place (MnTile), A copied; 2: both read in place.  Opt-in: the in-place kernels ran the
+// denoiser gradient products 4-10 % slower than copy + k-contiguous kernel, epoch unchanged
+// (profiles/r05zt_x6_inplace_*.txt)
+int x6_inplace() {
+  static const int v = [] {
+    const char* e = getenv("GMR_X6_INPLACE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 int x6_launch(int bm, int bn, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
-              const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n, int64_t kps, float* ws) {
+              const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n, int64_t kps, float* ws,
+              bool akc, bool bkc) {
 #define GMR_X6(BM_, BN_, WGM_, WGN_, NBUF_, OCC_)                                                                \
   {                                                                                                                \
+    if (!akc || !bkc) {                                                                                            \
+      if (akc)                                                                                                     \
+        hipLaunchKernelGGL((gemm_x6_kernel<BM_, BN_, WGM_, WGN_, NBUF_, OCC_, 0, true, false>), grid,              \
+                           dim3(64 * WGM_ * WGN_), 0, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws); \
+      else if (!bkc)                                                                                               \
+        hipLaunchKernelGGL((gemm_x6_kernel<BM_, BN_, WGM_, WGN_, NBUF_, OCC_, 0, false, false>), grid,             \
+                           dim3(64 * WGM_ * WGN_), 0, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws); \
+      else                                                                                                         \
+        return -1;                                                                                                 \
+      return 0;                                                                                                    \
+    }                                                                                                              \
     if (NBUF_ == 2 && x6_pipe())                                                                                   \
       hipLaunchKernelGGL((gemm_x6_kernel<BM_, BN_, WGM_, WGN_, NBUF_, OCC_, NBUF_ - 1>), grid, dim3(64 * WGM_ * WGN_), \
                          0, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws);                           \
@@ -467,6 +555,7 @@ int x6_launch(int bm, int bn, dim3 grid, hipStream_t st, int64_t M, int64_t N, i
   // the others' MFMA steps (GMR_GEMM_X6_NB128 = 1 / 3: always two / three single-buffered blocks,
   // = 2: one double-buffered block per CU; for A/B runs)
   // 64^2 (4 waves of 32^2, LDS double-buffered, 48 KiB: three blocks per CU) for the small products
+  if (bm == 64 && bn == 64 && (!akc || !bkc)) return -1;  // 64^2 split tiles: NT calls only (make_plan)
   if (bm == 64 && bn == 64 && x6_ring()) {
     hipLaunchKernelGGL((gemm_x6_kernel<64, 64, 2, 2, 2, 3, 2>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C,
                        ldc, epi, tiles_n, kps, ws);

@@ -1,4 +1,6 @@
 """HIP kernels vs the CPU oracle / torch-fp32 references, through the C-ABI (GPU only)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -705,6 +707,54 @@ def test_gemm_x6_fp32_accuracy(K, tile, ta, tb):
         assert _lib_kind(ta, tb, 1000, 700, 7050, tile | X6) == 6
     if tile == 64 and (ta, tb) != (0, 1):
         assert _lib_kind(ta, tb, 1000, 700, 7050, tile | X6) == 32
+
+
+@pytest.mark.parametrize("tile", [128, 256128, 128256])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (1, 0)])
+def test_gemm_x6_inplace_operands_bit_exact(K, tile, ta, tb):
+    """TN / NN split-bf16 calls (default: their m- / n-contiguous operands copied k-contiguous; with
+    GMR_X6_INPLACE = 1 / 2 read in place by gemm_x6.hip's MnTile, test_gemm_x6_inplace_subprocess) equal, bit
+    for bit, the NT call on k-contiguous copies of the same operands (same plane images, same MFMA order), on
+    ragged edges (M, N not multiples of 4; padded and unpadded leading dimensions), a partial last k tile and
+    split-K slabs, with the posterior epilogue."""
+    rng = _rng(39)
+    for M, N, Kd, split, padded in ((517, 261, 1000, 1, True), (130, 1001, 2052, 4, False),
+                                    (1000, 64, 7052, 2, True)):
+        a = rng.standard_normal((M, Kd)).astype(np.float32)
+        b = rng.standard_normal((N, Kd)).astype(np.float32)
+        pad = lambda x: np.pad(x, ((0, 0), (0, (-x.shape[1]) % 4 if padded else 0)))  # noqa: E731  16-byte rows
+        A = _dev(pad(a.T))[:, :M] if ta else _dev(a)
+        B = _dev(pad(b.T))[:, :N]
+        bias = _dev(rng.standard_normal(N).astype(np.float32))
+        aux = _dev(rng.standard_normal((M, N)).astype(np.float32))
+        outs = []
+        for AA, BB, t_a, t_b in ((A, B, bool(ta), False), (_dev(a), _dev(b), False, True)):
+            C = aux.clone()
+            K.gemm(AA, BB, C, trans_a=t_a, trans_b=t_b, epi=K.EPI_POSTERIOR, bias=bias, aux=C, slope=0.5,
+                   beta=0.25, tile=tile | X6, split_k=split)
+            outs.append(C)
+        assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)), (M, N, Kd, split)
+        want = 0.5 * (torch.as_tensor(a, dtype=torch.float64) @ torch.as_tensor(b, dtype=torch.float64).t()
+                      + bias.double().cpu()) + 0.25 * aux.double().cpu()
+        torch.testing.assert_close(outs[0].double().cpu(), want, rtol=1e-4, atol=2e-3)  # fp32 sums, K <= 7,052
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_gemm_x6_inplace_subprocess(mode):
+    """GMR_X6_INPLACE (read once per process) = 1: B read in place, the m-contiguous A of TN calls copied;
+    = 2: both in place.  The bit-exact cases above (NN and TN), in a child process with that setting."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path[:0] = ['tests', 'generative-multimodal-recommendation_amd']\n"
+            "import test_kernels_gpu as t\nfrom gmr import kernels as K, _lib\n_lib.load()\n"
+            "for tile in (128, 256128, 128256):\n    for ta in (0, 1):\n"
+            "        t.test_gemm_x6_inplace_operands_bit_exact(K, tile, ta, 0)\n"
+            "print('OK')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GMR_X6_INPLACE=mode)
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-2000:] + r.stderr[-2000:]
 
 
 def _lib_kind(ta, tb, M, N, Kd, tile):
