@@ -1043,8 +1043,9 @@ __device__ __forceinline__ void c6_split8(const float (&v)[8], c6bf8 (&o)[3]) {
 // fp32 block (32 x 64, stride kClLd) -> the three row-major and the three transposed bf16 planes
 __device__ __forceinline__ void c6_convert(const float* sf, __bf16* stg) {
   const int t = threadIdx.x;
-  {  // row-major: thread -> row t / 8, columns 8 (t % 8) .. + 8
-    const int r = t >> 3, c = (t & 7) * 8;
+  {  // row-major: thread -> row t / 8, columns 8 c' .. + 8 with c' = t % 8 rotated by -1 in rows 4 i + 2, 4 i + 3
+     // (conflict-free 16-byte reads of s_f and writes of the planes; plain t % 8 cost 2-way on the reads)
+    const int r = t >> 3, c = (((t & 7) + ((r & 2) ? 7 : 0)) & 7) * 8;
     const float4 a = ld4(sf + r * kClLd + c), b = ld4(sf + r * kClLd + c + 4);
     const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     c6bf8 o[3];
@@ -1052,8 +1053,10 @@ __device__ __forceinline__ void c6_convert(const float* sf, __bf16* stg) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) *reinterpret_cast<c6bf8*>(stg + p * kC6PA + r * kC6A + c) = o[p];
   }
-  {  // transposed: thread -> column d = t / 4, slot group g = t % 4 (slots 8 g .. 8 g + 7)
-    const int d = t >> 2, g = t & 3;
+  {  // transposed: thread -> column d = t % 64, slot group g = t / 64 (slots 8 g .. 8 g + 7): a wave reads 64
+     // consecutive floats of one staged row per load and its 16-byte stores land on distinct banks (the
+     // (t / 4, t % 4) mapping cost 2-way conflicts on both, ~17 % of the pass's LDS cycles: profiles/r05zy_*)
+    const int d = t & 63, g = t >> 6;
     float v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = sf[(16 * (g >> 1) + 4 * (g & 1) + (q & 3) + 8 * (q >> 2)) * kClLd + d];

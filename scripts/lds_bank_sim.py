@@ -1,0 +1,75 @@
+import collections
+G128R=[list(range(0,4))+list(range(12,16))+list(range(20,28)), list(range(4,12))+list(range(16,20))+list(range(28,32)),
+       list(range(32,36))+list(range(44,48))+list(range(52,60)), list(range(36,44))+list(range(48,52))+list(range(60,64))]
+G32=[list(range(0,32)), list(range(32,64))]
+GW128=[list(range(8*i,8*i+8)) for i in range(8)]
+def cycles(addrs, groups, nd, mod):
+    tot=0; ideal=0
+    for g in groups:
+        banks=collections.defaultdict(set)
+        for l in g:
+            a=addrs[l]//4
+            for k in range(nd): banks[(a+k)%mod].add(a+k)
+        tot+=max(len(v) for v in banks.values()); ideal+=1
+    return tot, ideal
+kC6A,kC6B=72,40; kC6PA=32*kC6A; kC6PB=64*kC6B; kClLd=68
+res=collections.Counter(); ideal=collections.Counter()
+def add(name, addrs, groups, nd, mod):
+    c,i=cycles(addrs,groups,nd,mod); res[name]+=c; ideal[name]+=i
+for w in range(4):
+    lanes=range(64)
+    # sprod reads
+    for p in range(3):
+        for k in range(4):
+            add('sprod_b128r',[2*(p*kC6PA+(l%32)*kC6A+16*k+8*(l//32)) for l in lanes],G128R,4,64)
+    for t2 in range(2):
+        for p in range(3):
+            for base in (0,32):
+                add('Bt_b128r',[2*(3*kC6PA+p*kC6PB+(base+l%32)*kC6B+8*(2*t2+l//32)) for l in lanes],G128R,4,64)
+    # convert
+    ts=[64*w+l for l in lanes]
+    for half in (0,4):
+        add('conv_rowread_b128',[4*((t>>3)*kClLd+(t&7)*8+half) for t in ts],G128R,4,64)
+    for p in range(3):
+        add('conv_roww_b128',[2*(p*kC6PA+(t>>3)*kC6A+(t&7)*8) for t in ts],GW128,4,32)
+    for q in range(8):
+        add('conv_tread_b32',[4*((16*((t&3)>>1)+4*((t&3)&1)+(q&3)+8*(q>>2))*kClLd+(t>>2)) for t in ts],G32,1,32)
+    for p in range(3):
+        add('conv_tw_b128',[2*(3*kC6PA+p*kC6PB+(t>>2)*kC6B+8*(t&3)) for t in ts],GW128,4,32)
+    for q in range(2):
+        add('cl_store_b128',[4*(((t+256*q)>>4)*kClLd+((t+256*q)&15)*4) for t in ts],GW128,4,32)
+for k in res: print(f"{k:20s} cycles {res[k]:5d} ideal {ideal[k]:5d} extra {res[k]-ideal[k]}")
+print('total extra', sum(res.values())-sum(ideal.values()), 'total', sum(res.values()))
+print('--- candidates')
+def rowread_extra(fc):
+    ex=0
+    for w in range(4):
+        ts=[64*w+l for l in range(64)]
+        for half in (0,4):
+            c,i=cycles([4*((t>>3)*kClLd+fc(t)*8+half) for t in ts],G128R,4,64); ex+=c-i
+        for p in range(3):
+            c,i=cycles([2*(p*kC6PA+(t>>3)*kC6A+fc(t)*8) for t in ts],GW128,4,32); ex+=c-i
+    return ex
+for name,fc in [('base',lambda t:t&7),('rot',lambda t:((t&7)+(t>>3))&7),('xor',lambda t:(t&7)^((t>>3)&7)),
+                ('rot2',lambda t:((t&7)+2*(t>>3))&7),('xor1',lambda t:(t&7)^(((t>>3)&1)*4)),('rot4',lambda t:((t&7)+4*((t>>3)&1))&7),
+                ('xorh',lambda t:(t&7)^(((t>>4)&1)*4))]:
+    print(name, rowread_extra(fc))
+ex=0
+for w in range(4):
+    ts=[64*w+l for l in range(64)]
+    for q in range(8):
+        c,i=cycles([4*((16*((t>>6)>>1)+4*((t>>6)&1)+(q&3)+8*(q>>2))*kClLd+(t&63)) for t in ts],G32,1,32); ex+=c-i
+    for p in range(3):
+        c,i=cycles([2*(3*kC6PA+p*kC6PB+(t&63)*kC6B+8*(t>>6)) for t in ts],GW128,4,32); ex+=c-i
+print('transposed remap extra', ex)
+import itertools
+best=None
+for s in itertools.product(range(8), repeat=4):
+    for mode in ('add','xor'):
+        if mode=='add': fc=lambda t,s=s:((t&7)+s[(t>>3)&3])&7
+        else: fc=lambda t,s=s:(t&7)^s[(t>>3)&3]
+        e=rowread_extra(fc)
+        if best is None or e<best[0]: best=(e,s,mode)
+        if e==0: break
+    if best[0]==0: break
+print('best', best)
