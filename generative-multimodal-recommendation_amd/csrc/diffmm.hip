@@ -40,6 +40,22 @@ __device__ __forceinline__ void softmax2(const float* mw, float& w0, float& w1) 
   w1 = eb / s;
 }
 
+// normalize backward of one 64-column row held by 16 lanes (4 columns each): (g - y <y,g>) / nrm, the projection
+// term dropped when the norm was clamped, then the leaky-ReLU backward on sign(y) (slope 1: none); the
+// expression of normalize_bwd_kernel, so the fused callers give its bits
+__device__ __forceinline__ float4 nbwd_leaky(float4 g, float4 y, float nv, float slope) {
+  float dp = row16_sum(dot4(y, g));
+  if (nv <= 1e-12f) dp = 0.f;
+  float4 o = gmr::f4_scale(1.f / nv, sub4(g, gmr::f4_scale(dp, y)));
+  if (slope != 1.f) {
+    o.x *= y.x > 0.f ? 1.f : slope;
+    o.y *= y.y > 0.f ? 1.f : slope;
+    o.z *= y.z > 0.f ? 1.f : slope;
+    o.w *= y.w > 0.f ? 1.f : slope;
+  }
+  return o;
+}
+
 // E = G + H + lam * [Qi[:, :64] | Qt[:, :64]] (in place over G);  M = w0*E_img + w1*E_txt
 __global__ void combine_fwd_kernel(int64_t n, float* __restrict__ G, const float* __restrict__ H,
                                    const float* __restrict__ Qi, const float* __restrict__ Qt,
@@ -149,10 +165,10 @@ __global__ void normalize_bwd_kernel(int64_t n, int cols, const float* __restric
 
 // BPR with gathers: x = <a,p> - <a,n>;  loss_b = -log(1e-10 + sigmoid(x));
 // contributions (scaled by 1/B): slot b -> d a, slot B+b -> d p, slot 2B+b -> d n.
-__global__ void bpr_kernel(int B, int64_t U, const float* __restrict__ Emb, const int* __restrict__ users,
-                           const int* __restrict__ pos, const int* __restrict__ neg, float* __restrict__ loss,
-                           float* __restrict__ contrib, float inv_norm) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void bpr_rows(int gid, int B, int64_t U, const float* __restrict__ Emb,
+                                         const int* __restrict__ users, const int* __restrict__ pos,
+                                         const int* __restrict__ neg, float* __restrict__ loss,
+                                         float* __restrict__ contrib, float inv_norm) {
   const int b = gid >> 4;
   const bool ok = b < B;
   const int c = (gid & 15) * 4;
@@ -170,6 +186,12 @@ __global__ void bpr_kernel(int B, int64_t U, const float* __restrict__ Emb, cons
   st4(contrib + (int64_t)b * 64 + c, gmr::f4_scale(gx, sub4(p, q)));
   st4(contrib + ((int64_t)B + b) * 64 + c, gmr::f4_scale(gx, a));
   st4(contrib + (2 * (int64_t)B + b) * 64 + c, gmr::f4_scale(-gx, a));
+}
+
+__global__ void bpr_kernel(int B, int64_t U, const float* __restrict__ Emb, const int* __restrict__ users,
+                           const int* __restrict__ pos, const int* __restrict__ neg, float* __restrict__ loss,
+                           float* __restrict__ contrib, float inv_norm) {
+  bpr_rows(blockIdx.x * blockDim.x + threadIdx.x, B, U, Emb, users, pos, neg, loss, contrib, inv_norm);
 }
 
 // Row softmax of contrastive logits L (already divided by temp), in place:
@@ -267,13 +289,58 @@ __global__ void scatter_sorted_kernel(int n, int cols, const unsigned long long*
   st4(o, gmr::f4_add(ld4(o), s));
 }
 
+// The contrastive views' sparse gradient rows through the sorted plan (as scatter_sorted_kernel, cols = 128),
+// taken through the normalize backward of each 64-column view (y = CLN, nrm = [nrm_img | nrm_txt] per node) and
+// added to dK: dK[key] += nbwd([s_img | s_txt]).  The normalize backward is linear in its input, so adding
+// nbwd(sparse part) to the table pass's nbwd(dense part) (cl_table_reduce_nbwd_kernel) gives nbwd of the sum.
+__global__ void scatter_sorted_nbwd_kernel(int n, const unsigned long long* __restrict__ plan,
+                                           const float* __restrict__ contrib, int64_t ldc,
+                                           const float* __restrict__ y, const float* __restrict__ nrm, int64_t nn,
+                                           float* __restrict__ dK) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = gid >> 5;
+  if (i >= n) return;  // (whole 32-lane entries: the 16-lane row sums below see complete groups)
+  const int c = (int)(gid & 31) * 4;
+  const unsigned long long e = plan[i];
+  const unsigned key = (unsigned)(e >> 32);
+  if (key == 0xFFFFFFFFu) return;
+  if (i > 0 && (unsigned)(plan[i - 1] >> 32) == key) return;
+  float4 s = f4(0, 0, 0, 0);
+  for (int64_t j0 = i; j0 < n; j0 += 8) {
+    unsigned long long ej[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ej[q] = j0 + q < n ? plan[j0 + q] : ~0ull;
+    float4 x[8];
+    int m = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const bool in = (unsigned)(ej[q] >> 32) == key && m == q;
+      m += in ? 1 : 0;
+      x[q] = in ? ld4(contrib + (int64_t)(unsigned)(ej[q] & 0xFFFFFFFFull) * ldc + c) : f4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < m) s = gmr::f4_add(s, x[q]);
+    if (m < 8) break;
+  }
+  const int half = c >> 6;
+  const float4 g = nbwd_leaky(s, ld4(y + (int64_t)key * 128 + c), nrm[half * nn + key], 1.f);
+  float* o = dK + (int64_t)key * 128 + c;
+  st4(o, gmr::f4_add(ld4(o), g));
+}
+
 // final backward: dM = dEmb + T1 + ris * nbwd(M, dEmb);  dE = [w0 dM | w1 dM];
 // per-block partial sums of <E_img, dM>, <E_txt, dM> for the modal-weight gradient.
-__global__ void __launch_bounds__(256) final_bwd_kernel(int64_t n, const float* __restrict__ dEmb,
+// clear: dEmb is zeroed after it is read (this is its last reader in the step), so the next step's sorted
+// scatter adds onto zeros without a fill pass.
+// Ri / Rt (optional, lam): the left halves of the UI-graph backward sources, lam * dE_img / lam * dE_txt
+// (what cl_bwd_kernel would write there).
+__global__ void __launch_bounds__(256) final_bwd_kernel(int64_t n, float* __restrict__ dEmb,
                                                         const float* __restrict__ T1, const float* __restrict__ M,
                                                         const float* __restrict__ nrmM, float ris,
                                                         const float* __restrict__ E, const float* __restrict__ mw,
-                                                        float* __restrict__ dE, float* __restrict__ part) {
+                                                        float* __restrict__ dE, float* __restrict__ part, int clear,
+                                                        float lam, float* __restrict__ Ri, float* __restrict__ Rt) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t r = gid >> 4;
   const bool ok = r < n;
@@ -287,6 +354,7 @@ __global__ void __launch_bounds__(256) final_bwd_kernel(int64_t n, const float* 
     m = ld4(M + r * 64 + c);
     t = ld4(T1 + r * 64 + c);
     nv = nrmM[r];
+    if (clear) st4(dEmb + r * 64 + c, f4(0.f, 0.f, 0.f, 0.f));
   }
   float4 y = gmr::f4_scale(1.f / nv, m);
   float dp = row16_sum(dot4(y, g));
@@ -297,8 +365,13 @@ __global__ void __launch_bounds__(256) final_bwd_kernel(int64_t n, const float* 
     float4 ei = ld4(E + r * 128 + c), et = ld4(E + r * 128 + 64 + c);
     si = dot4(ei, dm);
     st = dot4(et, dm);
-    st4(dE + r * 128 + c, gmr::f4_scale(w0, dm));
-    st4(dE + r * 128 + 64 + c, gmr::f4_scale(w1, dm));
+    const float4 di = gmr::f4_scale(w0, dm), dt = gmr::f4_scale(w1, dm);
+    st4(dE + r * 128 + c, di);
+    st4(dE + r * 128 + 64 + c, dt);
+    if (Ri) {
+      st4(Ri + r * 128 + c, gmr::f4_scale(lam, di));
+      st4(Rt + r * 128 + c, gmr::f4_scale(lam, dt));
+    }
   }
   __shared__ float red[2][4];
   si = gmr::wave_sum(si);
@@ -315,8 +388,8 @@ __global__ void __launch_bounds__(256) final_bwd_kernel(int64_t n, const float* 
 }
 
 // modal-weight gradient: dw_i = sum of partials; dmw = w .* (dw - <w, dw>)  (softmax backward)
-__global__ void mw_grad_kernel(int nparts, const float* __restrict__ part, const float* __restrict__ mw,
-                               float* __restrict__ dmw, int accumulate) {
+__device__ __forceinline__ void mw_grad_block(int nparts, const float* __restrict__ part, const float* __restrict__ mw,
+                                              float* __restrict__ dmw, int accumulate) {
   __shared__ float red[2][4];
   float a = 0.f, b = 0.f;
   for (int i = threadIdx.x; i < nparts; i += 256) {
@@ -342,6 +415,11 @@ __global__ void mw_grad_kernel(int nparts, const float* __restrict__ part, const
   }
 }
 
+__global__ void mw_grad_kernel(int nparts, const float* __restrict__ part, const float* __restrict__ mw,
+                               float* __restrict__ dmw, int accumulate) {
+  mw_grad_block(nparts, part, mw, dmw, accumulate);
+}
+
 // dG = dE + [T2[:U]; 0]   (N x 128)
 __global__ void dg_kernel(int64_t n, int64_t U, const float* __restrict__ dE, const float* __restrict__ T2,
                           float* __restrict__ dG) {
@@ -356,18 +434,23 @@ __global__ void dg_kernel(int64_t n, int64_t U, const float* __restrict__ dE, co
 
 // contrastive backward through "K = C + adj@C":  dC = dK + T  (in place over T); also
 // build the iadj/tadj backward sources  Rsrc_img = [lam*dE_img | dC_img], Rsrc_txt likewise.
-__global__ void cl_bwd_kernel(int64_t n, const float* __restrict__ dK, const float* __restrict__ T,
+// clear: dK[:, :64] is zeroed after it is read (its last reader in the step; only the next step's sorted scatter
+// writes it, onto zeros); left: also write the lam * dE left halves (0: final_bwd_kernel wrote them)
+__global__ void cl_bwd_kernel(int64_t n, float* __restrict__ dK, const float* __restrict__ T,
                               const float* __restrict__ dE, float lam, float* __restrict__ Ri,
-                              float* __restrict__ Rt) {
+                              float* __restrict__ Rt, int clear, int left) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n * 16) return;
   const int64_t r = gid >> 4;
   const int c = (int)(gid & 15) * 4;
   float4 dci = gmr::f4_add(ld4(dK + r * 128 + c), ld4(T + r * 128 + c));
   float4 dct = gmr::f4_add(ld4(dK + r * 128 + 64 + c), ld4(T + r * 128 + 64 + c));
-  st4(Ri + r * 128 + c, gmr::f4_scale(lam, ld4(dE + r * 128 + c)));
+  if (clear) st4(dK + r * 128 + c, f4(0.f, 0.f, 0.f, 0.f));
+  if (left) {
+    st4(Ri + r * 128 + c, gmr::f4_scale(lam, ld4(dE + r * 128 + c)));
+    st4(Rt + r * 128 + c, gmr::f4_scale(lam, ld4(dE + r * 128 + 64 + c)));
+  }
   st4(Ri + r * 128 + 64 + c, dci);
-  st4(Rt + r * 128 + c, gmr::f4_scale(lam, ld4(dE + r * 128 + 64 + c)));
   st4(Rt + r * 128 + 64 + c, dct);
 }
 
@@ -376,26 +459,41 @@ __global__ void cl_bwd_kernel(int64_t n, const float* __restrict__ dK, const flo
 //   dE0[U:]  = T2i_img + T2i_txt + Ri[U:, :64] + Rt[U:, :64] + 2 reg iE
 //   dNF[:, :64] = T3[U:, :64] + Ri[U:, 64:] ;  dNF[:, 64:] = T3[U:, 64:] + Rt[U:, 64:]
 // T2 = adj@dE (its item rows feed diE), T3 = adj@dG.
+// NF / nrmF (optional, slope): dNF leaves through the modality projections' backward, normalize_bwd_kernel with
+// the leaky-ReLU slope on each 64-column half (the same expression: bit-identical to the separate launches)
 __global__ void assemble_kernel(int64_t n, int64_t U, const float* __restrict__ T2, const float* __restrict__ T3,
                                 const float* __restrict__ Ri, const float* __restrict__ Rt,
                                 const float* __restrict__ E0, float reg2, float* __restrict__ dE0,
-                                float* __restrict__ dNF) {
+                                float* __restrict__ dNF, const float* __restrict__ NF,
+                                const float* __restrict__ nrmF, float slope, float* __restrict__ dK_clear,
+                                int t3u_from_t2) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n * 16) return;
   const int64_t r = gid >> 4;
   const int c = (int)(gid & 15) * 4;
   const int64_t o = r * 128 + c;
+  if (dK_clear) st4(dK_clear + o, f4(0.f, 0.f, 0.f, 0.f));  // dK[:, :64]: zero for the next step's scatter
   float4 g;
   if (r < U) {
-    g = gmr::f4_add(ld4(T3 + o), ld4(T3 + o + 64));
+    // T3's user rows gather only item rows of dG = dE there: they ARE T2's user rows (adj is bipartite), so a
+    // caller that computed only T3's item rows passes t3u_from_t2
+    const float* T3u = t3u_from_t2 ? T2 : T3;
+    g = gmr::f4_add(ld4(T3u + o), ld4(T3u + o + 64));
     g = gmr::f4_add(g, gmr::f4_add(ld4(Ri + o), ld4(Ri + o + 64)));
     g = gmr::f4_add(g, gmr::f4_add(ld4(Rt + o), ld4(Rt + o + 64)));
   } else {
     g = gmr::f4_add(ld4(T2 + o), ld4(T2 + o + 64));
     g = gmr::f4_add(g, gmr::f4_add(ld4(Ri + o), ld4(Rt + o)));
     const int64_t ri = r - U;
-    st4(dNF + ri * 128 + c, gmr::f4_add(ld4(T3 + o), ld4(Ri + o + 64)));
-    st4(dNF + ri * 128 + 64 + c, gmr::f4_add(ld4(T3 + o + 64), ld4(Rt + o + 64)));
+    float4 gi = gmr::f4_add(ld4(T3 + o), ld4(Ri + o + 64));
+    float4 gt = gmr::f4_add(ld4(T3 + o + 64), ld4(Rt + o + 64));
+    if (NF) {  // (all 16 lanes of a row take this branch together: the row sums below are lane-complete)
+      const int64_t I = n - U;
+      gi = nbwd_leaky(gi, ld4(NF + ri * 128 + c), nrmF[ri], slope);
+      gt = nbwd_leaky(gt, ld4(NF + ri * 128 + 64 + c), nrmF[I + ri], slope);
+    }
+    st4(dNF + ri * 128 + c, gi);
+    st4(dNF + ri * 128 + 64 + c, gt);
   }
   g = gmr::f4_fma(reg2, ld4(E0 + r * 64 + c), g);
   st4(dE0 + r * 64 + c, g);
@@ -416,18 +514,37 @@ __global__ void sum_kernel(int64_t n, const float* __restrict__ x, float scale, 
 }
 
 // squared Frobenius norm: per-block fp64 partials (grid-stride) then one ordered sum
-__global__ void __launch_bounds__(256) sqnorm_part_kernel(int64_t n, const float* __restrict__ x,
-                                                          double* __restrict__ part) {
+__device__ __forceinline__ void sqnorm_block(int bid, int nblocks, int64_t n, const float* __restrict__ x,
+                                             double* __restrict__ part) {
   __shared__ double red[4];
   double s = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = (int64_t)bid * 256 + threadIdx.x; i < n; i += (int64_t)nblocks * 256) {
     const double v = x[i];
     s += v * v;
   }
   s = gmr::wave_sum_d(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) part[bid] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(256) sqnorm_part_kernel(int64_t n, const float* __restrict__ x,
+                                                          double* __restrict__ part) {
+  sqnorm_block(blockIdx.x, gridDim.x, n, x, part);
+}
+
+// the BPR rows (blocks [0, nb)) and the regulariser's squared-norm partials of E0 (blocks [nb, nb + g), the
+// partition of sqnorm_part_kernel with g blocks: the same partials) in one launch (DiffMM rec step)
+__global__ void __launch_bounds__(256) bpr_sqnorm_kernel(int B, int64_t U, const float* __restrict__ Emb,
+                                                         const int* __restrict__ users, const int* __restrict__ pos,
+                                                         const int* __restrict__ neg, float* __restrict__ loss,
+                                                         float* __restrict__ contrib, float inv_norm, int nb,
+                                                         int64_t n_sq, const float* __restrict__ x, int g,
+                                                         double* __restrict__ part) {
+  if ((int)blockIdx.x < nb)
+    bpr_rows(blockIdx.x * blockDim.x + threadIdx.x, B, U, Emb, users, pos, neg, loss, contrib, inv_norm);
+  else
+    sqnorm_block((int)blockIdx.x - nb, g, n_sq, x, part);
 }
 
 __global__ void sqnorm_fin_kernel(int nparts, const double* __restrict__ part, float scale, float* __restrict__ out,
@@ -581,8 +698,39 @@ extern "C" int gmr_dmm_final_bwd(int64_t n, const float* dEmb, const float* T1, 
                                  float ris, const float* E, const float* mw, float* dE, float* partials,
                                  void* stream) {
   GMR_ARG(dEmb && T1 && M && nrmM && E && mw && dE && partials && n > 0, "bad args");
+  hipLaunchKernelGGL(final_bwd_kernel, ROWS16(n), 0, (hipStream_t)stream, n, const_cast<float*>(dEmb), T1, M, nrmM,
+                     ris, E, mw, dE, partials, 0, 0.f, nullptr, nullptr);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dmm_final_bwd2(int64_t n, float* dEmb, const float* T1, const float* M, const float* nrmM, float ris,
+                                  const float* E, const float* mw, float* dE, float* partials, int32_t clear, float lam,
+                                  float* Ri, float* Rt, void* stream) {
+  GMR_ARG(dEmb && T1 && M && nrmM && E && mw && dE && partials && n > 0 && (!Ri) == (!Rt), "bad args");
   hipLaunchKernelGGL(final_bwd_kernel, ROWS16(n), 0, (hipStream_t)stream, n, dEmb, T1, M, nrmM, ris, E, mw, dE,
-                     partials);
+                     partials, (int)clear, lam, Ri, Rt);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dmm_bpr_sqnorm(int32_t B, int64_t U, const float* Emb, const int32_t* users, const int32_t* pos,
+                                  const int32_t* neg, float* loss, float* contrib, float inv_norm, int64_t n_sq,
+                                  const float* x, double* sq_parts, void* stream) {
+  GMR_ARG(Emb && users && pos && neg && loss && contrib && x && sq_parts && B > 0 && n_sq >= 0, "bad args");
+  const int nb = gmr::grid_for((int64_t)B * 16, 256);
+  const int g = gmr::grid_for(n_sq, 256 * 8, GMR_SQNORM_PARTS);  // gmr_sqnorm_nparts(n_sq)
+  hipLaunchKernelGGL(bpr_sqnorm_kernel, dim3((unsigned)(nb + g)), dim3(256), 0, (hipStream_t)stream, B, U, Emb, users,
+                     pos, neg, loss, contrib, inv_norm, nb, n_sq, x, g, sq_parts);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_scatter_sorted_nbwd_f32(int32_t n, const uint64_t* plan, const float* contrib, int64_t ldc,
+                                           const float* y, const float* nrm, int64_t n_nodes, float* dK, void* stream) {
+  GMR_ARG(plan && contrib && y && nrm && dK && n > 0 && ldc >= 128 && ldc % 4 == 0, "bad args");
+  hipLaunchKernelGGL(scatter_sorted_nbwd_kernel, dim3(gmr::grid_for((int64_t)n * 32, 256)), dim3(256), 0,
+                     (hipStream_t)stream, n, (const unsigned long long*)plan, contrib, ldc, y, nrm, n_nodes, dK);
   GMR_LAUNCHED();
   return GMR_OK;
 }
@@ -608,7 +756,17 @@ extern "C" int gmr_dmm_dg(int64_t n, int64_t U, const float* dE, const float* T2
 extern "C" int gmr_dmm_cl_bwd(int64_t n, const float* dK, const float* T, const float* dE, float lam, float* Ri,
                               float* Rt, void* stream) {
   GMR_ARG(dK && T && dE && Ri && Rt && n > 0, "bad args");
-  hipLaunchKernelGGL(cl_bwd_kernel, ROWS16(n), 0, (hipStream_t)stream, n, dK, T, dE, lam, Ri, Rt);
+  hipLaunchKernelGGL(cl_bwd_kernel, ROWS16(n), 0, (hipStream_t)stream, n, const_cast<float*>(dK), T, dE, lam, Ri, Rt,
+                     0, 1);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dmm_cl_bwd2(int64_t n, float* dK, const float* T, const float* dE, float lam, float* Ri, float* Rt,
+                               int32_t clear, int32_t left, void* stream) {
+  GMR_ARG(dK && T && Ri && Rt && n > 0 && (!left || dE), "bad args");
+  hipLaunchKernelGGL(cl_bwd_kernel, ROWS16(n), 0, (hipStream_t)stream, n, dK, T, dE, lam, Ri, Rt, (int)clear,
+                     (int)left);
   GMR_LAUNCHED();
   return GMR_OK;
 }
@@ -616,7 +774,18 @@ extern "C" int gmr_dmm_cl_bwd(int64_t n, const float* dK, const float* T, const 
 extern "C" int gmr_dmm_assemble(int64_t n, int64_t U, const float* T2, const float* T3, const float* Ri,
                                 const float* Rt, const float* E0, float reg2, float* dE0, float* dNF, void* stream) {
   GMR_ARG(T2 && T3 && Ri && Rt && E0 && dE0 && dNF && n > 0, "bad args");
-  hipLaunchKernelGGL(assemble_kernel, ROWS16(n), 0, (hipStream_t)stream, n, U, T2, T3, Ri, Rt, E0, reg2, dE0, dNF);
+  hipLaunchKernelGGL(assemble_kernel, ROWS16(n), 0, (hipStream_t)stream, n, U, T2, T3, Ri, Rt, E0, reg2, dE0, dNF,
+                     nullptr, nullptr, 1.f, nullptr, 0);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
+
+extern "C" int gmr_dmm_assemble2(int64_t n, int64_t U, const float* T2, const float* T3, const float* Ri,
+                                 const float* Rt, const float* E0, float reg2, float* dE0, float* dNF, const float* NF,
+                                 const float* nrmF, float slope, float* dK_clear, int32_t t3u_from_t2, void* stream) {
+  GMR_ARG(T2 && T3 && Ri && Rt && E0 && dE0 && dNF && NF && nrmF && n > 0 && U >= 0 && U <= n, "bad args");
+  hipLaunchKernelGGL(assemble_kernel, ROWS16(n), 0, (hipStream_t)stream, n, U, T2, T3, Ri, Rt, E0, reg2, dE0, dNF, NF,
+                     nrmF, slope, dK_clear, (int)t3u_from_t2);
   GMR_LAUNCHED();
   return GMR_OK;
 }
@@ -683,7 +852,47 @@ __global__ void __launch_bounds__(256) loss_total_kernel(int64_t B, const float*
     out[0] = v;
   }
 }
+
+// block 0: loss_total_kernel's sum (and acc[0] += loss when acc is given: the trainer's epoch loss, the bits of
+// its gmr_sum_f32 call); block 1: mw_grad_kernel (the modal-weight gradient from final_bwd's partials)
+__global__ void __launch_bounds__(256) loss_mw_kernel(int64_t B, const float* __restrict__ bpr, float inv_nr,
+                                                      const double* __restrict__ parts, int nparts, float reg,
+                                                      const float* __restrict__ cu, const float* __restrict__ ci,
+                                                      float ssl, float* __restrict__ out, float* __restrict__ acc,
+                                                      int nmw, const float* __restrict__ mwpart,
+                                                      const float* __restrict__ mw, float* __restrict__ dmw) {
+  if (blockIdx.x == 1) {
+    mw_grad_block(nmw, mwpart, mw, dmw, 0);
+    return;
+  }
+  __shared__ double red[4];
+  const double a = block_sum_d(B, bpr, red);
+  const double b = block_sum_d((int64_t)nparts, parts, red);
+  const double c = block_sum_d(B, cu, red);
+  const double d = block_sum_d(B, ci, red);
+  if (threadIdx.x == 0) {
+    float v = (float)(a * (double)inv_nr);
+    v = v + (float)(b * (double)reg);
+    v = v + (float)(c * (double)ssl);
+    v = v + (float)(d * (double)ssl);
+    out[0] = v;
+    if (acc) acc[0] = acc[0] + v;
+  }
+}
 }  // namespace
+
+extern "C" int gmr_dmm_loss_mw(int64_t B, const float* loss_bpr, float inv_nr, const double* parts, int64_t nparts,
+                               float reg_scale, const float* loss_cu, const float* loss_ci, float ssl_scale, float* out,
+                               float* acc, int64_t n_mw_parts, const float* mw_parts, const float* mw, float* dmw,
+                               void* stream) {
+  GMR_ARG(loss_bpr && parts && loss_cu && loss_ci && out && mw_parts && mw && dmw && B > 0 && nparts > 0 &&
+              nparts < (1 << 30) && n_mw_parts > 0 && n_mw_parts < (1 << 30),
+          "bad args");
+  hipLaunchKernelGGL(loss_mw_kernel, dim3(2), dim3(256), 0, (hipStream_t)stream, B, loss_bpr, inv_nr, parts,
+                     (int)nparts, reg_scale, loss_cu, loss_ci, ssl_scale, out, acc, (int)n_mw_parts, mw_parts, mw, dmw);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}
 
 extern "C" int gmr_dmm_loss_total(int64_t B, const float* loss_bpr, float inv_nr, const double* parts, int64_t nparts,
                                   float reg_scale, const float* loss_cu, const float* loss_ci, float ssl_scale,
@@ -1008,6 +1217,28 @@ __global__ void cl_table_reduce_kernel(int n, int nc, const float* __restrict__ 
   }
   for (; c < nc; ++c) s = gmr::f4_add(s, ld4(part_t + ((int64_t)c * n + j) * 64 + c4));
   st4(dT + j * ld + c4, s);
+}
+
+// the same sums, stored through the normalize backward of the table's view (y = normalised rows, ldy; nrm):
+// dT = nbwd(sum of the chunk partials) (DiffMM: the dense part of the text view's gradient, dK[:, 64:])
+__global__ void cl_table_reduce_nbwd_kernel(int n, int nc, const float* __restrict__ part_t, float* __restrict__ dT,
+                                            int64_t ld, const float* __restrict__ y, int64_t ldy,
+                                            const float* __restrict__ nrm) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (int64_t)n * 16) return;  // (whole 16-lane rows)
+  const int64_t j = g >> 4;
+  const int c4 = (int)(g & 15) * 4;
+  float4 s = ld4(part_t + j * 64 + c4);
+  int c = 1;
+  for (; c + 4 <= nc; c += 4) {
+    float4 t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = ld4(part_t + ((int64_t)(c + q) * n + j) * 64 + c4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s = gmr::f4_add(s, t[q]);
+  }
+  for (; c < nc; ++c) s = gmr::f4_add(s, ld4(part_t + ((int64_t)c * n + j) * 64 + c4));
+  st4(dT + j * ld + c4, nbwd_leaky(s, ld4(y + j * ldy + c4), nrm[j], 1.f));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1391,10 +1622,13 @@ extern "C" int64_t gmr_contrast_workspace_floats(int32_t B, int64_t n) {
   return kClCounters + (int64_t)p.nca * B * 65 + B + (int64_t)p.ncb * n * 64;
 }
 
-extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int64_t ldp, const float* T, int64_t ldt,
-                                      const float* CLN, const int32_t* nodes, int64_t node_off, float inv_temp,
-                                      float coef, float* loss, float* contrib, int64_t ld_contrib, float* dT,
-                                      int64_t ld_dt, float* workspace, int64_t workspace_floats, void* stream) {
+namespace {
+// y2 / ldy2 / nrm2 (optional): dT leaves through the normalize backward of the table's view (the reduce pass)
+int contrast_fused(const char* fn, int32_t B, int64_t n, const float* P, int64_t ldp, const float* T, int64_t ldt,
+                   const float* CLN, const int32_t* nodes, int64_t node_off, float inv_temp, float coef, float* loss,
+                   float* contrib, int64_t ld_contrib, float* dT, int64_t ld_dt, float* workspace,
+                   int64_t workspace_floats, const float* y2, int64_t ldy2, const float* nrm2, void* stream) {
+  (void)fn;
   GMR_ARG(P && T && CLN && nodes && loss && contrib && dT && workspace, "null pointer");
   GMR_ARG(B > 0 && n > 0 && n < (1ll << 31), "bad size");
   GMR_ARG(ldp >= 64 && ldt >= 64 && ld_contrib >= 128 && ld_dt >= 64 && ldp % 4 == 0 && ldt % 4 == 0 &&
@@ -1427,11 +1661,15 @@ extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int6
                        CLN, nodes, node_off, inv_temp, coef, loss, contrib, ld_contrib, r);
     GMR_LAUNCHED();
     // the table pass reduces its own partials (last block per tile) when its tiles fit the counters
-    const bool fix = cl_fixup() && gb.x <= (unsigned)kClCounters;
+    const bool fix = cl_fixup() && gb.x <= (unsigned)kClCounters && !y2;
     hipLaunchKernelGGL(table6, gb, dim3(256), 0, st, (int)n, B, T, ldt, P, ldp, r, inv_temp, p.chunk_b, part_t,
                        nullptr, fix ? counters : nullptr, dT, ld_dt);
     GMR_LAUNCHED();
-    if (!fix) {
+    if (!fix && y2) {
+      hipLaunchKernelGGL(cl_table_reduce_nbwd_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n,
+                         p.ncb, part_t, dT, ld_dt, y2, ldy2, nrm2);
+      GMR_LAUNCHED();
+    } else if (!fix) {
       hipLaunchKernelGGL(cl_table_reduce_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n, p.ncb,
                          part_t, dT, ld_dt);
       GMR_LAUNCHED();
@@ -1452,8 +1690,31 @@ extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int6
                     : (nf == 2 ? cl_table_kernel<false, 2> : cl_table_kernel<false, 1>);
   hipLaunchKernelGGL(table, gb, dim3(256), 0, st, B, (int)n, P, ldp, r, T, ldt, inv_temp, p.chunk_b, part_t);
   GMR_LAUNCHED();
-  hipLaunchKernelGGL(cl_table_reduce_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n, p.ncb, part_t,
-                     dT, ld_dt);
+  if (y2)
+    hipLaunchKernelGGL(cl_table_reduce_nbwd_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n, p.ncb,
+                       part_t, dT, ld_dt, y2, ldy2, nrm2);
+  else
+    hipLaunchKernelGGL(cl_table_reduce_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n, p.ncb,
+                       part_t, dT, ld_dt);
   GMR_LAUNCHED();
   return GMR_OK;
+}
+}  // namespace
+
+extern "C" int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int64_t ldp, const float* T, int64_t ldt,
+                                      const float* CLN, const int32_t* nodes, int64_t node_off, float inv_temp,
+                                      float coef, float* loss, float* contrib, int64_t ld_contrib, float* dT,
+                                      int64_t ld_dt, float* workspace, int64_t workspace_floats, void* stream) {
+  return contrast_fused(__func__, B, n, P, ldp, T, ldt, CLN, nodes, node_off, inv_temp, coef, loss, contrib, ld_contrib,
+                        dT, ld_dt, workspace, workspace_floats, nullptr, 0, nullptr, stream);
+}
+
+extern "C" int gmr_contrast_fused_nbwd_f32(int32_t B, int64_t n, const float* P, int64_t ldp, const float* T,
+                                           int64_t ldt, const float* CLN, const int32_t* nodes, int64_t node_off,
+                                           float inv_temp, float coef, float* loss, float* contrib, int64_t ld_contrib,
+                                           float* dT, int64_t ld_dt, const float* y, int64_t ldy, const float* nrm,
+                                           float* workspace, int64_t workspace_floats, void* stream) {
+  GMR_ARG(y && nrm && ldy >= 64 && ldy % 4 == 0 && (((uintptr_t)y) & 15) == 0, "bad normalised view");
+  return contrast_fused(__func__, B, n, P, ldp, T, ldt, CLN, nodes, node_off, inv_temp, coef, loss, contrib, ld_contrib,
+                        dT, ld_dt, workspace, workspace_floats, y, ldy, nrm, stream);
 }

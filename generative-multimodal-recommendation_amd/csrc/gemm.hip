@@ -388,6 +388,43 @@ __global__ void splitk_reduce_kernel(int64_t M, int64_t N, int splits, const flo
   C[m * ldc + n] = epi_apply(epi, s, m, n, C, ldc);
 }
 
+// split-K reduce of an N = 64 product through the modality projection's epilogue and the row normalisation that
+// follows it (GMR_EPI_LEAKY_NORM; models/diffmm.py:115-127 then F.normalize, :138-149): 16 lanes per row, each
+// element's slabs summed in slab order (splitk_reduce_kernel's bits), C = leaky(alpha s + bias), then
+// NF = C / max(|C|, 1e-12) and nrm as normalize_rows_kernel (diffmm.hip) computes them: the bits of the three
+// separate passes in one launch
+__global__ void splitk_reduce_leaky_norm_kernel(int64_t M, int splits, const float* __restrict__ ws,
+                                                float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ NF,
+                                                int64_t ldnf, float* __restrict__ nrm) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t m = gid >> 4;
+  if (m >= M) return;  // (whole 16-lane rows)
+  const int c = (int)(gid & 15) * 4;
+  const int64_t slab = M * 64, idx = m * 64 + c;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  int z = 0;
+  for (; z + 4 <= splits; z += 4) {
+    float4 a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = *reinterpret_cast<const float4*>(ws + (int64_t)(z + q) * slab + idx);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s = gmr::f4_add(s, a[q]);
+  }
+  for (; z < splits; ++z) s = gmr::f4_add(s, *reinterpret_cast<const float4*>(ws + (int64_t)z * slab + idx));
+  Epi e = epi;
+  e.kind = GMR_EPI_LEAKY;
+  const float v[4] = {epi_apply(e, s.x, m, c, C, ldc), epi_apply(e, s.y, m, c + 1, C, ldc),
+                      epi_apply(e, s.z, m, c + 2, C, ldc), epi_apply(e, s.w, m, c + 3, C, ldc)};
+  const float4 f = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(C + m * ldc + c) = f;
+  float ss = f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+#pragma unroll
+  for (int q = 8; q >= 1; q >>= 1) ss += __shfl_xor(ss, q);
+  const float nv = fmaxf(sqrtf(ss), 1e-12f);
+  *reinterpret_cast<float4*>(NF + m * ldnf + c) = gmr::f4_scale(1.f / nv, f);
+  if (c == 0) nrm[m] = nv;
+}
+
 // tile order inside each XCD's contiguous range: G > 1 walks G tile rows per column (the workgroups
 // resident on one XCD then share G A-panels and ~resident/G B-panels of each k slab in its L2 instead
 // of one A-panel and ~resident B-panels); 0/1 = row-major.  Default: G = 8 for products at least 32
@@ -423,13 +460,13 @@ int stages64() {
 }
 
 template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int MF>
-void launch_t(bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A,
+int launch_t(bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A,
               int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n,
               int64_t kps, float* ws, int* counters) {
   const dim3 blk(64 * WGM * WGN);
   if constexpr (MF == 6) {  // split-bf16 kernel (gemm_x6.hip): NT products, 16-byte aligned (make_plan)
-    x6_launch(BM, BN, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws, AKC, BKC);
-    return;
+    // -1: no split-bf16 kernel for this tile / operand layout (the caller reports GMR_ERR_ARG)
+    return x6_launch(BM, BN, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws, AKC, BKC);
   } else {
   if constexpr (MF == 32) {
     if (vec && glds) {
@@ -437,12 +474,12 @@ void launch_t(bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t
         if (stages64() == 3) {
           hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, AKC, BKC, 3>), grid, blk, 0, st, M, N, K, A, lda, B,
                              ldb, C, ldc, epi, tiles_n, kps, ws, counters);
-          return;
+          return 0;
         }
       }
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, AKC, BKC, 2>), grid, blk, 0, st, M, N, K, A, lda, B, ldb,
                          C, ldc, epi, tiles_n, kps, ws, counters);
-      return;
+      return 0;
     }
   }
   if (vec)
@@ -451,40 +488,41 @@ void launch_t(bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t
   else
     hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, AKC, BKC, false, MF>), grid, blk, 0, st, M, N, K, A, lda, B, ldb,
                        C, ldc, epi, tiles_n, kps, ws);
+  return 0;
   }
 }
 
 template <int BM, int BN, int WGM, int WGN, int MF>
-void launch_mf(int ta, int tb, bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K,
+int launch_mf(int ta, int tb, bool vec, bool glds, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K,
                const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi,
                int tiles_n, int64_t kps, float* ws, int* counters) {
   // AKC = A is k-contiguous (not transposed); BKC = B is k-contiguous (transposed)
   if (!ta && tb)
-    launch_t<BM, BN, WGM, WGN, true, true, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
+    return launch_t<BM, BN, WGM, WGN, true, true, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
                                                ws, counters);
   else if (!ta && !tb)
-    launch_t<BM, BN, WGM, WGN, true, false, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
+    return launch_t<BM, BN, WGM, WGN, true, false, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
                                                 ws, counters);
   else if (ta && !tb)
-    launch_t<BM, BN, WGM, WGN, false, false, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n,
+    return launch_t<BM, BN, WGM, WGN, false, false, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n,
                                                  kps, ws, counters);
   else
-    launch_t<BM, BN, WGM, WGN, false, true, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
+    return launch_t<BM, BN, WGM, WGN, false, true, MF>(vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
                                                 ws, counters);
 }
 
 template <int BM, int BN, int WGM, int WGN>
-void launch_tile(int mf, bool glds, int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N,
+int launch_tile(int mf, bool glds, int ta, int tb, bool vec, dim3 grid, hipStream_t st, int64_t M, int64_t N,
                  int64_t K, const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                  const Epi& epi, int tiles_n, int64_t kps, float* ws, int* counters) {
   if (mf == 6)
-    launch_mf<BM, BN, WGM, WGN, 6>(ta, tb, vec, false, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws,
+    return launch_mf<BM, BN, WGM, WGN, 6>(ta, tb, vec, false, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps, ws,
                                    counters);
   else if (mf == 16)
-    launch_mf<BM, BN, WGM, WGN, 16>(ta, tb, vec, false, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
+    return launch_mf<BM, BN, WGM, WGN, 16>(ta, tb, vec, false, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
                                     ws, counters);
   else
-    launch_mf<BM, BN, WGM, WGN, 32>(ta, tb, vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
+    return launch_mf<BM, BN, WGM, WGN, 32>(ta, tb, vec, glds, grid, st, M, N, K, A, lda, B, ldb, C, ldc, epi, tiles_n, kps,
                                     ws, counters);
 }
 
@@ -727,7 +765,11 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   GMR_ARG(A && B && C, "null operand");
   GMR_ARG(M > 0 && N > 0 && K > 0, "empty GEMM");
   GMR_ARG(lda >= (trans_a ? M : K) && ldb >= (trans_b ? K : N) && ldc >= N, "leading dimension too small");
-  GMR_ARG(epilogue >= GMR_EPI_NONE && epilogue <= GMR_EPI_DRELU, "bad epilogue");
+  GMR_ARG(epilogue >= GMR_EPI_NONE && epilogue <= GMR_EPI_LEAKY_NORM, "bad epilogue");
+  GMR_ARG(epilogue != GMR_EPI_LEAKY_NORM ||
+              (N == 64 && aux && rowvec1 && ld_aux >= 64 && ld_aux % 4 == 0 && ldc % 4 == 0 &&
+               (((uintptr_t)aux | (uintptr_t)C) & 15) == 0),
+          "GMR_EPI_LEAKY_NORM: N = 64, 16-byte aligned C and aux (the normalised rows), rowvec1 (the norms)");
   GMR_ARG(!(epilogue == GMR_EPI_POSTERIOR || epilogue == GMR_EPI_DTANH || epilogue == GMR_EPI_ROWSCALE_AUX ||
             epilogue == GMR_EPI_DRELU) || aux,
           "epilogue needs aux");
@@ -795,33 +837,40 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
     // [0, tiles) of the workspace, zero on entry and on exit).  Off by default: each slice's
     // agent-scope release writes back its XCD's L2, and that cost more than the reduce launch it
     // saves (projections 15 -> 48 us, 19445 x 1000 x 7050 2.30 -> 2.59 ms; profiles/r02u_fixup.txt)
-    if (pl.glds && vec && tm * tn <= GMR_GEMM_COUNTER_WORDS && inkernel_fixup())
+    if (pl.glds && vec && tm * tn <= GMR_GEMM_COUNTER_WORDS && inkernel_fixup() && epilogue != GMR_EPI_LEAKY_NORM)
       counters = reinterpret_cast<int*>(workspace);
   }
+  GMR_ARG(epilogue != GMR_EPI_LEAKY_NORM || splits > 1, "GMR_EPI_LEAKY_NORM needs a split-K plan");
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)(tm * tn), 1, (unsigned)splits);
   const int tnp = (int)tn | (tile_group(tn) << 20);
+  int lrc = 0;
   switch (tile) {
     case 256:
-      launch_tile<256, 256, 4, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
+      lrc = launch_tile<256, 256, 4, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
       break;
     case 256128:
-      launch_tile<256, 128, 4, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
+      lrc = launch_tile<256, 128, 4, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
       break;
     case 128256:
-      launch_tile<128, 256, 2, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
+      lrc = launch_tile<128, 256, 2, 4>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
       break;
     case 12864:
-      launch_tile<128, 64, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
+      lrc = launch_tile<128, 64, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
       break;
     case 128:
-      launch_tile<128, 128, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
+      lrc = launch_tile<128, 128, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
       break;
     default:
-      launch_tile<64, 64, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
+      lrc = launch_tile<64, 64, 2, 2>(pl.mf, pl.glds, trans_a, trans_b, vec, grid, st, M, N, K, A, lda, B, ldb, C, ldc, e, tnp, kps, ws, counters);
   }
+  GMR_ARG(lrc == 0, "no split-bf16 kernel for this tile and operand layout");
   GMR_LAUNCHED();
-  if (ws && !counters) {
+  if (ws && !counters && epilogue == GMR_EPI_LEAKY_NORM) {
+    hipLaunchKernelGGL(splitk_reduce_leaky_norm_kernel, dim3(gmr::grid_for(M * 16, 256)), dim3(256), 0, st, M, splits,
+                       ws, C, ldc, e, const_cast<float*>(aux), ld_aux, const_cast<float*>(rowvec1));
+    GMR_LAUNCHED();
+  } else if (ws && !counters) {
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gmr::grid_for(M * N, 256)), dim3(256), 0, st, M, N, splits, ws, C,
                        ldc, e);
     GMR_LAUNCHED();

@@ -364,7 +364,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const floatx16 (&acc)[BM / WGM
 // akc / bkc: A / B k-contiguous (A [M][K], B [N][K]) or m- / n-contiguous (A stored K x M, B stored K x N),
 // the latter read in place by the 128^2 / 256 x 128 / 128 x 256 tiles (NN: bkc = 0; TN: both 0); -1 = no kernel
 int x6_ring();  // gemm_x6.hip: the register-ring 64^2 split-bf16 kernel is on (GMR_X6_RING, default 1)
-int x6_inplace();  // gemm_x6.hip: TN / NN operands read in place, no transposed copies (GMR_X6_INPLACE, default 1)
+int x6_inplace();  // gemm_x6.hip: TN / NN operands read in place, no transposed copies (GMR_X6_INPLACE, default 0: opt-in, measured slower)
 int x6_launch(int bm, int bn, dim3 grid, hipStream_t st, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
               const float* B, int64_t ldb, float* C, int64_t ldc, const Epi& epi, int tiles_n, int64_t kps, float* ws,
               bool akc = true, bool bkc = true);

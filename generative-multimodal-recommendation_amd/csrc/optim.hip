@@ -83,3 +83,18 @@ extern "C" int gmr_zero(void* ptr, int64_t bytes, void* stream) {
   if (e != hipSuccess) return gmr::hip_status(__func__, e);
   return GMR_OK;
 }
+
+// Stream-timing probe for the ordering tests (gmr.kernels.Streams.PERTURB): one wave that sleeps about `us`
+// microseconds (s_sleep 127 = 8,128 clocks, ~3.4 us at 2.4 GHz) and touches no memory, so whatever is queued
+// behind it on `stream` starts that much later while the other streams run on.
+__global__ void delay_kernel(int iters) {
+  for (int i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
+extern "C" int gmr_delay(int32_t us, void* stream) {
+  GMR_ARG(us >= 0 && us <= 1000000, "us must be in [0, 1e6]");
+  if (us == 0) return GMR_OK;
+  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (us + 2) / 3);
+  GMR_LAUNCHED();
+  return GMR_OK;
+}

@@ -72,6 +72,8 @@ struct SideSrc {
 struct SideDst {
   float* y[4];
   int64_t ld[4];
+  const float* z[4];  // the beta term's source (Y = alpha A X + beta Z; z = y for the in-place form)
+  int64_t ldz[4];
 };
 
 __device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
@@ -106,11 +108,15 @@ __device__ __forceinline__ int grp_bcast(int x, int j) {  // j is a constant aft
 }
 
 // NS = 32-column slices of the product (d = 32 NS), EB = entries in flight per lane group.  The body of one
-// product; spmm_side_kernel runs one, spmm_side_jobs_kernel up to four independent ones (blockIdx.y)
-template <int EB, int NS>
+// product; spmm_side_kernel runs one, spmm_side_jobs_kernel up to four independent ones (blockIdx.y).
+// ONE: only the rows of side `only` are computed (the other side's rows are left as they are), and all 8 XCDs
+// work on it: NS slice groups of 8 / NS XCDs (the DiffMM backward's second GCN hop, whose user rows equal the
+// first hop's, models/diffmm.py:141-153)
+template <int EB, int NS, bool ONE = false>
 __device__ __forceinline__ void side_body(const int* __restrict__ plan, const SideSrc& src, float alpha, float beta,
-                                          const SideDst& dst, float* __restrict__ scratch, int wpx, int nt) {
-  constexpr int G = 2 * NS;                    // (side, slice) groups
+                                          const SideDst& dst, float* __restrict__ scratch, int wpx, int nt,
+                                          int only = 0) {
+  constexpr int G = ONE ? NS : 2 * NS;         // (side, slice) groups
   constexpr int PHASES = G > 8 ? G / 8 : 1;    // groups per XCD, one after the other
   constexpr int P = G >= 8 ? 1 : 8 / G;        // XCDs per group
   constexpr int EPL = EB / 8;                  // packed entries per lane per round
@@ -133,7 +139,7 @@ __device__ __forceinline__ void side_body(const int* __restrict__ plan, const Si
   for (int ph = 0; ph < PHASES; ++ph) {
     const int g = G >= 8 ? xcd + 8 * ph : xcd % G;
     const int part_i = G >= 8 ? 0 : xcd / G;
-    const int side = g / NS, slice = g % NS;
+    const int side = ONE ? only : g / NS, slice = g % NS;
     const int c0 = slice * 32 + sub * 4;       // this lane's 4 columns
     const int blk = c0 >> 6, cin = c0 & 63;
     const float* __restrict__ lo = src.lo[blk] + cin;
@@ -141,10 +147,12 @@ __device__ __forceinline__ void side_body(const int* __restrict__ plan, const Si
     const int64_t ldl = src.ld_lo[blk], ldh = src.ld_hi[blk];
     float* __restrict__ yc = dst.y[blk] + cin;
     const int64_t ldy = dst.ld[blk];
+    const float* __restrict__ zc = dst.z[blk] + cin;
+    const int64_t ldz = dst.ldz[blk];
     auto store = [&](int row, float4 acc) {
       float* yp = yc + (int64_t)row * ldy;
       float4 o = gmr::f4_scale(alpha, acc);
-      if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
+      if (beta != 0.f) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(zc + (int64_t)row * ldz), o);
       if (nt) {
         f32x4 ov = {o.x, o.y, o.z, o.w};
         __builtin_nontemporal_store(ov, reinterpret_cast<f32x4*>(yp));
@@ -322,7 +330,7 @@ __device__ __forceinline__ void side_body(const int* __restrict__ plan, const Si
         auto store_row = [&](int row, float4 acc) {
           float* yp = yc + (int64_t)row * ldy;
           float4 o = gmr::f4_scale(alpha, acc);
-          if constexpr (BETA) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(yp), o);
+          if constexpr (BETA) o = gmr::f4_fma(beta, *reinterpret_cast<const float4*>(zc + (int64_t)row * ldz), o);
           if (nt) {
             f32x4 ov = {o.x, o.y, o.z, o.w};
             __builtin_nontemporal_store(ov, reinterpret_cast<f32x4*>(yp));
@@ -432,11 +440,12 @@ __device__ __forceinline__ void side_body(const int* __restrict__ plan, const Si
   }
 }
 
-template <int EB, int NS>
+template <int EB, int NS, bool ONE = false>
 __global__ void __launch_bounds__(kSideThreads) spmm_side_kernel(const int* __restrict__ plan, SideSrc src,
                                                                   float alpha, float beta, SideDst dst,
-                                                                  float* __restrict__ scratch, int wpx, int nt) {
-  side_body<EB, NS>(plan, src, alpha, beta, dst, scratch, wpx, nt);
+                                                                  float* __restrict__ scratch, int wpx, int nt,
+                                                                  int only) {
+  side_body<EB, NS, ONE>(plan, src, alpha, beta, dst, scratch, wpx, nt, only);
 }
 
 // Multi-job launch (round 5, gmr_spmm_side_jobs_f32): independent side-split products of the same width in one
@@ -609,13 +618,22 @@ int side_nt() {  // non-temporal Y stores (GMR_SPMM_NT semantics: 0 = plain)
 
 template <int NS>
 void side_launch(int eb, const int* plan, const SideSrc& src, float alpha, float beta, const SideDst& dst,
-                 float* scratch, int wpx, int nt, hipStream_t st) {
+                 float* scratch, int wpx, int nt, hipStream_t st, int only = -1) {
+  if (only >= 0) {  // one side, on all eight XCDs
+    if (eb == 8)
+      hipLaunchKernelGGL((spmm_side_kernel<8, NS, true>), dim3(8 * wpx), dim3(kSideThreads), 0, st, plan, src, alpha,
+                         beta, dst, scratch, wpx, nt, only);
+    else
+      hipLaunchKernelGGL((spmm_side_kernel<16, NS, true>), dim3(8 * wpx), dim3(kSideThreads), 0, st, plan, src, alpha,
+                         beta, dst, scratch, wpx, nt, only);
+    return;
+  }
   if (eb == 8)
     hipLaunchKernelGGL((spmm_side_kernel<8, NS>), dim3(8 * wpx), dim3(kSideThreads), 0, st, plan, src, alpha, beta, dst,
-                       scratch, wpx, nt);
+                       scratch, wpx, nt, 0);
   else
     hipLaunchKernelGGL((spmm_side_kernel<16, NS>), dim3(8 * wpx), dim3(kSideThreads), 0, st, plan, src, alpha, beta,
-                       dst, scratch, wpx, nt);
+                       dst, scratch, wpx, nt, 0);
 }
 
 template <int NS>
@@ -639,6 +657,8 @@ int side_fill(int n_blocks, const float* const* x_lo, const int64_t* ld_lo, cons
     s.ld_hi[b] = on ? ld_hi[b] : 0;
     d.y[b] = on ? y[b] : nullptr;
     d.ld[b] = on ? ld_y[b] : 0;
+    d.z[b] = d.y[b];
+    d.ldz[b] = d.ld[b];
     if (on) {
       GMR_ARG(s.lo[b] && s.hi[b] && d.y[b], "null block pointer");
       GMR_ARG(((uintptr_t)s.lo[b] | (uintptr_t)s.hi[b] | (uintptr_t)d.y[b]) % 16 == 0, "blocks must be 16-byte aligned");
@@ -813,39 +833,52 @@ extern "C" int gmr_spmm_side_pack_classes(const int32_t* rowptr, const int32_t* 
   return GMR_OK;
 }
 
-extern "C" int gmr_spmm_side_f32(const int32_t* plan, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
-                                 const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
-                                 float* const* y, const int64_t* ld_y, float* scratch, int32_t wpx, void* stream) {
+namespace {
+int side_call(const int32_t* plan, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
+              const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
+              const float* const* z, const int64_t* ld_z, float* const* y, const int64_t* ld_y, int32_t only,
+              float* scratch, int32_t wpx, void* stream) {
   GMR_ARG(plan && scratch && x_lo && ld_lo && x_hi && ld_hi && y && ld_y, "null argument");
   GMR_ARG(wpx >= 0 && wpx <= 1024, "wpx in [0, 1024] (0 = default)");
   GMR_ARG(n_blocks == 1 || n_blocks == 2 || n_blocks == 4, "1, 2 or 4 blocks of 64 columns");
+  GMR_ARG(only >= -1 && only <= 1, "only_side must be -1 (both), 0 (rows < split) or 1 (rows >= split)");
   SideSrc s;
   SideDst d;
-  for (int b = 0; b < 4; ++b) {
-    const bool on = b < n_blocks;
-    s.lo[b] = on ? x_lo[b] : nullptr;
-    s.hi[b] = on ? x_hi[b] : nullptr;
-    s.ld_lo[b] = on ? ld_lo[b] : 0;
-    s.ld_hi[b] = on ? ld_hi[b] : 0;
-    d.y[b] = on ? y[b] : nullptr;
-    d.ld[b] = on ? ld_y[b] : 0;
-    if (on) {
-      GMR_ARG(s.lo[b] && s.hi[b] && d.y[b], "null block pointer");
-      GMR_ARG(((uintptr_t)s.lo[b] | (uintptr_t)s.hi[b] | (uintptr_t)d.y[b]) % 16 == 0, "blocks must be 16-byte aligned");
-      GMR_ARG(s.ld_lo[b] % 4 == 0 && s.ld_hi[b] % 4 == 0 && d.ld[b] % 4 == 0 && d.ld[b] >= 64,
-              "leading dimensions must be multiples of 4");
+  if (side_fill(n_blocks, x_lo, ld_lo, x_hi, ld_hi, split, y, ld_y, s, d) != GMR_OK) return GMR_ERR_ARG;
+  if (z) {
+    GMR_ARG(ld_z, "null ld_z");
+    for (int b = 0; b < n_blocks; ++b) {
+      GMR_ARG(z[b] && ((uintptr_t)z[b]) % 16 == 0 && ld_z[b] % 4 == 0 && ld_z[b] >= 64,
+              "z blocks: 16-byte aligned, leading dimension a multiple of 4 and >= 64");
+      d.z[b] = z[b];
+      d.ldz[b] = ld_z[b];
     }
   }
-  s.split = split;
   const hipStream_t st = (hipStream_t)stream;
   const int eb = side_eb(), nt = side_nt();
   if (wpx == 0 || getenv("GMR_SPMM_SIDE_WPX") || g_side_tuned) wpx = side_wpx();
   if (n_blocks == 1)
-    side_launch<2>(eb, plan, s, alpha, beta, d, scratch, wpx, nt, st);
+    side_launch<2>(eb, plan, s, alpha, beta, d, scratch, wpx, nt, st, only);
   else if (n_blocks == 2)
-    side_launch<4>(eb, plan, s, alpha, beta, d, scratch, wpx, nt, st);
+    side_launch<4>(eb, plan, s, alpha, beta, d, scratch, wpx, nt, st, only);
   else
-    side_launch<8>(eb, plan, s, alpha, beta, d, scratch, wpx, nt, st);
+    side_launch<8>(eb, plan, s, alpha, beta, d, scratch, wpx, nt, st, only);
   GMR_LAUNCHED();
   return GMR_OK;
+}
+}  // namespace
+
+extern "C" int gmr_spmm_side_f32(const int32_t* plan, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
+                                 const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
+                                 float* const* y, const int64_t* ld_y, float* scratch, int32_t wpx, void* stream) {
+  return side_call(plan, n_blocks, x_lo, ld_lo, x_hi, ld_hi, split, alpha, beta, nullptr, nullptr, y, ld_y, -1,
+                   scratch, wpx, stream);
+}
+
+extern "C" int gmr_spmm_side2_f32(const int32_t* plan, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
+                                  const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
+                                  const float* const* z, const int64_t* ld_z, float* const* y, const int64_t* ld_y,
+                                  int32_t only_side, float* scratch, int32_t wpx, void* stream) {
+  return side_call(plan, n_blocks, x_lo, ld_lo, x_hi, ld_hi, split, alpha, beta, z, ld_z, y, ld_y, only_side, scratch,
+                   wpx, stream);
 }

@@ -43,6 +43,7 @@ SIGNATURES = {
     "gmr_event_create": (I32, [P]),
     "gmr_event_destroy": (I32, [P]),
     "gmr_stream_fork": (I32, [P, P, P]),
+    "gmr_delay": (I32, [I32, P]),
     "gmr_score_f16": (I32, [I64, I64, I64, P, I64, P, I64, P, I64, P]),
     "gmr_spmm_multi_f32": (I32, [P, P, I64, I64, P, I32, I32, P, P, P, P, I64, F32, F32, P, P, P, I32, P]),
     "gmr_spmm_jobs_f32": (I32, [I32, P, P]),
@@ -55,6 +56,7 @@ SIGNATURES = {
     "gmr_spmm_side_pack_classes": (I32, [P, P, P, P, P, P]),
     "gmr_spmm_side_tune": (I32, [I32, I32]),
     "gmr_spmm_side_f32": (I32, [P, I32, P, P, P, P, I64, F32, F32, P, P, P, I32, P]),
+    "gmr_spmm_side2_f32": (I32, [P, I32, P, P, P, P, I64, F32, F32, P, P, P, P, I32, P, I32, P]),
     "gmr_graph_exec_create": (I32, [P, I32, P, P]),
     "gmr_graph_exec_info": (I32, [P, P, P, P, P]),
     "gmr_graph_exec_launch": (I32, [P, P]),
@@ -78,6 +80,14 @@ SIGNATURES = {
     "gmr_dmm_dg": (I32, [I64, I64, P, P, P, P]),
     "gmr_dmm_cl_bwd": (I32, [I64, P, P, P, F32, P, P, P]),
     "gmr_dmm_assemble": (I32, [I64, I64, P, P, P, P, P, F32, P, P, P]),
+    "gmr_dmm_final_bwd2": (I32, [I64, P, P, P, P, F32, P, P, P, P, I32, F32, P, P, P]),
+    "gmr_dmm_cl_bwd2": (I32, [I64, P, P, P, F32, P, P, I32, I32, P]),
+    "gmr_dmm_assemble2": (I32, [I64, I64, P, P, P, P, P, F32, P, P, P, P, F32, P, I32, P]),
+    "gmr_dmm_bpr_sqnorm": (I32, [I32, I64, P, P, P, P, P, P, F32, I64, P, P, P]),
+    "gmr_dmm_loss_mw": (I32, [I64, P, F32, P, I64, F32, P, P, F32, P, P, I64, P, P, P, P]),
+    "gmr_scatter_sorted_nbwd_f32": (I32, [I32, P, P, I64, P, P, I64, P, P]),
+    "gmr_contrast_fused_nbwd_f32": (I32, [I32, I64, P, I64, P, I64, P, P, I64, F32, F32, P, P, I64, P, I64, P, I64, P, P,
+                                          I64, P]),
     "gmr_normalize_rows_f32": (I32, [I64, I32, P, I64, P, I64, P, P]),
     "gmr_normalize_rows_bwd_f32": (I32, [I64, I32, P, I64, P, P, I64, P, I64, F32, I32, P]),
     "gmr_bpr_fwd_bwd": (I32, [I32, I64, P, P, P, P, P, P, F32, P]),
@@ -218,6 +228,8 @@ def check(rc, name="gmr"):
 
 
 _fns = {}
+# a gmr.tape.Tape while one records a step (every call below is also noted on it), else None
+recorder = None
 
 
 def call(name, *args):
@@ -231,4 +243,8 @@ def call(name, *args):
     if len(args) != n:
         raise TypeError(f"{name} takes {n} arguments, got {len(args)}")
     rc = fn(*args)
-    return rc if rc == 0 else check(rc, name)
+    if rc != 0:
+        return check(rc, name)
+    if recorder is not None:
+        recorder.note(name, fn, args)
+    return rc

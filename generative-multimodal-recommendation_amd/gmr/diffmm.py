@@ -87,6 +87,11 @@ class _RecLoss(torch.autograd.Function):
 
 class DiffMM(GeneralRecommender):
     REC_PARAMS = ("uEmbeds", "iEmbeds", "image_trans", "text_trans", "modal_weight")
+    # rec_step is a fixed sequence of C-ABI calls for a given batch shape and graph set (no per-step draws or
+    # scalars), so the trainer may replay it from a host tape (gmr/tape.py); tape_replayed() keeps the Python-side
+    # counters of a replayed step
+    tape_safe = True
+    rec_step_takes_acc = True  # rec_step(..., acc=) adds the loss to the trainer's epoch sum itself
 
     def __init__(self, config, dataloader):
         super().__init__(config, dataloader)
@@ -185,11 +190,14 @@ class DiffMM(GeneralRecommender):
             return self._w
         N, I, U, dev = self.N, self.n_items, self.n_users, self.device
         f = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731
+        z = lambda *s: torch.zeros(s, dtype=torch.float32, device=dev)  # noqa: E731
         w = {"B": B,
              "F": f(I, 128), "NF": f(I, 128), "nrmF": f(2, I),
              "G": f(N, 128), "H": f(N, 128), "Qi": f(N, 128), "Qt": f(N, 128), "K2": f(N, 128),
              "M": f(N, 64), "L": f(N, 64), "Emb": f(N, 64), "nrmM": f(N), "CLN": f(N, 128), "nrmCL": f(2, N),
-             "dEmb": f(N, 64), "dCLN": f(N, 128), "T1": f(N, 64), "dE": f(N, 128), "T2": f(N, 128),
+             # zero on entry to every step: dEmb (final_bwd clears it after reading) and dK = dCLN[:, :64]
+             # (cl_bwd clears it after reading); the sorted scatters of the next step add onto those zeros
+             "dEmb": z(N, 64), "dCLN": z(N, 128), "T1": f(N, 64), "dE": f(N, 128), "T2": f(N, 128),
              "DG": f(N, 128), "T3": f(N, 128), "Tcl": f(N, 128), "Ri": f(N, 128), "Rt": f(N, 128),
              "OutI": f(N, 128), "OutT": f(N, 128), "dNF": f(I, 128),
              "partials": f(int(_lib.load().gmr_dmm_final_bwd_partials(N))),
@@ -201,17 +209,31 @@ class DiffMM(GeneralRecommender):
         self._w = w
         return w
 
+    def reset_step_buffers(self):
+        """Restore the work-buffer state a rec step expects on entry (tests that overwrite the buffers call it):
+        dEmb and dCLN[:, :64] zero (each step's last reader of them clears them for the next step)."""
+        if self._w is not None:
+            self._w["dEmb"].zero_()
+            self._w["dCLN"].zero_()
+
     # ================================================================= forward_MM
     def _project(self, w):
-        """F = leaky_relu([v_feat @ image_trans | t_feat @ text_trans], 0.2); NF = row-normalised F."""
+        """F = leaky_relu([v_feat @ image_trans | t_feat @ text_trans], 0.2); NF = row-normalised F (the split-K
+        reduce of each projection writes F, NF and the norms: GMR_EPI_LEAKY_NORM)."""
         s = self.rec_slab
         st = self._streams
         with st.on(1):  # the text projection runs beside the image one
-            K.gemm(self.t_feat, s.view("text_trans"), w["F"][:, 64:], epi=K.EPI_LEAKY, slope=0.2)
-            K.normalize_rows(w["F"][:, 64:], w["NF"][:, 64:], w["nrmF"][1])
-        K.gemm(self.v_feat, s.view("image_trans"), w["F"][:, :64], epi=K.EPI_LEAKY, slope=0.2)
-        K.normalize_rows(w["F"][:, :64], w["NF"][:, :64], w["nrmF"][0])
+            self._project1(self.t_feat, s.view("text_trans"), w, 1)
+        self._project1(self.v_feat, s.view("image_trans"), w, 0)
         st.join(1)
+
+    def _project1(self, X, W, w, j):
+        F, NF = w["F"][:, 64 * j:64 * (j + 1)], w["NF"][:, 64 * j:64 * (j + 1)]
+        if int(_lib.load().gmr_gemm_workspace_floats(0, 0, X.shape[0], 64, X.shape[1], K.GEMM_TILE_FLAGS, 0)) > 0:
+            K.gemm(X, W, F, epi=K.EPI_LEAKY_NORM, slope=0.2, aux=NF, rv1=w["nrmF"][j])
+        else:  # (a product too short to split K: the epilogue and the normalisation as two passes)
+            K.gemm(X, W, F, epi=K.EPI_LEAKY, slope=0.2)
+            K.normalize_rows(F, NF, w["nrmF"][j])
 
     def _forward_mm(self, w, with_cl, on_cl=None):
         U = self.n_users
@@ -263,21 +285,26 @@ class DiffMM(GeneralRecommender):
     def _contrast(self, w, nodes, off, n_table, slot0, loss_out, B, norm, slot="u"):
         """InfoNCE of CLN[:, :64] (view 1) vs CLN[:, 64:] (view 2) for the gathered nodes
         (contrastLoss, diffmm.py:251-258): one fused MFMA pass over the table for the loss rows and
-        dP, one for the dense table gradient (gmr_contrast_fused_f32) - no B x n logits in HBM."""
+        dP, one for the dense table gradient, which leaves through the normalize backward of view 2 into
+        dK[:, 64:] (gmr_contrast_fused_nbwd_f32) - no B x n logits in HBM."""
         CLN, P1 = w["CLN"], w["P1_" + slot][:B]
         K.gather_rows(CLN[:, :64], nodes, P1, off=off)
         contrib = w["contrib_cl"][slot0:slot0 + B]
         ws = K.contrast_workspace(B, n_table, self.device, "cl_" + slot)
-        K.contrast_fused(P1, CLN[off:off + n_table, 64:], CLN, nodes, off, 1.0 / self.temp, self.ssl_reg / norm,
-                         loss_out, contrib, w["dCLN"][off:off + n_table, 64:], ws)
+        T, dT = CLN[off:off + n_table, 64:], w["dCLN"][off:off + n_table, 64:]
+        with K._Probe("infonce", (B, n_table)):
+            _lib.call("gmr_contrast_fused_nbwd_f32", B, n_table, ptr(P1), 64, ptr(T), 128, ptr(CLN), ptr(nodes), off,
+                      1.0 / self.temp, self.ssl_reg / norm, ptr(loss_out), ptr(contrib), 128, ptr(dT), 128, ptr(T), 128,
+                      ptr(w["nrmCL"][1][off:off + n_table]), ptr(ws), ws.numel(), stream())
 
-    def rec_step(self, users, pos, neg, plan_bpr=None, plan_cl=None, norm_rows=None, reg_share=1.0):
+    def rec_step(self, users, pos, neg, plan_bpr=None, plan_cl=None, norm_rows=None, reg_share=1.0, acc=None):
         """Loss of calculate_loss (cl_method 0) and all rec-parameter gradients (into rec_slab.grad).
 
         users/pos/neg: int32 device tensors of one batch; plan_*: sorted scatter plans (built here
         when not supplied by the loader).  Data parallel: norm_rows = rows of the global batch (the
         batch means use it) and reg_share = 1 / ranks (the regulariser is counted once after the
-        gradient all-reduce); the defaults give the single-device loss."""
+        gradient all-reduce); the defaults give the single-device loss.  acc: a device float the step's
+        loss is added to (the trainer's epoch sum), in the loss reduction's own launch."""
         if self.image_UI_matrix is None or self.text_UI_matrix is None:
             raise RuntimeError("the UI graphs are built by DiffMMTrainer before the BPR phase")
         if self.cl_method != 0:
@@ -293,140 +320,141 @@ class DiffMM(GeneralRecommender):
         st = self._streams
 
         def contrast():
-            # the two InfoNCE terms run side by side, beside the GCN layer of forward_MM; each zeroes its own
-            # rows of dCLN first ([:, 64:] is then written by its table pass, [:, :64] by the scatters after the
-            # join), off the main stream
+            # the two InfoNCE terms run side by side, beside the GCN layer of forward_MM; each table pass writes
+            # its rows of dK[:, 64:] (dK[:, :64] is zero on entry and takes the sorted scatter's rows)
             with st.on(0):
-                K.zero_(w["dCLN"][:U])
                 self._contrast(w, users, 0, U, 0, w["loss_cu"], B, nr, slot="u")
             with st.on(1):
-                K.zero_(w["dCLN"][U:])
                 self._contrast(w, pos, U, I, B, w["loss_ci"], B, nr, slot="i")
 
         self._forward_mm(w, with_cl=True, on_cl=contrast)
-        # --- losses and their sparse gradient contributions
-        _lib.call("gmr_bpr_fwd_bwd", B, U, ptr(w["Emb"]), ptr(users), ptr(pos), ptr(neg), ptr(w["loss_bpr"]),
-                  ptr(w["contrib_bpr"]), 1.0 / nr, stream())
+        # --- the BPR rows and their sparse gradient contributions, with the regulariser's |E0|^2 partials
+        _lib.call("gmr_dmm_bpr_sqnorm", B, U, ptr(w["Emb"]), ptr(users), ptr(pos), ptr(neg), ptr(w["loss_bpr"]),
+                  ptr(w["contrib_bpr"]), 1.0 / nr, N * 64, ptr(E0), ptr(w["sqws"]), stream())
         loss = w["loss"][:1]
-        _lib.call("gmr_sqnorm_part_f32", N * 64, ptr(E0), ptr(w["sqws"]), stream())
-        if BWD_EARLY and SPMM_FUSE & FUSE_BWD3 and not SPMM_FUSE & FUSE_BWD_CL:
-            return self._rec_bwd_early(w, users, plan_bpr, plan_cl, loss, nr, reg_share)
-        st.join(0, 1)
-        # BPR mean + regulariser + both InfoNCE means in one ordered reduction (calculate_loss, :243-249)
-        _lib.call("gmr_dmm_loss_total", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(w["sqws"]), self._sq_parts,
-                  self.reg_weight * reg_share, ptr(w["loss_cu"]), ptr(w["loss_ci"]), self.ssl_reg / nr, ptr(loss),
-                  stream())
-        # --- backward
-        dEmb, dCLN = w["dEmb"], w["dCLN"]
+        dEmb, dK = w["dEmb"], w["dCLN"]
         adj, iadj, tadj = self.norm_adj, self.image_UI_matrix, self.text_UI_matrix
-        dK = w["dCLN"]
-        # contrastive views (side stream 0, beside the BPR branch below): sparse terms into dCLN,
-        # dK = normalize backward (the +1e-8 shift has unit Jacobian), Tcl = adj^T dK
-        with st.on(0):
-            _lib.call("gmr_scatter_sorted_f32", plan_cl.numel(), 128, ptr(plan_cl), ptr(w["contrib_cl"]), 128,
-                      ptr(dCLN), 128, stream())
-            K.normalize_rows_bwd(w["CLN"][:, :64], w["nrmCL"][0], dCLN[:, :64], dK[:, :64])
-            K.normalize_rows_bwd(w["CLN"][:, 64:], w["nrmCL"][1], dCLN[:, 64:], dK[:, 64:])
-            if not SPMM_FUSE & FUSE_BWD_CL:
+
+        def scatter_bpr():
+            _lib.call("gmr_scatter_sorted_f32", plan_bpr.numel(), 64, ptr(plan_bpr), ptr(w["contrib_bpr"]), 64,
+                      ptr(dEmb), 64, stream())
+
+        def final_bwd():
+            # dE = [w0 dM | w1 dM] and the UI-graph sources' left halves lam * dE; dEmb cleared for the next step
+            _lib.call("gmr_dmm_final_bwd2", N, ptr(dEmb), ptr(w["T1"]), ptr(w["M"]), ptr(w["nrmM"]), self.ris_lambda,
+                      ptr(w["G"]), ptr(s.view("modal_weight")), ptr(w["dE"]), ptr(w["partials"]), 1,
+                      self.ris_adj_lambda, ptr(w["Ri"]), ptr(w["Rt"]), stream())
+
+        def loss_mw():
+            # BPR mean + regulariser + both InfoNCE means in one ordered reduction (calculate_loss, :243-249), the
+            # epoch sum, and the modal-weight gradient from final_bwd's partials: one launch on side stream 1
+            # (nothing on the main stream reads them; _rec_tail joins stream 1)
+            with st.on(1):
+                _lib.call("gmr_dmm_loss_mw", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(w["sqws"]), self._sq_parts,
+                          self.reg_weight * reg_share, ptr(w["loss_cu"]), ptr(w["loss_ci"]), self.ssl_reg / nr,
+                          ptr(loss), ptr(acc), w["partials"].numel() // 2, ptr(w["partials"]),
+                          ptr(s.view("modal_weight")), ptr(s.gview("modal_weight")), stream())
+
+        def scatter_cl():
+            # contrastive views: the sparse terms through the normalize backward, added to dK (the dense part of
+            # dK[:, 64:] came out of the table passes already through it)
+            _lib.call("gmr_scatter_sorted_nbwd_f32", plan_cl.numel(), ptr(plan_cl), ptr(w["contrib_cl"]), 128,
+                      ptr(w["CLN"]), ptr(w["nrmCL"]), N, ptr(dK), stream())
+
+        side = adj.side is not None  # side-split plan: the fused forms below (round 6)
+
+        def tcl():
+            # contrastive views through "K = C + adj@C" (diffmm.py:171-195): dC = dK + adj^T dK, written straight
+            # into the right halves of the UI-graph backward sources Ri / Rt (one SpMM with a separate beta source)
+            if side:
+                K.spmm_side2(adj, [w["Ri"][:, 64:], w["Rt"][:, 64:]], [(dK[:, :64],), (dK[:, 64:],)],
+                             [dK[:, :64], dK[:, 64:]], beta=1.0, partial=w["part_cl"])
+            else:
                 adj.spmm(w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], partial=w["part_cl"])
-        K.zero_(dEmb)
-        _lib.call("gmr_scatter_sorted_f32", plan_bpr.numel(), 64, ptr(plan_bpr), ptr(w["contrib_bpr"]), 64,
-                  ptr(dEmb), 64, stream())
-        # (no slab zeroing: every rec gradient segment is written, not accumulated - E0 by gmr_dmm_assemble,
-        # the projections by their GEMMs, modal_weight by gmr_dmm_mw_grad)
-        if SPMM_FUSE & FUSE_BWD_CL:  # Tcl = adj^T dK and T1 = adj^T dEmb (adj symmetric) in one launch
+
+        def cl_bwd():
+            if not side:  # dC = dK + Tcl into Ri / Rt's right halves; dK[:, :64] cleared
+                _lib.call("gmr_dmm_cl_bwd2", N, ptr(dK), ptr(w["Tcl"]), None, 0.0, ptr(w["Ri"]), ptr(w["Rt"]), 1, 0,
+                          stream())
+
+        def gcn_hops():
+            # second GCN hop T3 = adj^T dG, dG = dE + [T2[:U]; 0] (diffmm.py:141-153).  adj is bipartite: T3's user
+            # rows gather dG's item rows = dE's, i.e. they are T2's user rows; its item rows are
+            # adj^T (dE_u + T2_u) = T2_i + adj^T T2_u: one item-side product with T2 as the beta source
+            if side:
+                K.spmm_side2(adj, [w["T3"][:, :64], w["T3"][:, 64:]], [(w["T2"][:, :64],), (w["T2"][:, 64:],)],
+                             [w["T2"][:, :64], w["T2"][:, 64:]], beta=1.0, only_side=1)
+            else:
+                _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
+                adj.spmm(w["T3"], [(w["DG"][:, :64],), (w["DG"][:, 64:],)])
+
+        ui_t = [(self._transpose_of(iadj), w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)], None, None),
+                (self._transpose_of(tadj), w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)], None, None)]
+        t2 = (adj, w["T2"], [(w["dE"][:, :64],), (w["dE"][:, 64:],)], None, None)
+        if BWD_EARLY and SPMM_FUSE & FUSE_BWD3 and not SPMM_FUSE & FUSE_BWD_CL:
+            # GMR_BWD_EARLY: the BPR branch (dEmb scatter, T1 = adj^T dEmb, final_bwd) on the main stream beside the
+            # InfoNCE passes' tail; then the contrastive branch after the join (epoch 69.2 -> 67.7 ms, round 5)
+            scatter_bpr()
+            adj.spmm(w["T1"], [(dEmb,)])                                        # adj^T dEmb (adj symmetric)
+            final_bwd()
+            st.join(0, 1)
+            loss_mw()
+            scatter_cl()
+            tcl()
+            cl_bwd()
+            K.spmm_jobs(ui_t + [t2])
+            gcn_hops()
+            return self._rec_tail(w, loss, reg_share, side)
+        st.join(0, 1)
+        with st.on(0):  # contrastive views beside the BPR branch: dK, Tcl = adj^T dK
+            scatter_cl()
+            if not SPMM_FUSE & FUSE_BWD_CL or side:
+                tcl()
+        scatter_bpr()
+        if SPMM_FUSE & FUSE_BWD_CL and not side:  # Tcl = adj^T dK and T1 = adj^T dEmb (adj symmetric) in one launch
             st.join(0)
             K.spmm_jobs([(adj, w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], None, w["part_cl"]),
                          (adj, w["T1"], [(dEmb,)], None, None)])
         else:
-            adj.spmm(w["T1"], [(dEmb,)])                                        # adj^T dEmb (adj symmetric)
-        _lib.call("gmr_dmm_final_bwd", N, ptr(dEmb), ptr(w["T1"]), ptr(w["M"]), ptr(w["nrmM"]), self.ris_lambda,
-                  ptr(w["G"]), ptr(s.view("modal_weight")), ptr(w["dE"]), ptr(w["partials"]), stream())
-        _lib.call("gmr_dmm_mw_grad", w["partials"].numel() // 2, ptr(w["partials"]), ptr(s.view("modal_weight")),
-                  ptr(s.gview("modal_weight")), 0, stream())
+            adj.spmm(w["T1"], [(dEmb,)])
+        final_bwd()
+        loss_mw()
         if SPMM_FUSE & FUSE_BWD3:
-            # the UI-graph transposes of the contrastive/ris branch and the first GCN hop adj^T dE
-            # are independent: one launch; then the second hop.  cl_bwd reads dK / Tcl of the side stream.
+            # the UI-graph transposes of the contrastive/ris branch and the first GCN hop adj^T dE are
+            # independent: one launch; then the second hop.  cl_bwd reads dK / Tcl of the side stream.
             st.join(0)
-            _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
-                      ptr(w["Rt"]), stream())
-            K.spmm_jobs([(self._transpose_of(iadj), w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)], None, None),
-                         (self._transpose_of(tadj), w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)], None, None),
-                         (adj, w["T2"], [(w["dE"][:, :64],), (w["dE"][:, 64:],)], None, None)])
-            _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
-            adj.spmm(w["T3"], [(w["DG"][:, :64],), (w["DG"][:, 64:],)])
-            return self._rec_tail(w, loss, reg_share)
-        # the contrastive branch (side stream 0, now also after dE) and the two-hop GCN branch (main)
+            cl_bwd()
+            K.spmm_jobs(ui_t + [t2])
+            gcn_hops()
+            return self._rec_tail(w, loss, reg_share, side)
+        # the contrastive branch (side stream 0, now also after final_bwd) and the two-hop GCN branch (main)
         # only meet in assemble
         with st.on(0):
-            _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
-                      ptr(w["Rt"]), stream())
+            cl_bwd()
             if SPMM_FUSE & FUSE_UI_T:  # both UI-graph transposes in one launch
-                K.spmm_jobs([(self._transpose_of(iadj), w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)], None,
-                              None),
-                             (self._transpose_of(tadj), w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)], None,
-                              None)])
+                K.spmm_jobs(ui_t)
             else:
                 with st.on(1):
-                    self._transpose_of(tadj).spmm(w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)])
-                self._transpose_of(iadj).spmm(w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)])
+                    ui_t[1][0].spmm(w["OutT"], ui_t[1][2])
+                ui_t[0][0].spmm(w["OutI"], ui_t[0][2])
                 st.join(1)
-        adj.spmm(w["T2"], [(w["dE"][:, :64],), (w["dE"][:, 64:],)])
-        _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
-        adj.spmm(w["T3"], [(w["DG"][:, :64],), (w["DG"][:, 64:],)])
+        adj.spmm(w["T2"], t2[2])
+        gcn_hops()
         st.join(0)
-        return self._rec_tail(w, loss, reg_share)
+        return self._rec_tail(w, loss, reg_share, side)
 
-    def _rec_bwd_early(self, w, users, plan_bpr, plan_cl, loss, nr, reg_share):
-        """The backward of rec_step with the BPR branch issued before the InfoNCE join (GMR_BWD_EARLY): the same
-        kernels and arguments as the FUSE_BWD3 path, in an order whose only cross-stream dependency is the join
-        before the contrastive branch (dCLN is written by the InfoNCE passes and the sorted scatter below)."""
-        N, U = self.N, self.n_users
-        B = users.numel()
-        s = self.rec_slab
-        st = self._streams
-        adj, iadj, tadj = self.norm_adj, self.image_UI_matrix, self.text_UI_matrix
-        dEmb, dCLN = w["dEmb"], w["dCLN"]
-        dK = dCLN
-        # BPR branch (main), beside the InfoNCE passes on the side streams
-        K.zero_(dEmb)
-        _lib.call("gmr_scatter_sorted_f32", plan_bpr.numel(), 64, ptr(plan_bpr), ptr(w["contrib_bpr"]), 64,
-                  ptr(dEmb), 64, stream())
-        adj.spmm(w["T1"], [(dEmb,)])                                            # adj^T dEmb (adj symmetric)
-        _lib.call("gmr_dmm_final_bwd", N, ptr(dEmb), ptr(w["T1"]), ptr(w["M"]), ptr(w["nrmM"]), self.ris_lambda,
-                  ptr(w["G"]), ptr(s.view("modal_weight")), ptr(w["dE"]), ptr(w["partials"]), stream())
-        _lib.call("gmr_dmm_mw_grad", w["partials"].numel() // 2, ptr(w["partials"]), ptr(s.view("modal_weight")),
-                  ptr(s.gview("modal_weight")), 0, stream())
-        st.join(0, 1)
-        # BPR mean + regulariser + both InfoNCE means in one ordered reduction (calculate_loss, :243-249), on
-        # side stream 1 (nothing on the main stream reads it; _rec_tail joins stream 1)
-        with st.on(1):
-            _lib.call("gmr_dmm_loss_total", B, ptr(w["loss_bpr"]), 1.0 / nr, ptr(w["sqws"]), self._sq_parts,
-                      self.reg_weight * reg_share, ptr(w["loss_cu"]), ptr(w["loss_ci"]), self.ssl_reg / nr,
-                      ptr(loss), stream())
-        # contrastive branch (main): sparse terms into dCLN, dK = normalize backward, Tcl = adj^T dK
-        _lib.call("gmr_scatter_sorted_f32", plan_cl.numel(), 128, ptr(plan_cl), ptr(w["contrib_cl"]), 128,
-                  ptr(dCLN), 128, stream())
-        K.normalize_rows_bwd(w["CLN"][:, :64], w["nrmCL"][0], dCLN[:, :64], dK[:, :64])
-        K.normalize_rows_bwd(w["CLN"][:, 64:], w["nrmCL"][1], dCLN[:, 64:], dK[:, 64:])
-        adj.spmm(w["Tcl"], [(dK[:, :64],), (dK[:, 64:],)], partial=w["part_cl"])
-        _lib.call("gmr_dmm_cl_bwd", N, ptr(dK), ptr(w["Tcl"]), ptr(w["dE"]), self.ris_adj_lambda, ptr(w["Ri"]),
-                  ptr(w["Rt"]), stream())
-        K.spmm_jobs([(self._transpose_of(iadj), w["OutI"], [(w["Ri"][:, :64],), (w["Ri"][:, 64:],)], None, None),
-                     (self._transpose_of(tadj), w["OutT"], [(w["Rt"][:, :64],), (w["Rt"][:, 64:],)], None, None),
-                     (adj, w["T2"], [(w["dE"][:, :64],), (w["dE"][:, 64:],)], None, None)])
-        _lib.call("gmr_dmm_dg", N, U, ptr(w["dE"]), ptr(w["T2"]), ptr(w["DG"]), stream())
-        adj.spmm(w["T3"], [(w["DG"][:, :64],), (w["DG"][:, 64:],)])
-        return self._rec_tail(w, loss, reg_share)
-
-    def _rec_tail(self, w, loss, reg_share):
-        """assemble dE0 / dNF, then the modality projections' backward (end of rec_step)."""
+    def _rec_tail(self, w, loss, reg_share, side):
+        """assemble dE0 / dNF (dNF through the projections' normalize + leaky backward; with the fused side-split
+        backward also the clear of dK[:, :64] and T3's user rows read from T2), then the modality projections'
+        weight gradients (end of rec_step)."""
         N, U = self.N, self.n_users
         s = self.rec_slab
         st = self._streams
         E0 = s.view("E0")
-        _lib.call("gmr_dmm_assemble", N, U, ptr(w["T2"]), ptr(w["T3"]), ptr(w["OutI"]), ptr(w["OutT"]), ptr(E0),
-                  2.0 * self.reg_weight * reg_share, ptr(s.gview("E0")), ptr(w["dNF"]), stream())
+        dNF = w["dNF"]
+        _lib.call("gmr_dmm_assemble2", N, U, ptr(w["T2"]), ptr(w["T3"]), ptr(w["OutI"]), ptr(w["OutT"]), ptr(E0),
+                  2.0 * self.reg_weight * reg_share, ptr(s.gview("E0")), ptr(dNF), ptr(w["NF"]), ptr(w["nrmF"]), 0.2,
+                  ptr(w["dCLN"]) if side else None, int(side), stream())
         if dist.is_dist() and EARLY_REDUCE and self.dp_early_reduce:
             # data parallel: E0's gradient (6.8 MB of the 7.9 MB slab) is final here; its RCCL all-reduce
             # runs beside the projection-weight GEMMs below (the Trainer reduces the rest and waits)
@@ -434,16 +462,16 @@ class DiffMM(GeneralRecommender):
                 raise RuntimeError("rec_step: the previous step's early all-reduce was never taken "
                                    "(reduce_slab_grads consumes it)")
             self._early = dist.all_reduce_start(s.grad[:self.early_reduce_cut(s)])
-        # modality projections: normalize + leaky-relu backward, then W grads (text beside image)
-        dNF = w["dNF"]
+        # modality projection weight gradients (text beside image)
         with st.on(1):
-            K.normalize_rows_bwd(w["NF"][:, 64:], w["nrmF"][1], dNF[:, 64:], dNF[:, 64:], slope=0.2)
             K.gemm(self.t_feat, dNF[:, 64:], s.gview("text_trans"), trans_a=True)
-        K.normalize_rows_bwd(w["NF"][:, :64], w["nrmF"][0], dNF[:, :64], dNF[:, :64], slope=0.2)
         K.gemm(self.v_feat, dNF[:, :64], s.gview("image_trans"), trans_a=True)
         st.join(1)
         self._step += 1
         return loss[0]
+
+    def tape_replayed(self):
+        self._step += 1
 
     def early_reduce_cut(self, slab):
         """Gradient words of `slab` that rec_step all-reduces itself (E0, issued as soon as it is final);

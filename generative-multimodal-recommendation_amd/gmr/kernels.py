@@ -12,6 +12,7 @@ import torch
 from . import _lib
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_TANH, EPI_LEAKY, EPI_POSTERIOR, EPI_DTANH, EPI_ROWSCALE_AUX, EPI_BIAS_RELU, EPI_DRELU = range(9)
+EPI_LEAKY_NORM = 9  # leaky + row normalisation in the split-K reduce: aux = normalised rows, rv1 = norms (written)
 
 _ws = {}
 
@@ -90,6 +91,12 @@ class Streams:
 
     PRIORITY = int(os.environ.get("GMR_SIDE_PRIO", "0"))  # torch stream priority of the side streams (-1: high)
 
+    # stream-ordering probe (tests/test_stream_order_gpu.py): None, or (where, i, us) - at every fork onto side
+    # stream i a ~us-microsecond sleep kernel is queued on that side stream ("side": its work starts late, so a
+    # main-stream read of it without a join sees stale data) or on the forking stream ("main": the side work runs
+    # ahead of everything the forking stream issues next).  A correctly joined step gives the same bits either way.
+    PERTURB = None
+
     def __init__(self, n):
         self.side = [torch.cuda.Stream(priority=Streams.PRIORITY) for _ in range(n)]
         self._raw = [ctypes.c_void_p(s.cuda_stream) for s in self.side]
@@ -145,6 +152,9 @@ class _OnSide:
         if _cur_device is not None and _cur_device() != st._dev:
             raise RuntimeError(f"Streams built on device {st._dev} used while device {_cur_device()} is current")
         _lib.call("gmr_stream_fork", stream(), st._raw[i], st._ev[2 * i])
+        pb = Streams.PERTURB
+        if pb is not None and pb[1] == i:
+            _lib.call("gmr_delay", int(pb[2]), st._raw[i] if pb[0] == "side" else stream())
         if _get_stream is None or _set_stream is None:
             self.prev = None
             self.ctx = torch.cuda.stream(st.side[i])
@@ -448,6 +458,42 @@ def _side_call(self, nb, lo, ldl, hi, ldh, split, alpha, beta, ys, ldy, partial)
 
 
 CSR._side_call = _side_call
+
+
+def spmm_side2(a, outs, blocks, z, split=None, alpha=1.0, beta=1.0, only_side=-1, partial=None):
+    """outs[b] = alpha * A @ X_b + beta * z[b] on a side-split plan (gmr_spmm_side2_f32): X_b = blocks[b] (a (lo,)
+    or (lo, hi) split source as in CSR.spmm), z[b] an n_rows x 64 view (the beta term's source, may differ from
+    outs[b]); only_side 0 / 1 computes only the rows below / from the split (the others are left untouched)."""
+    if a.side is None:
+        raise ValueError("spmm_side2 needs a side-split plan")
+    nb = len(blocks)
+    if nb not in (1, 2, 4) or len(outs) != nb or len(z) != nb:
+        raise ValueError("1, 2 or 4 blocks, one output and one z view each")
+    for o in list(outs) + list(z):
+        if o.shape != (a.n_rows, 64):
+            raise ValueError(f"output / z block shape {tuple(o.shape)} != ({a.n_rows}, 64)")
+    PArr, LArr = ctypes.c_void_p * 4, ctypes.c_int64 * 4
+    lo = PArr(*[b[0].data_ptr() for b in blocks] + [0] * (4 - nb))
+    ldl = LArr(*[_ld(b[0]) for b in blocks] + [0] * (4 - nb))
+    if split is None:
+        split, hi, ldh = a.n_cols, lo, ldl
+    else:
+        hi = PArr(*[b[1].data_ptr() for b in blocks] + [0] * (4 - nb))
+        ldh = LArr(*[_ld(b[1]) for b in blocks] + [0] * (4 - nb))
+    ys = PArr(*[o.data_ptr() for o in outs] + [0] * (4 - nb))
+    ldy = LArr(*[_ld(o) for o in outs] + [0] * (4 - nb))
+    zs = PArr(*[o.data_ptr() for o in z] + [0] * (4 - nb))
+    ldz = LArr(*[_ld(o) for o in z] + [0] * (4 - nb))
+    key = (a.nnz, a.n_rows, a.n_cols, nb, beta != 0.0)
+    if only_side >= 0:  # one side of a bipartite product: its rows, half the entries, the other side's X rows
+        sp = a.side[1]
+        rows = sp if only_side == 0 else a.n_rows - sp
+        key = (a.nnz // 2, rows, a.n_rows - rows, nb, beta != 0.0)
+    with _Probe("spmm", key):
+        _lib.call("gmr_spmm_side2_f32", ptr(a.side[0]), nb, lo, ldl, hi, ldh, int(split), float(alpha), float(beta), zs,
+                  ldz, ys, ldy, int(only_side), ptr(a.partial if partial is None else partial), a.side_wpx[nb],
+                  stream())
+    return outs
 
 
 class GraphExec:

@@ -22,6 +22,7 @@ from . import dist
 from . import kernels as K
 from .kernels import ptr, stream
 from .slab import FlatAdam
+from .tape import Tape
 from .topk_evaluator import TopKEvaluator
 from .utils import dict2str, early_stopping
 
@@ -36,6 +37,10 @@ GRAPH_EXEC = os.environ.get("GMR_GRAPH_EXEC", "1") != "0"
 # Diffusion phase 22.6 -> 22.0-22.8 ms, epoch 68.3 -> 67.9 ms averaged over three pairs (within the box's
 # noise; profiles/r05ze_indep_denoisers_ab.txt)
 INDEP_DENOISERS = os.environ.get("GMR_INDEP_DENOISERS", "1") != "0"
+# one process, full-size BPR batches of models whose rec step is a fixed call sequence (DiffMM: `tape_safe`): the
+# step's C-ABI calls are recorded once per epoch (per graph rebuild) and replayed without the Python layer
+# (gmr/tape.py); GMR_TAPE=0 issues every step through Python
+TAPE = os.environ.get("GMR_TAPE", "1") != "0"
 
 
 _CAPTURE = {}
@@ -124,6 +129,8 @@ class Trainer:
         # the replay appears to lose the three-stream overlap of the eager step).
         self._use_graphs = os.environ.get("GMR_GRAPHS", "0") == "1" and hasattr(model, "graph_key")
         self._graph = None
+        self._use_tape = TAPE and getattr(model, "tape_safe", False)
+        self._tape = None
         self.fused_eval = FUSED_EVAL  # per trainer, so a test can run both eval paths in one process
 
     def _build_optimizer(self):
@@ -151,11 +158,15 @@ class Trainer:
             if u.numel() > 0:
                 if self._use_graphs and W == 1 and u.numel() == train_data.batch_size:
                     self._graphed_step(u, p, ng, pb, pc, norm, share, acc)
+                elif self._use_tape and W == 1 and u.numel() == train_data.batch_size and K._probe is None:
+                    self._taped_step(u, p, ng, pb, pc, norm, share, acc)
                 elif W > 1 and getattr(self.model, "rec_step_takes_batch", False):
                     # in-batch terms see the whole global step (GenRecV1's B x B InfoNCE keys)
                     loss = self.model.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share,
                                                gbatch=train_data.step_rows(d, b))
                     _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
+                elif getattr(self.model, "rec_step_takes_acc", False):  # the step adds its loss to acc itself
+                    self.model.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share, acc=acc)
                 else:
                     loss = self._rec_step(u, p, ng, pb, pc, norm, share, sum(rank_rows[:dist.rank()]))
                     _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
@@ -182,6 +193,27 @@ class Trainer:
         if getattr(self.model, "rec_step_takes_row0", False):
             return self.model.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share, row0=row0)
         return self.model.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share)
+
+    def _taped_step(self, u, p, ng, pb, pc, norm, share, acc):
+        """One full-size BPR step replayed from a host tape (gmr/tape.py): the eager step's calls, streams and
+        order, without the Python layer.  Recorded on the first step after the model's device graphs, the
+        batch shape, the current stream or the stream probes change (the recording step runs eagerly)."""
+        m = self.model
+        key = (u.numel(), norm, share, m.graph_key(), stream().value, K.Streams.SERIAL, K.Streams.PERTURB)
+        inputs = (u, p, ng, pb, pc)
+        if self._tape is None or self._tape[0] != key:
+            self._tape = None
+            t = Tape(inputs)
+            with t.recording():
+                if getattr(m, "rec_step_takes_acc", False):
+                    m.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share, acc=acc)
+                else:
+                    loss = m.rec_step(u, p, ng, pb, pc, norm_rows=norm, reg_share=share)
+                    _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
+            self._tape = (key, t)
+            return
+        self._tape[1].replay(inputs)
+        m.tape_replayed()
 
     def _graphed_step(self, u, p, ng, pb, pc, norm, share, acc):
         """One full-size BPR step replayed from a HIP graph (torch.cuda.CUDAGraph over the fused

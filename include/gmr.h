@@ -48,6 +48,10 @@ extern "C" {
 #define GMR_GEMM_X6 (1 << 26)        /* tile flag: split-bf16 operands on the bf16 MFMA (six products, fp32-accurate) */
 #define GMR_GEMM_F32 (1 << 27)       /* tile flag: force the fp32-input MFMA (overrides GMR_GEMM_X6=1 in the environment) */
 #define GMR_EPI_DRELU 8        /* C = aux[m,n] > 0 ? alpha*acc : 0  ReLU (+ dropout) backward  */
+#define GMR_EPI_LEAKY_NORM 9   /* C = leaky_relu(alpha*acc + bias, slope) and its row normalisation in the split-K
+                                  reduce: aux (WRITTEN, ld_aux) = C[m] / max(|C[m]|, 1e-12), rowvec1 (WRITTEN) = that
+                                  norm; N = 64 plans with split-K only (DiffMM modality projection + F.normalize,
+                                  models/diffmm.py:115-127, 138-149) */
 
 const char* gmr_last_error_string(void);
 int gmr_version(void);
@@ -57,6 +61,9 @@ int gmr_zero(void* ptr, int64_t bytes, void* stream);
 int gmr_event_create(void** ev /* host */);
 int gmr_event_destroy(void* ev);
 int gmr_stream_fork(void* from, void* to, void* ev);
+/* test probe (no reference counterpart): a one-wave kernel that sleeps ~us microseconds on `stream`, used to
+ * perturb side-stream timing in the stream-ordering tests */
+int gmr_delay(int32_t us, void* stream);
 
 /* ---------------------------------------------------------------- K1 graph convolution
  * Y = alpha * A * X + beta * Y for CSR A (int32 rowptr/col, fp32 val).
@@ -183,6 +190,14 @@ int gmr_spmm_side_tune(int32_t wpx, int32_t eb);
 int gmr_spmm_side_f32(const int32_t* plan, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
                       const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
                       float* const* y_blocks, const int64_t* ld_y, float* scratch, int32_t wpx, void* stream);
+/* The same product as Y = alpha A X + beta Z: z_blocks / ld_z (NULL: Z = Y) give the beta term's source, and
+ * only_side 0 / 1 computes only the rows < split / >= split (the other rows of Y are left untouched; -1: all),
+ * with all eight XCDs on that side.  DiffMM's backward (round 6, models/diffmm.py:141-195): Tcl and the
+ * contrastive views' dC = dK + adj^T dK in one pass, and the second GCN hop's item rows T3i = T2i + adj^T T2u. */
+int gmr_spmm_side2_f32(const int32_t* plan, int32_t n_blocks, const float* const* x_lo, const int64_t* ld_lo,
+                       const float* const* x_hi, const int64_t* ld_hi, int64_t split, float alpha, float beta,
+                       const float* const* z_blocks, const int64_t* ld_z, float* const* y_blocks, const int64_t* ld_y,
+                       int32_t only_side, float* scratch, int32_t wpx, void* stream);
 /* Up to 4 independent side-split products of the same width (n_blocks) in ONE launch (round 5; the forward's
  * Qi / Qt / G and the backward's UI-graph transposes, models/diffmm.py:129-195): job q has its own plan,
  * hub scratch, split and block arrays at entries [4 q, 4 q + n_blocks) of x_lo / ld_lo / x_hi / ld_hi / y /
@@ -277,6 +292,32 @@ int gmr_dmm_cl_bwd(int64_t n, const float* dK, const float* T, const float* dE, 
                    void* stream);
 int gmr_dmm_assemble(int64_t n, int64_t U, const float* T2, const float* T3, const float* Ri, const float* Rt,
                      const float* E0, float reg2, float* dE0, float* dNF, void* stream);
+/* Round 6: the rec step's small passes folded into their neighbours (same reference lines).
+ * final_bwd2: clear != 0 zeroes dEmb after reading it (its last reader; the next step's sorted scatter adds onto
+ *   zeros, so no fill pass); Ri / Rt (both or neither): also write lam * dE_img / lam * dE_txt into their left
+ *   halves (what gmr_dmm_cl_bwd writes there).
+ * cl_bwd2: clear != 0 zeroes dK[:, :64] after reading it; left = 0 leaves Ri / Rt's left halves alone.
+ * assemble2: dNF leaves through the modality projections' normalize + leaky-ReLU backward (NF = the normalised
+ *   projections I x 128, nrmF = their norms [2][I], slope) - gmr_normalize_rows_bwd_f32 on each half, same bits;
+ *   dK_clear (N x 128, optional): its [:, :64] half is zeroed (the contrastive view gradient's last reader);
+ *   t3u_from_t2: T3's user rows are read from T2 (they are equal: adj is bipartite) - T3 holds item rows only.
+ * bpr_sqnorm: gmr_bpr_fwd_bwd and gmr_sqnorm_part_f32(n_sq, x, sq_parts) in one launch (same bits).
+ * loss_mw: gmr_dmm_loss_total (+ acc[0] += loss when acc is not NULL: the trainer's epoch-loss sum) and
+ *   gmr_dmm_mw_grad (accumulate 0) in one two-block launch. */
+int gmr_dmm_final_bwd2(int64_t n, float* dEmb, const float* T1, const float* M, const float* nrmM, float ris,
+                       const float* E, const float* mw, float* dE, float* partials, int32_t clear, float lam, float* Ri,
+                       float* Rt, void* stream);
+int gmr_dmm_cl_bwd2(int64_t n, float* dK, const float* T, const float* dE, float lam, float* Ri, float* Rt,
+                    int32_t clear, int32_t left, void* stream);
+int gmr_dmm_assemble2(int64_t n, int64_t U, const float* T2, const float* T3, const float* Ri, const float* Rt,
+                      const float* E0, float reg2, float* dE0, float* dNF, const float* NF, const float* nrmF,
+                      float slope, float* dK_clear, int32_t t3u_from_t2, void* stream);
+int gmr_dmm_bpr_sqnorm(int32_t B, int64_t U, const float* Emb, const int32_t* users, const int32_t* pos,
+                       const int32_t* neg, float* loss, float* contrib, float inv_norm, int64_t n_sq, const float* x,
+                       double* sq_parts, void* stream);
+int gmr_dmm_loss_mw(int64_t B, const float* loss_bpr, float inv_nr, const double* parts, int64_t nparts,
+                    float reg_scale, const float* loss_cu, const float* loss_ci, float ssl_scale, float* out,
+                    float* acc, int64_t n_mw_parts, const float* mw_parts, const float* mw, float* dmw, void* stream);
 
 /* F.normalize (p=2, eps=1e-12) over rows and its backward (optionally fused with leaky-ReLU backward) */
 int gmr_normalize_rows_f32(int64_t n, int32_t cols, const float* x, int64_t ldx, float* y, int64_t ldy, float* nrm,
@@ -314,11 +355,25 @@ int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int64_t ldp, co
                            const float* CLN, const int32_t* nodes, int64_t node_off, float inv_temp, float coef,
                            float* loss, float* contrib, int64_t ld_contrib, float* dT, int64_t ld_dt, float* workspace,
                            int64_t workspace_floats, void* stream);
+/* The same with dT taken through the normalize backward of the table's view in the reduce pass (y = the
+ * normalised table rows n x 64, ldy; nrm = their norms): dT = nbwd(dense gradient).  DiffMM: the dense part of
+ * dK[:, 64:] (contrastLoss's F.normalize, diffmm.py:252-253); the sparse part goes through
+ * gmr_scatter_sorted_nbwd_f32 (the normalize backward is linear in its input). */
+int gmr_contrast_fused_nbwd_f32(int32_t B, int64_t n, const float* P, int64_t ldp, const float* T, int64_t ldt,
+                                const float* CLN, const int32_t* nodes, int64_t node_off, float inv_temp, float coef,
+                                float* loss, float* contrib, int64_t ld_contrib, float* dT, int64_t ld_dt,
+                                const float* y, int64_t ldy, const float* nrm, float* workspace,
+                                int64_t workspace_floats, void* stream);
 /* K2 gather / deterministic scatter-add through a sorted (key << 32 | slot) plan */
 int gmr_gather_rows_f32(int32_t B, int32_t cols, const float* src, int64_t lds, const int32_t* idx, int64_t off,
                         float* out, int64_t ldo, void* stream);
 int gmr_scatter_sorted_f32(int32_t n, int32_t cols, const uint64_t* plan, const float* contrib, int64_t ldc,
                            float* dst, int64_t ldd, void* stream);
+/* 128-wide contribution rows through the plan, each 64-column half taken through the normalize backward of the
+ * contrastive view it belongs to (y = CLN, N x 128; nrm = [2][n_nodes] norms) and ADDED to dK (N x 128):
+ * dK[key] += [nbwd(s[:64]) | nbwd(s[64:])]  (DiffMM contrastLoss's sparse terms, diffmm.py:252-258) */
+int gmr_scatter_sorted_nbwd_f32(int32_t n, const uint64_t* plan, const float* contrib, int64_t ldc, const float* y,
+                                const float* nrm, int64_t n_nodes, float* dK, void* stream);
 int gmr_sort_batch_keys(int64_t n_batches, const int32_t* keys, const int64_t* offsets, const int32_t* key_add,
                         int32_t n_keysets, int64_t key_stride, uint64_t* out, int64_t out_stride, int32_t pow2,
                         void* stream);

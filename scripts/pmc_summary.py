@@ -21,13 +21,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLASSES = {"gemm": ("gemm_kernel", "gemm_glds_kernel", "splitk_reduce_kernel"),
            "gemm_x6": ("gemm_x6_kernel", "split3_planes_kernel"),
            "spmm": ("spmm_seg_kernel", "spmm_fix_kernel", "spmm_lane_kernel", "spmm_lane_jobs_kernel",
-                    "lane_fix_kernel", "lane_fix_jobs_kernel", "spmm_blk_kernel", "spmm_chunk_kernel", "spmm_side_kernel"),
+                    "lane_fix_kernel", "lane_fix_jobs_kernel", "spmm_blk_kernel", "spmm_chunk_kernel", "spmm_side_kernel",
+                    "spmm_side_jobs_kernel"),
            "infonce": ("cl_rows_kernel", "cl_table_kernel", "cl6_kernel", "cl6p_kernel", "cl_finalize_kernel",
-                       "cl_table_reduce_kernel")}
+                       "cl_table_reduce_kernel", "cl_table_reduce_nbwd_kernel")}
 # launches of a class = launches of its primary kernels (one per gmr_* call)
 PRIMARY = {"gemm": ("gemm_kernel", "gemm_glds_kernel"), "gemm_x6": ("gemm_x6_kernel",),
            "spmm": ("spmm_seg_kernel", "spmm_lane_kernel", "spmm_lane_jobs_kernel", "spmm_blk_kernel",
-                    "spmm_chunk_kernel", "spmm_side_kernel"),
+                    "spmm_chunk_kernel", "spmm_side_kernel",
+                    "spmm_side_jobs_kernel"),
            "infonce": ("cl_rows_kernel", "cl6_rows")}
 UTIL = {"gemm": ("gemm_kernel", "gemm_glds_kernel"), "gemm_x6": ("gemm_x6_kernel",), "spmm": (),
         "infonce": ("cl_rows_kernel", "cl_table_kernel", "cl6_kernel", "cl6p_kernel")}
