@@ -1654,6 +1654,7 @@ int contrast_fused(const char* fn, int32_t B, int64_t n, const float* P, int64_t
                       : (fast ? cl6_kernel<true, false> : cl6_kernel<false, false>);
     auto table6 = pipe ? (fast ? cl6p_kernel<true, true> : cl6p_kernel<false, true>)
                        : (fast ? cl6_kernel<true, true> : cl6_kernel<false, true>);
+
     hipLaunchKernelGGL(rows6, ga, dim3(256), 0, st, B, (int)n, P, ldp, T, ldt, nullptr, inv_temp, p.chunk_a, part_u,
                        part_z, nullptr, nullptr, 0);
     GMR_LAUNCHED();

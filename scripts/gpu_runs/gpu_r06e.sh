@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 6 (e): gc-row error diagnostics (denoiser output vs fp64, Z product vs exact)
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -q -s --timeout 200 --timeout-method thread tests/test_diffmm_train_gpu.py -m gpu \
+  -k "diffusion_step_vs" > gpurun_out/r06e_gc.log 2>&1
+grep -E "^\[|passed|failed" gpurun_out/r06e_gc.log
+echo done

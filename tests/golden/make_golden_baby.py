@@ -35,6 +35,7 @@ Usage:  python tests/golden/make_golden_baby.py [baby|sports|diffrec|diffrec_tra
          (main_diffrec_train's docstring)
   diffmm_train -> diffmm_baby_train.npz / _meta.json: one diffusion step per denoiser and one rec step at
          the baby shape with the reference's draws / batch (main_diffmm_train's docstring), ~30 s
+  diffmm_train_sports -> diffmm_sports_train.npz / _meta.json: the same at config 4's sports shape, ~2 min
   vbpr   (config 1) -> vbpr_baby.npz / _meta.json: VBPR init digests, one loss + backward, valid top-50 +
          metrics, each also in fp64 (main_vbpr's docstring), about a minute
 """
@@ -295,8 +296,9 @@ def _reference_diffmm(shape="baby"):
     return ref, cfg, tr, tl, model
 
 
-def main_diffmm_train():
-    """DiffMM training at the baby shape (VERDICT r4 missing #1), from the seed-999 init:
+def main_diffmm_train(shape="baby"):
+    """DiffMM training at the baby shape (VERDICT r4 missing #1) or, with shape = "sports", at config 4's
+    35,598 x 18,357 shape (VERDICT r5 missing #3), from the seed-999 init:
 
     diffusion  one step of the reference's diffusion loop (common/trainer.py:505-527) on 2,048 users
                (the first 2,048 of a seeded permutation, x0 = their train rows as the DiffusionDataset
@@ -309,17 +311,20 @@ def main_diffmm_train():
                denoiser gradient (whole when small, else row / column sums + 4,096 sampled entries).
     rec step   calculate_loss (models/diffmm.py:203-249) + backward on the reference loader's first
                2,048-row batch, with the UI graphs built from the reference's own top-1 p_sample edges
-               (diffmm_baby.npz, trainer.py:545-576): loss, its parts, and every rec gradient.
+               (diffmm_<shape>.npz, trainer.py:545-576): loss, its parts, and every rec gradient.
+    Round 6: the reference's own image / text feats of the diffusion step (getImageFeats / getTextFeats,
+    models/diffmm.py:115-127) are stored too, so the test can feed the denoiser step exactly the reference's
+    inputs (the gc loss rows then compare the diffusion kernels alone, not the projection GEMM's rounding).
     """
     import torch
-    ref, cfg, tr, tl, model = _reference_diffmm("baby")
+    ref, cfg, tr, tl, model = _reference_diffmm(shape)
     U, I = model.n_users, model.n_items
     B = int(cfg["train_batch_size"])
     e_loss = float(cfg["e_loss"])
     dm = model.diffusion_model
     meta = {"U": U, "I": I, "n_train": len(tr), "B": B, "e_loss": e_loss, "torch": torch.__version__,
-            "numpy": np.__version__, "generator": "tests/golden/make_golden_baby.py diffmm_train",
-            "reference": REF_SRC}
+            "numpy": np.__version__, "generator": f"tests/golden/make_golden_baby.py diffmm_train {shape}",
+            "reference": REF_SRC, "shape": shape}
     out = {}
     rs = np.random.default_rng(31)
     users = rs.permutation(U)[:B]
@@ -333,6 +338,8 @@ def main_diffmm_train():
             x0[r, it] = 1.0
     iE = model.getItemEmbeds().detach()
     feats = {"image": model.getImageFeats().detach(), "text": model.getTextFeats().detach()}
+    for m in feats:
+        out[f"dif_feats_{m}"] = feats[m].numpy().astype(np.float32)
     dens = {m: getattr(model, "denoise_model_" + m) for m in ("image", "text")}
     picks = {}
     for mod, den in dens.items():
@@ -389,8 +396,39 @@ def main_diffmm_train():
                                   "keep_sha256": hashlib.sha256(keep.numpy().tobytes()).hexdigest()}
         for n, p_ in dens[mod].named_parameters():
             _grad_record(out, f"dif_g_{mod}_" + n.replace(".", "_"), p_.grad.detach().numpy(), picks.get((mod, n)))
+        # the same step evaluated in float64 (round 6): the reference's parameters, inputs and draws widened (the
+        # fp32 schedule coefficients and time embedding as the reference computes them), so the per-row diff / gc
+        # losses have a truth that both the reference's fp32 run and the HIP path are measured against
+        import copy
+        den64 = copy.deepcopy(dens[mod]).double()
+        den64.emb_layer.register_forward_pre_hook(lambda m_, a: (a[0].double(),))
+        keep64 = keep.double()
+        den64.drop.register_forward_hook(lambda m_, i, o, k=keep64, q=p: i[0] * k / (1 - q))
+        orig_randint = torch.randint
+        rng_state = torch.get_rng_state()  # (the widened Dropout still draws: the replay loop's stream is kept)
+        torch.randn_like = lambda x, *a, **k: noise.double()
+        torch.randint = lambda *a, **k: ts.clone()
+        try:
+            cap64 = []
+            hz = den64.register_forward_hook(lambda m_, i, o: cap64.append(o.detach().clone()))
+            with torch.no_grad():
+                d64, g64 = dm.training_losses(den64, x0.double(), iE.double(), torch.as_tensor(users).double(),
+                                              feats[mod].double())
+            hz.remove()
+            # Z = out @ feats (the gc term's model embeddings) and 4,096 sampled entries of the output, in fp64
+            out[f"dif_{mod}_Z64"] = (cap64[0] @ feats[mod].double()).numpy()
+            out[f"dif_{mod}_out64_pick"] = cap64[0].reshape(-1).numpy()[out[f"dif_pick_{mod}_out_layers_0_weight"]]
+        finally:
+            torch.randn_like = orig_randn_like
+            torch.randint = orig_randint
+            torch.set_rng_state(rng_state)
+        out[f"dif_{mod}_diff_rows64"] = d64.numpy().astype(np.float64)
+        out[f"dif_{mod}_gc_rows64"] = g64.numpy().astype(np.float64)
+        rel = lambda a, b: float(np.max(np.abs(a - b) / np.abs(b)))  # noqa: E731
+        meta["diffusion"][mod]["fp32_vs_fp64_rel"] = {"diff_rows": rel(out[f"dif_{mod}_diff_rows"], d64.numpy()),
+                                                      "gc_rows": rel(out[f"dif_{mod}_gc_rows"], g64.numpy())}
     # ---- rec step on the reference's UI graphs (its own top-1 edges, diffmm_baby.npz)
-    gb = np.load(os.path.join(HERE, "diffmm_baby.npz"), allow_pickle=False)
+    gb = np.load(os.path.join(HERE, f"diffmm_{shape}.npz"), allow_pickle=False)
     rb = object.__new__(ref["trainer"].DiffMMTrainer)
     rb.user_num, rb.item_num, rb.device = U, I, torch.device("cpu")
     ones = np.ones(U)
@@ -424,11 +462,11 @@ def main_diffmm_train():
     gi = model.iEmbeds.grad.detach().numpy()
     out["rec_g_uEmbeds_rows"] = gu[batch[0][:256].numpy()].astype(np.float32)
     out["rec_g_iEmbeds_rows"] = gi[batch[1][:256].numpy()].astype(np.float32)
-    np.savez_compressed(os.path.join(HERE, "diffmm_baby_train.npz"), **out)
-    with open(os.path.join(HERE, "diffmm_baby_train_meta.json"), "w") as f:
+    np.savez_compressed(os.path.join(HERE, f"diffmm_{shape}_train.npz"), **out)
+    with open(os.path.join(HERE, f"diffmm_{shape}_train_meta.json"), "w") as f:
         json.dump(meta, f, indent=1, default=float)
     shutil.rmtree(TMP)
-    print("wrote", os.path.join(HERE, "diffmm_baby_train.npz"), meta["diffusion"], meta["rec"])
+    print("wrote", os.path.join(HERE, f"diffmm_{shape}_train.npz"), meta["diffusion"], meta["rec"])
 
 
 def main_vbpr():
@@ -545,10 +583,12 @@ def main():
         return main_diffrec_train()
     if shape == "diffmm_train":
         return main_diffmm_train()
+    if shape == "diffmm_train_sports":
+        return main_diffmm_train("sports")
     if shape == "vbpr":
         return main_vbpr()
     if shape not in ("baby", "sports"):
-        raise SystemExit("shape: baby, sports, diffrec, diffrec_train, diffmm_train or vbpr")
+        raise SystemExit("shape: baby, sports, diffrec, diffrec_train, diffmm_train, diffmm_train_sports or vbpr")
     ref = _import_reference()
     import torch
     import utils.utils as rutils

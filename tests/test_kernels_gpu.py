@@ -495,7 +495,7 @@ def test_contrast_table_fixup_bit_exact(K, B, n, monkeypatch):
     _contrast_env_bit_exact(K, B, n, monkeypatch, "GMR_CL_FIXUP", repeats=3)
 
 
-def _contrast_env_bit_exact(K, B, n, monkeypatch, env, repeats=1):
+def _contrast_env_bit_exact(K, B, n, monkeypatch, env, repeats=1, value="1"):
     monkeypatch.setenv("GMR_CL_X6", "1")
     rng = _rng(13)
     C = rng.standard_normal((n, 128)).astype(np.float32)
@@ -506,7 +506,7 @@ def _contrast_env_bit_exact(K, B, n, monkeypatch, env, repeats=1):
     K.gather_rows(Cd[:, :64], nd, P, off=0)
     ws = K.contrast_workspace(B, n, DEV, "test_cl_" + env)
     outs = []
-    for pipe in ["0"] + ["1"] * repeats:
+    for pipe in ["0"] + [value] * repeats:
         monkeypatch.setenv(env, pipe)
         loss = torch.empty(B, device=DEV)
         contrib = torch.empty((B, 128), device=DEV)

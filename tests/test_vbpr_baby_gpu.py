@@ -27,7 +27,7 @@ import pytest
 import torch
 
 from test_baby_gpu import EVAL_PATHS, check_metrics_vs_reference, check_topk_vs_reference
-from test_diffmm_baby_train_gpu import _check_grad
+from test_diffmm_train_gpu import _check_grad
 
 pytestmark = pytest.mark.gpu
 
