@@ -57,10 +57,6 @@ SIGNATURES = {
     "gmr_spmm_side_tune": (I32, [I32, I32]),
     "gmr_spmm_side_f32": (I32, [P, I32, P, P, P, P, I64, F32, F32, P, P, P, I32, P]),
     "gmr_spmm_side2_f32": (I32, [P, I32, P, P, P, P, I64, F32, F32, P, P, P, P, I32, P, I32, P]),
-    "gmr_graph_exec_create": (I32, [P, I32, P, P]),
-    "gmr_graph_exec_info": (I32, [P, P, P, P, P]),
-    "gmr_graph_exec_launch": (I32, [P, P]),
-    "gmr_graph_exec_destroy": (I32, [P]),
     "gmr_spmm_side_jobs_f32": (I32, [I32, P, P, I32, P, P, P, P, P, F32, F32, P, P, I32, P]),
     "gmr_bipartite_nnz": (I64, [I64, I64, I64, I32]),
     "gmr_bipartite_workspace_ints": (I64, [I64, I64]),
@@ -185,12 +181,8 @@ SIGNATURES = {
     "gmr_xattn_fwd_f32": (I32, [I64, I32, I32, P, P, F32, P, P, I64, U64, U64, I64, P, I64, P]),
     "gmr_xattn_bwd_workspace_floats": (I64, [I64, I32, I32]),
     "gmr_xattn_bwd_f32": (I32, [I64, I32, I32, P, I64, P, I64, P, P, F32, P, P, P, I64, P]),
-    "gmr_decoder_split_f32": (I32, [I32, I32, P, P, I64, P, P]),
     "gmr_nce_pairs_f32": (I32, [I32, I64, I64, I64, P, P, P, I64, P, I64, P]),
     "gmr_nce_combine_f32": (I32, [I32, I64, I64, I64, P, P, P, I64, P, I64, P, I64, P]),
-    "gmr_decoder_masks_u8": (I32, [I64, I32, I32, I32, F32, U64, U64, I64, P, P, I64, P, P, P, P, I64, P]),
-    "gmr_decoder_fwd_f32": (I32, [I64, I32, I32, I32, P, I64, P, I64, P, P, I64, P, P, F32, I32, P, P, I64, P, P, P, P,
-                                  I64, P, I64, I64, I64, P]),
 }
 
 _lib = None

@@ -496,41 +496,6 @@ def spmm_side2(a, outs, blocks, z, split=None, alpha=1.0, beta=1.0, only_side=-1
     return outs
 
 
-class GraphExec:
-    """Native multi-stream executor of a captured step (include/gmr.h gmr_graph_exec_*): `graph` is a
-    torch.cuda.CUDAGraph captured with keep_graph=True (kept referenced here: its nodes own the kernel arguments);
-    launch() re-issues every node from C++ on the executor's streams, forked from and joined into the current
-    stream.  `side`: a Streams whose side streams the executor issues on (the eager step's, so the hardware-queue
-    mapping is the same), else up to `n_side` streams of its own."""
-
-    def __init__(self, graph, side=None, n_side=2):
-        self.graph = graph
-        h = ctypes.c_void_p()
-        arr = None
-        if side is not None:
-            n_side = len(side._raw)
-            arr = (ctypes.c_void_p * n_side)(*[r.value for r in side._raw])
-            self._side = side  # keep the streams alive
-        _lib.call("gmr_graph_exec_create", ctypes.c_void_p(graph.raw_cuda_graph()), int(n_side), arr, ctypes.byref(h))
-        self.handle = h
-
-    def info(self):
-        v = [ctypes.c_int64() for _ in range(4)]
-        _lib.call("gmr_graph_exec_info", self.handle, *[ctypes.byref(x) for x in v])
-        return dict(zip(("nodes", "kernels", "streams", "cross_edges"), (x.value for x in v)))
-
-    def launch(self):
-        _lib.call("gmr_graph_exec_launch", self.handle, stream())
-
-    def __del__(self):
-        h = getattr(self, "handle", None)
-        if h is not None and h.value:
-            try:
-                _lib.load().gmr_graph_exec_destroy(h)
-            except Exception:  # interpreter shutdown
-                pass
-
-
 def score_f16(a, b, out):
     """out = fp16(a) @ fp16(b)^T with fp32 accumulation (gmr_score_f16; a: E x 64, b: I x 64)."""
     E, d = a.shape

@@ -29,9 +29,6 @@ from .utils import dict2str, early_stopping
 # full-rank eval through the fused score -> mask -> top-k kernel (gmr_score_topk_f32); GMR_EVAL_FUSED=0
 # keeps the score GEMM + mask + radix top-k over an E x I buffer (A/B)
 FUSED_EVAL = os.environ.get("GMR_EVAL_FUSED", "1") != "0"
-# graphed BPR steps (GMR_GRAPHS=1) re-issue the captured step through the native multi-stream executor
-# (K.GraphExec, csrc/graph_exec.hip, on the model's own side streams) unless GMR_GRAPH_EXEC=0 (then hipGraphLaunch)
-GRAPH_EXEC = os.environ.get("GMR_GRAPH_EXEC", "1") != "0"
 # DiffMM diffusion phase, one process: each denoiser's chain of steps and Adam updates runs on its own stream
 # with one join after the phase (GMR_INDEP_DENOISERS=0: join after every step, Adam on the main stream).
 # Diffusion phase 22.6 -> 22.0-22.8 ms, epoch 68.3 -> 67.9 ms averaged over three pairs (within the box's
@@ -228,20 +225,12 @@ class Trainer:
             def body():
                 loss = self.model.rec_step(*static, norm_rows=norm, reg_share=share)
                 _lib.call("gmr_sum_f32", 1, ptr(loss.view(1)), 1.0, ptr(acc), 1, stream())
-            g = capture_graph(body, keep_graph=True)
-            runner = None
-            if GRAPH_EXEC:  # the native multi-stream executor (csrc/graph_exec.hip); else hipGraphLaunch
-                runner = K.GraphExec(g, side=getattr(self.model, "_streams", None))
-            else:
-                g.instantiate()
-            self._graph = (key, g, static, runner)
-        _, g, static, runner = self._graph
+            g = capture_graph(body)
+            self._graph = (key, g, static)
+        _, g, static = self._graph
         for dst, src in zip(static, (u, p, ng, pb, pc)):
             dst.copy_(src)
-        if runner is not None:
-            runner.launch()
-        else:
-            g.replay()
+        g.replay()
 
     def _generate_train_loss_output(self, epoch_idx, s_time, e_time, losses):
         out = "epoch %d training [time: %.2fs, " % (epoch_idx, e_time - s_time)

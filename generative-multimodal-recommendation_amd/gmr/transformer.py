@@ -31,11 +31,8 @@ def _round4(n):
     return (n + 3) // 4 * 4
 
 
-# GMR_DEC_FUSED=1 (opt-in): run the decoder stack as one launch (gmr_decoder_fwd_f32, csrc/decoder.hip) when
-# d_model = 512 and nhead = 8.  Default 0, layer by layer: at the GenRecV1 batch (2,048 rows) the fused stack
-# fills 64 of 256 CUs and re-streams every weight plane per 32-row block, 1.49 ms per call vs ~0.7 ms for the
-# tiled GEMMs + row kernels (epoch 165 vs 121 ms, profiles/r04s_genrecv1_ab.txt)
-DEC_FUSED = os.environ.get("GMR_DEC_FUSED", "0") != "0"
+# (round 4's one-launch decoder stack, GMR_DEC_FUSED, lost to the layer-by-layer path at the 2,048-row batch -
+# 1.49 ms per call vs ~0.7 ms, epoch 165 vs 121 ms, profiles/r04s_genrecv1_ab.txt - and was removed in round 6)
 # the layer-by-layer decoder issued from C++ (gmr_decoder_layers_fwd_f32, csrc/decoder_host.hip): the same kernels
 # and arguments as the Python loop below (bit-identical), without its ~7 us of Python per launch; GMR_DEC_NATIVE=0
 # keeps the Python loop (A/B, and the path that takes injected masks)
@@ -88,19 +85,6 @@ class TransformerDenoiser:
         self.layer_stride = (o["transformer_decoder_layers_1_linear1_weight"] - o["transformer_decoder_layers_0_linear1_weight"]
                              if num_layers > 1 else 0)
         self._cache = None  # (T, train_drop, keep) of the time tables / cross-attention tables held
-        # fused decoder stack (gmr_decoder_*): layer 0's slab offsets of its four weights and eleven vectors
-        self._dec_ok = D == 512 and nhead == 8
-        self._dec_planes = None
-        self._planes_ok = False
-        if self._dec_ok:
-            p0 = "transformer_decoder_layers_0_"
-            self._dec_w = (ctypes.c_int64 * 4)(o[p0 + "self_attn_in_proj_weight"] + 2 * D * D,
-                                               o[p0 + "self_attn_out_proj_weight"], o[p0 + "linear1_weight"],
-                                               o[p0 + "linear2_weight"])
-            self._dec_v = (ctypes.c_int64 * 11)(*[o[p0 + n] + (2 * D if n.endswith("in_proj_bias") else 0) for n in (
-                "self_attn_in_proj_bias", "self_attn_out_proj_bias", "norm1_weight", "norm1_bias",
-                "multihead_attn_out_proj_bias", "norm2_weight", "norm2_bias", "linear1_bias", "linear2_bias",
-                "norm3_weight", "norm3_bias")])
         # layer 0's slab offsets for gmr_decoder_layers_fwd_f32 (value rows / bias of in_proj: + 2 D)
         p0 = "transformer_decoder_layers_0_"
         self._lay_off = (ctypes.c_int64 * len(_DEC_OFFSETS))(*[
@@ -118,7 +102,7 @@ class TransformerDenoiser:
         table caches: a forward issued on another stream beside this one's work (GenRecV1's value-only
         p_sample beside the training backward, the rebuild chunks) touches none of this one's buffers."""
         t = copy.copy(self)
-        t._ws, t._cache, t._lay_bufs, t._dec_planes, t._planes_ok, t._last = None, None, None, None, False, None
+        t._ws, t._cache, t._lay_bufs, t._last = None, None, None, None
         return t
 
     # ------------------------------------------------------------------ parameters
@@ -202,22 +186,18 @@ class TransformerDenoiser:
         row0 + r, so a data-parallel rank draws what one process holding the whole batch draws) unless
         `masks` gives them ({'a','c','1','2','3','f'} -> uint8 (L, B, ...)); returns out (B x I).
         reuse_tables: the weights are the previous forward's (p_sample steps after the first): the time
-        tables and the cross-attention tables of the same T and mode are kept.  The decoder stack runs
-        fused (GMR_DEC_FUSED, d_model 512, no injected masks); keep_acts=False (no backward follows: the
-        p_sample steps) stores only its last layer's rows."""
+        tables and the cross-attention tables of the same T and mode are kept.  keep_acts is accepted for the
+        callers of the removed fused stack (every layer's activations are kept)."""
         B = x.shape[0]
         w = self._work(B)
         D, I, L, H2 = self.D, self.I, self.L, self.H2
         train_drop = self.training and self.p > 0.0
         keep = 1.0 - self.p
-        fused = DEC_FUSED and self._dec_ok and masks is None
-        mode = (T, train_drop, keep, fused)
+        mode = (T, train_drop, keep)
         reuse = reuse_tables and self._cache == mode
-        if not reuse:
-            self._planes_ok = False  # the weights may have changed since the planes were split
         te, ste, TB, S = self._tables(T, reuse)
         self._T = T
-        if (train_drop or fused) and not reuse:  # cross-attention head tables of the L layers (gmr_xattn_table_f32)
+        if train_drop and not reuse:  # cross-attention head tables of the L layers (gmr_xattn_table_f32)
             p0 = "transformer_decoder_layers_0_"
             _lib.call("gmr_xattn_table_f32", L, D, self.nhead, ptr(self.v(p0 + "multihead_attn_out_proj_weight")),
                       ptr(self.v(p0 + "multihead_attn_in_proj_bias")[2 * D:]), self.layer_stride,
@@ -232,12 +212,10 @@ class TransformerDenoiser:
         h = w["h"][0, :B]
         _lib.call("gmr_adaln_fwd", B, D, ptr(h0), D, ptr(t_rows), -1 if t_rows is not None else int(t_const), ptr(S),
                   2 * D, ptr(h), D, stream())
-        native = DEC_NATIVE and not fused and masks is None
-        if fused:
-            h = self._decoder_fused(w, B, h, train_drop, keep, seed, step, row0, keep_acts)
-        elif native:
+        native = DEC_NATIVE and masks is None
+        if native:
             h = self._decoder_native(w, B, train_drop, keep, seed, step, row0, reuse)
-        for l in range(L if not (fused or native) else 0):
+        for l in range(L if not native else 0):
             p = f"transformer_decoder_layers_{l}_"
             wv = self.v(p + "self_attn_in_proj_weight")[2 * D:]
             bv = self.v(p + "self_attn_in_proj_bias")[2 * D:]
@@ -300,35 +278,6 @@ class TransformerDenoiser:
                bias=self.v("output_proj_3_bias"))
         self._last = (B, x, t_rows, t_const, train_drop, keep)
         self._cache = mode
-        return out
-
-    def _decoder_fused(self, w, B, h, train_drop, keep, seed, step, row0, keep_acts):
-        """The L decoder layers in one launch (gmr_decoder_fwd_f32): rows h (B x D) -> w['h'][L]; the weights'
-        bf16 planes split once per weight version, the dropout masks drawn with the layer-by-layer path's
-        keys into the same mask buffers; keep_acts: the activations the backward reads go to the same
-        workspace tensors the layer-by-layer forward fills."""
-        D, L, nh = self.D, self.L, self.nhead
-        if self._dec_planes is None:
-            self._dec_planes = torch.empty(L * 12 * D * D, dtype=torch.int16, device=self.device)
-        if not self._planes_ok:
-            _lib.call("gmr_decoder_split_f32", L, D, ptr(self.slab.data), ctypes.cast(self._dec_w, ctypes.c_void_p),
-                      self.layer_stride, ptr(self._dec_planes), stream())
-            self._planes_ok = True
-        ma, mc, m1, m2, m3, mf = (w["mask_" + k] for k in ("a", "c", "1", "2", "3", "f"))
-        if train_drop:
-            _lib.call("gmr_decoder_masks_u8", B, L, D, nh, keep, seed, step, int(row0), ptr(ma), ptr(mc), ma.stride(0),
-                      ptr(m1), ptr(m2), ptr(m3), ptr(mf), m1.stride(0), stream())
-        out = w["h"][L, :B]
-        acts = None
-        if keep_acts:
-            bufs = [w["h"], w["SAin"] if train_drop else w["V"], w["s1"], w["s2"], w["h2"], w["F1"], w["s3"], w["m1"],
-                    w["m2"], w["m3"]]
-            acts = (ctypes.c_void_p * 10)(*[t.data_ptr() for t in bufs])
-        _lib.call("gmr_decoder_fwd_f32", B, L, D, nh, ptr(h), K._ld(h), ptr(out), K._ld(out), ptr(self.slab.data),
-                  ctypes.cast(self._dec_v, ctypes.c_void_p), self.layer_stride, ptr(self._dec_planes), ptr(w["xP"]),
-                  keep, int(train_drop), ptr(ma), ptr(mc), ma.stride(0), ptr(m1), ptr(m2), ptr(m3), ptr(mf),
-                  m1.stride(0), ctypes.cast(acts, ctypes.c_void_p) if acts is not None else None, D, w["h"].stride(0),
-                  w["B"], stream())
         return out
 
     def _decoder_native(self, w, B, train_drop, keep, seed, step, row0, reuse):

@@ -702,33 +702,8 @@ int64_t gmr_xattn_bwd_workspace_floats(int64_t rows, int32_t D, int32_t nhead);
 int gmr_xattn_bwd_f32(int64_t rows, int32_t D, int32_t nhead, const float* dCA, int64_t ld, const uint8_t* mask,
                       int64_t ldm, const float* wo, const float* bv, float p_keep, float* g_wo, float* g_bv, float* ws,
                       int64_t ws_floats, void* stream);
-/* GenRecV1's decoder stack in one launch (csrc/decoder.hip; models/genrecv1.py:650-710 via
- * nn.TransformerDecoder on a length-1 target and a zero memory), d_model 512, 8 heads: per 16-row
- * workgroup the L layers' four products (split-bf16 matrix cores, fp32-accurate), LayerNorms, residual
- * adds, dropouts and the cross-attention mixture, rows kept in LDS; writes the last layer's rows only
- * (the p_sample forwards: no activations kept for a backward).  gmr_decoder_split_f32 splits the layers'
- * Wv (in_proj rows 2D..3D), Wo, W1, W2 (slab offsets w_offsets[0..3] of layer 0, layer_stride floats
- * apart) into bf16 planes [L][4][3][D][D]; gmr_decoder_masks_u8 draws the six dropout masks of the L
- * layers with gmr_dropout_f32 / gmr_keep_mask_u8's Philox keys (sites a c 1 2 3 f, step ((step * 64 +
- * l) * 8 + site) mod 2^48, counter (row0 + r) * width + index); gmr_decoder_fwd_f32 takes the slab
- * offsets of layer 0's bv, bo, norm1 w/b, cross-attention b_o, norm2 w/b, b1, b2, norm3 w/b (11), the
- * planes, the cross-attention head table (gmr_xattn_table_f32 with p_keep in train mode, 1 in eval mode,
- * where every head is kept) and in train mode the masks.  acts (NULL: only `out`, the last layer's rows)
- * = ten device pointers for a backward: layer inputs [L+1] (the last is `out`), SAin (V without
- * dropout), s1, s2, h2, F1, s3 ([L] x act_stride floats, rows of act_ld = 512) and the LayerNorm
- * statistics of LN1..3 ([L][3][stat_rows]: mean row 0, rstd row 1). */
-int gmr_decoder_split_f32(int32_t L, int32_t D, const float* slab, const int64_t* w_offsets, int64_t layer_stride,
-                          uint16_t* planes, void* stream);
-int gmr_decoder_masks_u8(int64_t B, int32_t L, int32_t D, int32_t nhead, float p_keep, uint64_t seed, uint64_t step,
-                         int64_t row0, uint8_t* mask_a, uint8_t* mask_c, int64_t msh, uint8_t* mask_1, uint8_t* mask_2,
-                         uint8_t* mask_3, uint8_t* mask_f, int64_t msd, void* stream);
-int gmr_decoder_fwd_f32(int64_t B, int32_t L, int32_t D, int32_t nhead, const float* h0, int64_t ld0, float* out,
-                        int64_t ldo, const float* slab, const int64_t* offsets, int64_t layer_stride,
-                        const uint16_t* planes, const float* xattn_table, float p_keep, int32_t train,
-                        const uint8_t* mask_a, const uint8_t* mask_c, int64_t msh,
-                        const uint8_t* mask_1, const uint8_t* mask_2, const uint8_t* mask_3, const uint8_t* mask_f,
-                        int64_t msd, float* const* acts, int64_t act_ld, int64_t act_stride, int64_t stat_rows,
-                        void* stream);
+/* (Round 4's one-launch decoder stack, gmr_decoder_fwd_f32 / _masks_u8 / _split_f32, was removed in round 6:
+ * opt-in, slower than the layer-by-layer path at the GenRecV1 batch in every round it was measured.) */
 /* The same L decoder layers layer by layer, issued from C++ (csrc/decoder_host.hip, round 5): the kernels and
  * arguments of gmr/transformer.py's Python layer loop (gmr_gemm_f32 NT products with `tile`, gmr_dropout_f32,
  * gmr_layernorm_[drop_]fwd, gmr_xattn_fwd_f32 in train mode; the constant cross-attention row cav = b_v' Wo^T +
@@ -753,16 +728,9 @@ int gmr_adam_f32(int64_t n, float* param, const float* grad, float* exp_avg, flo
                  float beta2, float eps, float weight_decay, float step_size, float bias_correction2_sqrt,
                  void* stream);
 
-/* ---------------------------------------------------------------- native graph executor (round 5)
- * A captured HIP graph (the BPR rec step, common/trainer.py:144-208; csrc/graph_exec.hip) re-issued from C++ on
- * the launch stream plus up to n_side side streams (the caller's `side_streams[0..n_side)`, or the executor's
- * own when that is NULL): kernel / memset / memcpy / empty nodes in a topological order, each node on the stream
- * of a predecessor it continues, cross-stream edges as events; the side streams fork from and join back into
- * the launch `stream`.  The graph must outlive the executor (its nodes own the kernel argument blocks). */
-int gmr_graph_exec_create(void* graph, int32_t n_side, void* const* side_streams, void** exec_out);
-int gmr_graph_exec_info(const void* exec, int64_t* nodes, int64_t* kernels, int64_t* streams, int64_t* cross_edges);
-int gmr_graph_exec_launch(void* exec, void* stream);
-int gmr_graph_exec_destroy(void* exec);
+/* (Round 5's native executor of a captured HIP graph, gmr_graph_exec_*, was removed in round 6: its replayed
+ * step ran slower on the GPU than eager issue; the host tape of gmr/tape.py removes the Python issue cost and
+ * keeps the eager streams and order.) */
 
 #ifdef __cplusplus
 }

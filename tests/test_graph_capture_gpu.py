@@ -44,38 +44,6 @@ def test_captured_rec_step_replays_eager(golden):
     assert torch.equal(m.rec_slab.grad.view(torch.int32), grad_e.view(torch.int32))
 
 
-@pytest.mark.parametrize("streams", [0, 1, 3, "model"])
-def test_graph_executor_replays_eager(golden, streams):
-    """The native executor (gmr_graph_exec_*, csrc/graph_exec.hip) re-issues the captured step from C++ on the
-    launch stream plus side streams: loss and gradients equal the eager step's bit for bit with 0, 1 and 3 side
-    streams of its own and with the model's two side streams, and repeated launches stay identical."""
-    from gmr import kernels as K
-    g = golden("diffmm_tiny")
-    m = build_model(g)
-    b0, b1 = _batch(g, 0), _batch(g, 5)
-    pl0, pl1 = m._plans(*b0), m._plans(*b1)
-    loss_e = m.rec_step(*b1, *pl1).clone()
-    grad_e = m.rec_slab.grad.clone()
-    static = [t.clone() for t in (*b0, *pl0)]
-    m.rec_step(*static)
-    torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph(keep_graph=True)
-    with torch.cuda.graph(graph):
-        loss_g = m.rec_step(*static)
-    ex = K.GraphExec(graph, side=m._streams) if streams == "model" else K.GraphExec(graph, n_side=streams)
-    info = ex.info()
-    n_side = 2 if streams == "model" else streams
-    assert info["kernels"] >= 30 and 1 <= info["streams"] <= 1 + n_side, info
-    for dst, src in zip(static, (*b1, *pl1)):
-        dst.copy_(src)
-    for _ in range(3):
-        m.rec_slab.gview("E0").fill_(float("nan"))  # every launch rewrites the whole gradient
-        ex.launch()
-        torch.cuda.synchronize()
-        assert torch.equal(loss_g.view(torch.int32), loss_e.view(torch.int32))
-        assert torch.equal(m.rec_slab.grad.view(torch.int32), grad_e.view(torch.int32))
-
-
 def test_trainer_epoch_with_graphs_matches_eager(golden, monkeypatch):
     from gmr.dataloader import TrainDataLoader
     from gmr.dataset import RecDataset
