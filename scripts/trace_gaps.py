@@ -20,9 +20,9 @@ def main():
             name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name[:70], r.get("Queue_Id", "")))
     rows.sort()
-    bpr = [i for i, r in enumerate(rows) if "bpr_kernel" in r[2]]
+    bpr = [i for i, r in enumerate(rows) if "bpr_kernel" in r[2] or "bpr_sqnorm_kernel" in r[2]]
     # step k = from its bpr_kernel back to the previous step's adam_kernel (exclusive)
-    adam = [i for i, r in enumerate(rows) if "adam_kernel" in r[2]]
+    adam = [i for i, r in enumerate(rows) if "adam_kernel" in r[2] or "adam4_kernel" in r[2]]
     ends = []
     for b in bpr:
         nxt = [j for j in adam if j > b]
