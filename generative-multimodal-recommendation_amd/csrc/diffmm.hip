@@ -967,6 +967,15 @@ __device__ __forceinline__ void cl_load(float4 (&st)[2], const float* __restrict
     st[q] = r0 + r < r_end ? ld4(src + (int64_t)(r0 + r) * ld + c4) : f4(0.f, 0.f, 0.f, 0.f);
   }
 }
+// the same with row r of the block read from src row idx[r0 + r] + off (a gathered operand, read in place)
+__device__ __forceinline__ void cl_load_idx(float4 (&st)[2], const float* __restrict__ src, int64_t ld, int r0,
+                                            int r_end, const int* __restrict__ idx, int64_t off) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int id = threadIdx.x + 256 * q, r = id >> 4, c4 = (id & 15) * 4;
+    st[q] = r0 + r < r_end ? ld4(src + ((int64_t)idx[r0 + r] + off) * ld + c4) : f4(0.f, 0.f, 0.f, 0.f);
+  }
+}
 __device__ __forceinline__ void cl_store(const float4 (&st)[2], float* dst) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -1271,6 +1280,18 @@ __device__ __forceinline__ void c6_split8(const float (&v)[8], c6bf8 (&o)[3]) {
   }
 }
 
+// Y products (E T over the staged block) keep three of the six: hi*hi + hi*mid + mid*hi.  The dropped terms are
+// each <= 2^-18 |e t| (round-to-nearest splits: |mid| <= 2^-9 |x|, |lo| <= 2^-18 |x|), so a Y row is fp32-grade
+// (<= 1.2e-5 of sum |e t| worst case) for the gradients it feeds (dP, dT: the parity tests' 1e-4 bars); the
+// logits S, which feed exp and the loss rows (1e-5), keep all six (round 6: 48 -> 36 MFMAs per staged block)
+__device__ __forceinline__ void c6_split8_2(const float (&v)[8], c6bf8 (&o)[2]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 hh = (__bf16)__builtin_amdgcn_fmed3f(v[e], -0x1.fep127f, 0x1.fep127f);
+    o[0][e] = hh;
+    o[1][e] = (__bf16)(v[e] - (float)hh);
+  }
+}
 // fp32 block (32 x 64, stride kClLd) -> the three row-major and the three transposed bf16 planes
 __device__ __forceinline__ void c6_convert(const float* sf, __bf16* stg) {
   const int t = threadIdx.x;
@@ -1291,11 +1312,17 @@ __device__ __forceinline__ void c6_convert(const float* sf, __bf16* stg) {
     float v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = sf[(16 * (g >> 1) + 4 * (g & 1) + (q & 3) + 8 * (q >> 2)) * kClLd + d];
-    c6bf8 o[3];
-    c6_split8(v, o);
+    c6bf8 o[2];  // the Y products read the hi and mid planes only (c6_mfma3)
+    c6_split8_2(v, o);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) *reinterpret_cast<c6bf8*>(stg + 3 * kC6PA + p * kC6PB + d * kC6B + 8 * g) = o[p];
+    for (int p = 0; p < 2; ++p) *reinterpret_cast<c6bf8*>(stg + 3 * kC6PA + p * kC6PB + d * kC6B + 8 * g) = o[p];
   }
+}
+
+__device__ __forceinline__ clx16 c6_mfma3(const c6bf8 (&a)[2], const c6bf8 (&b)[2], clx16 c) {  // small terms first
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
 }
 
 __device__ __forceinline__ clx16 c6_mfma6(const c6bf8 (&a)[3], const c6bf8 (&b)[3], clx16 c) {  // small terms first
@@ -1423,15 +1450,15 @@ __global__ void __launch_bounds__(256, 2) cl6_kernel(int nf, int ns, const float
     for (int t2 = 0; t2 < 2; ++t2) {  // Y^T (64 d x 32) += Stg^T E^T, K = 32 staged rows in two steps
       const float evs[8] = {ev[8 * t2], ev[8 * t2 + 1], ev[8 * t2 + 2], ev[8 * t2 + 3],
                             ev[8 * t2 + 4], ev[8 * t2 + 5], ev[8 * t2 + 6], ev[8 * t2 + 7]};
-      c6bf8 eb[3], a0[3], a1[3];
-      c6_split8(evs, eb);
+      c6bf8 eb[2], a0[2], a1[2];
+      c6_split8_2(evs, eb);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < 2; ++p) {
         a0[p] = *reinterpret_cast<const c6bf8*>(Bt + p * kC6PB + l32 * kC6B + 8 * (2 * t2 + h));
         a1[p] = *reinterpret_cast<const c6bf8*>(Bt + p * kC6PB + (32 + l32) * kC6B + 8 * (2 * t2 + h));
       }
-      y0 = c6_mfma6(a0, eb, y0);
-      y1 = c6_mfma6(a1, eb, y1);
+      y0 = c6_mfma3(a0, eb, y0);
+      y1 = c6_mfma3(a1, eb, y1);
     }
     if (more) {  // s_f's last reader (the convert) finished before the previous barrier
       cl_store(st, s_f);
@@ -1455,12 +1482,16 @@ __global__ void __launch_bounds__(256, 2) cl6_kernel(int nf, int ns, const float
 // this block's logits, instead of each wave alternating MFMA-only and VALU-only phases.  Both staged
 // blocks are in LDS by then (block j + 2 is staged into block j's buffer after its Y product), so the
 // staging, the chunking and every sum are those of cl6_kernel: bit-identical results.
+// gidx (optional): the batch operand is read in place through the node index - the fragment rows F[gidx[f] +
+// goff] in the rows pass (!TABLE), the staged rows Stg[gidx[j] + goff] in the table pass - instead of from a
+// gathered copy (round 6: the two gather launches of the rec step; the same values, bit-identical sums)
 template <bool FAST, bool TABLE>
 __global__ void __launch_bounds__(256, 2) cl6p_kernel(int nf, int ns, const float* __restrict__ F, int64_t ldf,
                                                       const float* __restrict__ Stg, int64_t lds,
                                                       const float* __restrict__ w, float inv_t, int chunk,
                                                       float* __restrict__ part_y, float* __restrict__ part_z,
-                                                      int* __restrict__ cnt, float* __restrict__ dT, int64_t ld_dt) {
+                                                      int* __restrict__ cnt, float* __restrict__ dT, int64_t ld_dt,
+                                                      const int* __restrict__ gidx, int64_t goff) {
   __shared__ __attribute__((aligned(16))) __bf16 s_stg[2 * kC6Stage];
   __shared__ __attribute__((aligned(16))) float s_f[32 * kClLd];
   __shared__ float s_w[2][32];
@@ -1472,8 +1503,9 @@ __global__ void __launch_bounds__(256, 2) cl6p_kernel(int nf, int ns, const floa
   for (int k = 0; k < 4; ++k) {
     float4 a = f4(0.f, 0.f, 0.f, 0.f), b = a;
     if (f < nf) {
-      a = ld4(F + (int64_t)f * ldf + 16 * k + 8 * h);
-      b = ld4(F + (int64_t)f * ldf + 16 * k + 8 * h + 4);
+      const int64_t fr_row = !TABLE && gidx ? (int64_t)gidx[f] + goff : (int64_t)f;
+      a = ld4(F + fr_row * ldf + 16 * k + 8 * h);
+      b = ld4(F + fr_row * ldf + 16 * k + 8 * h + 4);
     }
     const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     c6_split8(v, fr[k]);
@@ -1494,7 +1526,10 @@ __global__ void __launch_bounds__(256, 2) cl6p_kernel(int nf, int ns, const floa
   auto stage = [&](int j, int buf) {  // block starting at row j -> s_stg[buf] (and its weights), two barriers
     float4 st[2];
     float sw = 0.f;
-    cl_load(st, Stg, lds, j, s1);
+    if (TABLE && gidx)
+      cl_load_idx(st, Stg, lds, j, s1, gidx, goff);
+    else
+      cl_load(st, Stg, lds, j, s1);
     if (TABLE && threadIdx.x < 32) sw = j + (int)threadIdx.x < s1 ? w[j + threadIdx.x] : 0.f;
     cl_store(st, s_f);
     __syncthreads();
@@ -1515,7 +1550,10 @@ __global__ void __launch_bounds__(256, 2) cl6p_kernel(int nf, int ns, const floa
   for (int j = s0; j < s1; j += 32) {
     const bool more = j + 32 < s1, refill = j + 64 < s1;
     if (refill) {  // block j + 2's rows travel while this block is computed
-      cl_load(st, Stg, lds, j + 64, s1);
+      if (TABLE && gidx)
+        cl_load_idx(st, Stg, lds, j + 64, s1, gidx, goff);
+      else
+        cl_load(st, Stg, lds, j + 64, s1);
       if (TABLE && threadIdx.x < 32) sw = j + 64 + (int)threadIdx.x < s1 ? w[j + 64 + threadIdx.x] : 0.f;
     }
     const __bf16* A = s_stg + cur * kC6Stage;
@@ -1538,15 +1576,15 @@ __global__ void __launch_bounds__(256, 2) cl6p_kernel(int nf, int ns, const floa
     for (int t2 = 0; t2 < 2; ++t2) {  // Y^T (64 d x 32) += Stg^T E^T, K = 32 staged rows in two steps
       const float evs[8] = {ev[8 * t2], ev[8 * t2 + 1], ev[8 * t2 + 2], ev[8 * t2 + 3],
                             ev[8 * t2 + 4], ev[8 * t2 + 5], ev[8 * t2 + 6], ev[8 * t2 + 7]};
-      c6bf8 eb[3], a0[3], a1[3];
-      c6_split8(evs, eb);
+      c6bf8 eb[2], a0[2], a1[2];
+      c6_split8_2(evs, eb);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < 2; ++p) {
         a0[p] = *reinterpret_cast<const c6bf8*>(Bt + p * kC6PB + l32 * kC6B + 8 * (2 * t2 + h));
         a1[p] = *reinterpret_cast<const c6bf8*>(Bt + p * kC6PB + (32 + l32) * kC6B + 8 * (2 * t2 + h));
       }
-      y0 = c6_mfma6(a0, eb, y0);
-      y1 = c6_mfma6(a1, eb, y1);
+      y0 = c6_mfma3(a0, eb, y0);
+      y1 = c6_mfma3(a1, eb, y1);
     }
     if (refill) {  // block j + 2 takes this block's buffer (s_f's last reader, a convert, finished before a barrier)
       cl_store(st, s_f);
@@ -1629,7 +1667,12 @@ int contrast_fused(const char* fn, int32_t B, int64_t n, const float* P, int64_t
                    float* contrib, int64_t ld_contrib, float* dT, int64_t ld_dt, float* workspace,
                    int64_t workspace_floats, const float* y2, int64_t ldy2, const float* nrm2, void* stream) {
   (void)fn;
+  // P == nullptr: the batch rows are read in place, P_i = CLN[node_off + nodes[i], 0:64] with ldp = CLN's leading
+  // dimension (the pipelined split-bf16 passes only)
+  const bool pin = P == nullptr;
+  if (pin) P = CLN;
   GMR_ARG(P && T && CLN && nodes && loss && contrib && dT && workspace, "null pointer");
+  GMR_ARG(!pin || (cl_x6() && cl_pipe()), "P = null (rows read through nodes) needs the pipelined split-bf16 passes");
   GMR_ARG(B > 0 && n > 0 && n < (1ll << 31), "bad size");
   GMR_ARG(ldp >= 64 && ldt >= 64 && ld_contrib >= 128 && ld_dt >= 64 && ldp % 4 == 0 && ldt % 4 == 0 &&
               ld_dt % 4 == 0,
@@ -1650,21 +1693,30 @@ int contrast_fused(const char* fn, int32_t B, int64_t n, const float* P, int64_t
   if (cl_x6()) {  // split-bf16 passes (128 fragment rows per workgroup)
     const dim3 ga((unsigned)((B + 127) / 128), (unsigned)p.nca), gb((unsigned)((n + 127) / 128), (unsigned)p.ncb);
     const bool pipe = cl_pipe();
-    auto rows6 = pipe ? (fast ? cl6p_kernel<true, false> : cl6p_kernel<false, false>)
-                      : (fast ? cl6_kernel<true, false> : cl6_kernel<false, false>);
-    auto table6 = pipe ? (fast ? cl6p_kernel<true, true> : cl6p_kernel<false, true>)
-                       : (fast ? cl6_kernel<true, true> : cl6_kernel<false, true>);
+    auto rows6 = fast ? cl6p_kernel<true, false> : cl6p_kernel<false, false>;
+    auto table6 = fast ? cl6p_kernel<true, true> : cl6p_kernel<false, true>;
+    auto rows6u = fast ? cl6_kernel<true, false> : cl6_kernel<false, false>;
+    auto table6u = fast ? cl6_kernel<true, true> : cl6_kernel<false, true>;
 
-    hipLaunchKernelGGL(rows6, ga, dim3(256), 0, st, B, (int)n, P, ldp, T, ldt, nullptr, inv_temp, p.chunk_a, part_u,
-                       part_z, nullptr, nullptr, 0);
+    const int* gi = pin ? nodes : nullptr;
+    if (pipe)
+      hipLaunchKernelGGL(rows6, ga, dim3(256), 0, st, B, (int)n, P, ldp, T, ldt, nullptr, inv_temp, p.chunk_a, part_u,
+                         part_z, nullptr, nullptr, 0, gi, node_off);
+    else
+      hipLaunchKernelGGL(rows6u, ga, dim3(256), 0, st, B, (int)n, P, ldp, T, ldt, nullptr, inv_temp, p.chunk_a, part_u,
+                         part_z, nullptr, nullptr, 0);
     GMR_LAUNCHED();
     hipLaunchKernelGGL(cl_finalize_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, p.nca, part_u, part_z,
                        CLN, nodes, node_off, inv_temp, coef, loss, contrib, ld_contrib, r);
     GMR_LAUNCHED();
     // the table pass reduces its own partials (last block per tile) when its tiles fit the counters
     const bool fix = cl_fixup() && gb.x <= (unsigned)kClCounters && !y2;
-    hipLaunchKernelGGL(table6, gb, dim3(256), 0, st, (int)n, B, T, ldt, P, ldp, r, inv_temp, p.chunk_b, part_t,
-                       nullptr, fix ? counters : nullptr, dT, ld_dt);
+    if (pipe)
+      hipLaunchKernelGGL(table6, gb, dim3(256), 0, st, (int)n, B, T, ldt, P, ldp, r, inv_temp, p.chunk_b, part_t,
+                         nullptr, fix ? counters : nullptr, dT, ld_dt, gi, node_off);
+    else
+      hipLaunchKernelGGL(table6u, gb, dim3(256), 0, st, (int)n, B, T, ldt, P, ldp, r, inv_temp, p.chunk_b, part_t,
+                         nullptr, fix ? counters : nullptr, dT, ld_dt);
     GMR_LAUNCHED();
     if (!fix && y2) {
       hipLaunchKernelGGL(cl_table_reduce_nbwd_kernel, dim3(gmr::grid_for(n * 16, 256)), dim3(256), 0, st, (int)n,

@@ -266,13 +266,21 @@ __global__ void __launch_bounds__(64 * WGM * WGN, OCC) gemm_x6_kernel(int64_t M,
   const int wm = w / WGN, wn = w % WGN;
   const int h = lane >> 5, l32 = lane & 31;
 
-  floatx16 acc[TM][TN];
+  // Two accumulators per output tile (round 6): hi * hi alone into acc, the five small products into sml, added
+  // once after the k loop.  The bf16 MFMA's fp32 accumulation is not unbiased when it adds products far below
+  // the accumulator (it rounds toward -inf by ~0.03 ulp per x6 k step, both signs of the result alike:
+  // scripts/micro/mfma_round.hip, profiles/r06j_mfma_rounding.txt); with the small products summed apart, at
+  // 2^-8 of the magnitude, that bias shrinks 13x on one-sign sums (-0.185 -> -0.014 ulp of scale over 64 steps)
+  // and the mean |error| halves (the gc term's Z = out @ feats sums the denoiser output's errors over 7,050 items,
+  // where a bias adds up linearly: gc rows 1.1e-5 -> 1.5e-6 off fp64 at baby, profiles/r06j_*).  Cost: +4-7 % on
+  // the p_sample products (the 128^2 three-blocks-per-CU tile no longer fits its registers), ~1 ms per epoch.
+  floatx16 acc[TM][TN], sml[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = sml[i][j][e] = 0.f;
 
   // one 16-deep MFMA step s (k = 16 s + 8 h + j: chunk 2 s + h of the 32-deep rows) of a stage
   auto mstep = [&](const __bf16* a_s, int s) {
@@ -294,11 +302,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN, OCC) gemm_x6_kernel(int64_t M,
       for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(a_s + p * APL + off);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {  // small terms first
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0][j], acc[i][j], 0, 0, 0);
+        sml[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1][j], sml[i][j], 0, 0, 0);
+        sml[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2][j], sml[i][j], 0, 0, 0);
+        sml[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0][j], sml[i][j], 0, 0, 0);
+        sml[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1][j], sml[i][j], 0, 0, 0);
+        sml[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0][j], sml[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0][j], acc[i][j], 0, 0, 0);
       }
     }
@@ -445,6 +453,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN, OCC) gemm_x6_kernel(int64_t M,
     }
   }
 
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] += sml[i][j];
+
   // epilogues that read an aux / C element per output leave through LDS as float4 row chunks (coalesced
   // C / aux traffic: the p_sample posterior product 870 -> 726 us at 8192 rows); the others store the
   // accumulator fragments directly (the row passes of the LDS epilogue cost the bias-only products)
@@ -565,11 +578,12 @@ int x6_launch(int bm, int bn, dim3 grid, hipStream_t st, int64_t M, int64_t N, i
   if (bm == 256 && bn == 128) GMR_X6(256, 128, 4, 2, 2, 1)
   if (bm == 128 && bn == 256) GMR_X6(128, 256, 2, 4, 2, 1)
   if (bm == 128 && bn == 128) {
-    // three blocks per CU (168 VGPRs) when the grid fills them: the 19445-row p_sample products -4..-8 %;
-    // two below that (the 448-tile weight gradients +4 % at three; profiles/r02x6_study.txt)
+    // two blocks per CU.  (Three (168 VGPRs) won 4-8 % on the 19445-row p_sample products with one accumulator
+    // set (profiles/r02x6_study.txt); with the two sets of round 6 it spills 392 bytes per lane, so it is
+    // opt-in, GMR_GEMM_X6_NB128 = 3.)
     const int nb = x6_nb128();
     if (nb == 2) GMR_X6(128, 128, 2, 2, 2, 1)
-    if (nb == 3 || (nb == 0 && (int64_t)grid.x * grid.z >= 768)) GMR_X6(128, 128, 2, 2, 1, 3)
+    if (nb == 3) GMR_X6(128, 128, 2, 2, 1, 3)
     GMR_X6(128, 128, 2, 2, 1, 2)
   }
 #undef GMR_X6

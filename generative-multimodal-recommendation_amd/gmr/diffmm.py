@@ -85,6 +85,12 @@ class _RecLoss(torch.autograd.Function):
         return (None, None, None, None, *grads)
 
 
+def _cl_rows_in_place():
+    """The InfoNCE passes read the batch rows through the node index (P = null, gmr_contrast_fused_nbwd_f32) on
+    their default pipelined split-bf16 form; the opt-in forms (GMR_CL_PIPE=0, GMR_CL_X6=0) take a gathered copy."""
+    return os.environ.get("GMR_CL_PIPE", "1") != "0" and os.environ.get("GMR_CL_X6", "1") != "0"
+
+
 class DiffMM(GeneralRecommender):
     REC_PARAMS = ("uEmbeds", "iEmbeds", "image_trans", "text_trans", "modal_weight")
     # rec_step is a fixed sequence of C-ABI calls for a given batch shape and graph set (no per-step draws or
@@ -287,13 +293,17 @@ class DiffMM(GeneralRecommender):
         (contrastLoss, diffmm.py:251-258): one fused MFMA pass over the table for the loss rows and
         dP, one for the dense table gradient, which leaves through the normalize backward of view 2 into
         dK[:, 64:] (gmr_contrast_fused_nbwd_f32) - no B x n logits in HBM."""
-        CLN, P1 = w["CLN"], w["P1_" + slot][:B]
-        K.gather_rows(CLN[:, :64], nodes, P1, off=off)
+        CLN = w["CLN"]
+        if _cl_rows_in_place():  # the passes read P_i = CLN[off + nodes[i], :64] through the index
+            P1, ldp = None, 128
+        else:
+            P1, ldp = w["P1_" + slot][:B], 64
+            K.gather_rows(CLN[:, :64], nodes, P1, off=off)
         contrib = w["contrib_cl"][slot0:slot0 + B]
         ws = K.contrast_workspace(B, n_table, self.device, "cl_" + slot)
         T, dT = CLN[off:off + n_table, 64:], w["dCLN"][off:off + n_table, 64:]
         with K._Probe("infonce", (B, n_table)):
-            _lib.call("gmr_contrast_fused_nbwd_f32", B, n_table, ptr(P1), 64, ptr(T), 128, ptr(CLN), ptr(nodes), off,
+            _lib.call("gmr_contrast_fused_nbwd_f32", B, n_table, ptr(P1), ldp, ptr(T), 128, ptr(CLN), ptr(nodes), off,
                       1.0 / self.temp, self.ssl_reg / norm, ptr(loss_out), ptr(contrib), 128, ptr(dT), 128, ptr(T), 128,
                       ptr(w["nrmCL"][1][off:off + n_table]), ptr(ws), ws.numel(), stream())
 

@@ -729,10 +729,12 @@ def contrast_workspace(B, n, device, tag):
 
 def contrast_fused(P, T, CLN, nodes, node_off, inv_temp, coef, loss, contrib, dT, ws):
     """K8 fused InfoNCE (include/gmr.h gmr_contrast_fused_f32): loss rows, dP rows into contrib and
-    the dense table gradient dT, without the B x n logits."""
-    B, n = P.shape[0], T.shape[0]
+    the dense table gradient dT, without the B x n logits.  P = None: the batch rows are read in place,
+    P_i = CLN[node_off + nodes[i], :64] (the pipelined split-bf16 passes only)."""
+    B, n = (P.shape[0] if P is not None else nodes.numel()), T.shape[0]
     with _Probe("infonce", (B, n)):
-        _lib.call("gmr_contrast_fused_f32", B, n, ptr(P), _ld(P), ptr(T), _ld(T), ptr(CLN), ptr(nodes), node_off,
+        _lib.call("gmr_contrast_fused_f32", B, n, ptr(P), _ld(P) if P is not None else _ld(CLN), ptr(T), _ld(T),
+                  ptr(CLN), ptr(nodes), node_off,
                   float(inv_temp), float(coef), ptr(loss), ptr(contrib), _ld(contrib), ptr(dT), _ld(dT), ptr(ws),
                   ws.numel(), stream())
 

@@ -349,6 +349,8 @@ int gmr_contrast_rows(int32_t B, const float* CLN, const int32_t* nodes, int64_t
  * <P_i,T_node(i)>/temp; contrib[i, 0:64] = dL/dP_i and contrib[i, 64:128] = -coef/temp P_i (the
  * T_node(i) term, for the caller's scatter); dT (n x 64, ld_dt, overwritten) = the dense table
  * gradient; gradients scaled by coef.  No B x n matrix in HBM; f32 MFMA; deterministic.
+ * P = NULL (round 6): the passes read P_i = CLN[node_off + nodes[i], 0:64] in place, ldp = CLN's leading
+ * dimension (no gathered copy; the default pipelined split-bf16 passes only, else an argument error).
  * workspace: gmr_contrast_workspace_floats(B, n) floats. */
 int64_t gmr_contrast_workspace_floats(int32_t B, int64_t n);
 int gmr_contrast_fused_f32(int32_t B, int64_t n, const float* P, int64_t ldp, const float* T, int64_t ldt,

@@ -8,6 +8,8 @@ python scripts/host_vs_gpu_probe.py [--steps 5]
 3. HIP events queued before and after those steps time them on the GPU once the blocker drains: with
    every launch already queued there are no host gaps, so that is the GPU-bound time per step.
 host cost > GPU time per step means the step is host-bound (the GPU idles between launches).
+--tape: the steps are replayed from a host tape recorded on the first batch (gmr/tape.py, the trainer's
+default issue path since round 6) instead of issued eagerly from Python.
 """
 import argparse
 import os
@@ -28,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--model", default="diffmm")
+    ap.add_argument("--tape", action="store_true")
     a = ap.parse_args()
     args = argparse.Namespace(model=a.model, shape="baby" if a.model != "genrecv1" else "tiktok", scoring_dtype=None)
     cfg, ds, tr, tl, vl, model, trainer = bench.setup(args)
@@ -35,6 +38,15 @@ def main():
     torch.cuda.synchronize()
     d = tl.epoch()
     batches = list(tl.batches(d))[:a.steps]
+    tape = None
+    if a.tape:
+        from gmr.tape import Tape
+        _, _, u, p, ng, pb, pc = batches[0]
+        acc = torch.zeros(1, device="cuda")
+        tape = Tape((u, p, ng, pb, pc))
+        with tape.recording():
+            model.rec_step(u, p, ng, pb, pc, acc=acc)
+        torch.cuda.synchronize()
     X = torch.randn(4096, 4096, device="cuda")
     Y = torch.empty_like(X)
 
@@ -57,13 +69,16 @@ def main():
         e0.record()
         t0 = time.perf_counter()
         for _, _, u, p, ng, pb, pc in batches:
-            model.rec_step(u, p, ng, pb, pc)
+            if tape is not None:
+                tape.replay((u, p, ng, pb, pc))
+            else:
+                model.rec_step(u, p, ng, pb, pc)
         t_host = time.perf_counter() - t0
         e1.record()
         pending = not e1.query()
         torch.cuda.synchronize()
         gpu_ms = e0.elapsed_time(e1)
-        print(f"rep {rep}: host issue {1e3 * t_host / len(batches):.3f} ms/step, GPU {gpu_ms / len(batches):.3f} "
+        print(f"{'tape' if tape is not None else 'eager'} rep {rep}: host issue {1e3 * t_host / len(batches):.3f} ms/step, GPU {gpu_ms / len(batches):.3f} "
               f"ms/step (blocker still running when the host finished: {pending})", flush=True)
 
 

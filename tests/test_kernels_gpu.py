@@ -495,6 +495,38 @@ def test_contrast_table_fixup_bit_exact(K, B, n, monkeypatch):
     _contrast_env_bit_exact(K, B, n, monkeypatch, "GMR_CL_FIXUP", repeats=3)
 
 
+@pytest.mark.parametrize("B,n", [(2048, 19445), (2048, 7050), (300, 1000), (37, 100), (64, 65)])
+def test_contrast_rows_in_place_bit_exact(K, B, n, monkeypatch):
+    """P = None (round 6): the passes read the batch rows CLN[off + nodes[i], :64] through the index instead of
+    a gathered copy - loss, dP and dT bit for bit (ragged B and n, an offset table, repeated nodes); the
+    unpipelined and fp32 forms refuse it."""
+    monkeypatch.setenv("GMR_CL_X6", "1")
+    monkeypatch.setenv("GMR_CL_PIPE", "1")
+    rng = _rng(14)
+    off = 7
+    C = rng.standard_normal((off + n + 5, 128)).astype(np.float32)
+    C /= np.linalg.norm(C, axis=1, keepdims=True)
+    nodes = rng.integers(0, n, B).astype(np.int32)
+    Cd, nd = _dev(C), _dev(nodes)
+    P = torch.empty((B, 64), device=DEV)
+    K.gather_rows(Cd[:, :64], nd, P, off=off)
+    ws = K.contrast_workspace(B, n, DEV, "test_cl_inplace")
+    outs = []
+    for p in (P, None):
+        loss = torch.empty(B, device=DEV)
+        contrib = torch.empty((B, 128), device=DEV)
+        dt = torch.empty((n, 128), device=DEV)
+        K.contrast_fused(p, Cd[off:off + n, 64:], Cd, nd, off, 1.0 / 0.2, 0.01 / B, loss, contrib, dt[:, 64:], ws)
+        outs.append((loss.cpu(), contrib.cpu(), dt[:, 64:].cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    for env in ("GMR_CL_PIPE", "GMR_CL_X6"):
+        monkeypatch.setenv(env, "0")
+        with pytest.raises(RuntimeError, match="pipelined"):
+            K.contrast_fused(None, Cd[off:off + n, 64:], Cd, nd, off, 5.0, 0.01 / B, loss, contrib, dt[:, 64:], ws)
+        monkeypatch.setenv(env, "1")
+
+
 def _contrast_env_bit_exact(K, B, n, monkeypatch, env, repeats=1, value="1"):
     monkeypatch.setenv("GMR_CL_X6", "1")
     rng = _rng(13)
