@@ -181,6 +181,8 @@ def test_diffusion_step_own_feats_vs_reference(bt):
         diff, gc = diff.cpu().numpy(), gc.cpu().numpy()
         wd, wg = g[f"dif_{mod}_diff_rows"], g[f"dif_{mod}_gc_rows"]
         np.testing.assert_allclose(diff, wd, rtol=1e-5, atol=1e-9, err_msg=f"{mod} diffusion loss rows")
+        print(f"[{meta.get('shape', 'baby')} {mod}] own feats: gc rows vs the reference's fp32 run, max rel "
+              f"{np.max(np.abs(gc - wg) / np.abs(wg)):.3e}", flush=True)
         np.testing.assert_allclose(gc, wg, rtol=2e-5, atol=1e-9, err_msg=f"{mod} gc loss rows")
         np.testing.assert_allclose(gc.mean(), wg.mean(), rtol=1e-5, err_msg=f"{mod} gc loss mean")
         step_loss = diff.mean() + gc.mean() * m.e_loss
