@@ -14,6 +14,20 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 
 __device__ __forceinline__ float unit01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }  // [0, 1)
 
+// Draw mapping of the per-element Bernoulli kernels (round 6): the 32-bit word of draw unit g (a global index,
+// keyed by the GLOBAL row so any row split draws the same values) is word g % 4 of Philox(seed, step, g / 4) -
+// one Philox call per four units instead of one per unit (the draws were 14 % and 11 % of the GenRecV1 leg's
+// wave cycles, profiles/r05zz4_legs_lds_stalls.txt: dropout_kernel, flip_step_kernel).  Kernels that take one
+// unit per thread compute the same word with ph_word; the hot ones give a thread the four units of one call.
+__device__ __forceinline__ uint32_t ph_pick(const uint4& r, int k) {
+  return k == 0 ? r.x : k == 1 ? r.y : k == 2 ? r.z : r.w;
+}
+__device__ __forceinline__ uint32_t ph_word(uint64_t seed, uint64_t step, uint64_t g) {
+  return ph_pick(gmr::Philox::gen(seed, step, g >> 2), (int)(g & 3));
+}
+// quads of global units covering the local units [0, n) whose global index is base + u
+__host__ __device__ __forceinline__ int64_t ph_quads(int64_t base, int64_t n) { return ((base + n + 3) >> 2) - (base >> 2); }
+
 // ----------------------------------------------------------------- schedule (get_cum, :480-498)
 // tables: [gamma_cum (T) | eps_cum (T) | pos_weight | sparsity]; fp32 op order of the reference
 // (no contraction), linspace as ATen's CPU kernel (start + step*i below the midpoint, end - step*(T-1-i) above).
@@ -61,25 +75,35 @@ __global__ void flip_schedule_kernel(int B, const int* __restrict__ users, const
 }
 
 // x_t = x0 xor Bernoulli(sigmoid((a_t - u) * temp)), a_t = gamma_cum[t] (x0 == 0) or eps_cum[t] (x0 == 1)
+// Draws: unit g = (row0 + b) I + i takes words 2 (g % 2), 2 (g % 2) + 1 of Philox(seed, step, g / 2) (two units
+// per call; each needs two words).  A thread takes the two units of one call.
 __global__ void flip_qsample_kernel(int B, int I, const float* __restrict__ x0, int64_t ld0, const int* __restrict__ t,
                                     int t_const, const float* __restrict__ tab, int T, float temp,
                                     const uint8_t* __restrict__ flip, int64_t ldf, uint64_t seed, uint64_t step,
                                     int64_t row0, float* __restrict__ xt, int64_t ldt) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)B * I) return;
-  const int b = (int)(gid / I), i = (int)(gid % I);
-  const float x = x0[(int64_t)b * ld0 + i];
-  bool f;
-  if (flip) {
-    f = flip[(int64_t)b * ldf + i] != 0;
-  } else {
-    const int tt = t ? t[b] : t_const;
-    const float a = x == 0.f ? tab[tt] : tab[T + tt];
-    const uint4 r = gmr::Philox::gen(seed, step, (uint64_t)((row0 + b) * I + i));
-    const float p = sigm((a - unit01(r.x)) * temp);
-    f = unit01(r.y) < p;
+  const int64_t n = (int64_t)B * I, base = row0 * I;
+  const int64_t q = (base >> 1) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t u0 = (q << 1) - base;
+  if (u0 >= n) return;
+  uint4 r = make_uint4(0u, 0u, 0u, 0u);
+  if (!flip) r = gmr::Philox::gen(seed, step, (uint64_t)q);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int64_t u = u0 + k;
+    if (u < 0 || u >= n) continue;
+    const int b = (int)((uint32_t)u / (uint32_t)I), i = (int)(u - (int64_t)b * I);
+    const float x = x0[(int64_t)b * ld0 + i];
+    bool f;
+    if (flip) {
+      f = flip[(int64_t)b * ldf + i] != 0;
+    } else {
+      const int tt = t ? t[b] : t_const;
+      const float a = x == 0.f ? tab[tt] : tab[T + tt];
+      const float p = sigm((a - unit01(k ? r.z : r.x)) * temp);
+      f = unit01(k ? r.w : r.y) < p;
+    }
+    xt[(int64_t)b * ldt + i] = f ? 1.f - x : x;
   }
-  xt[(int64_t)b * ldt + i] = f ? 1.f - x : x;
 }
 
 // p_sample step on the model logits: probs = sigmoid(z); x = Bernoulli(p1 / (p0 + p1)) with
@@ -89,26 +113,30 @@ __global__ void flip_step_kernel(int B, int I, const float* __restrict__ z, int6
                                  int T, int qi, int last, const uint8_t* __restrict__ draws, int64_t ldd, uint64_t seed,
                                  uint64_t step, int64_t row0, float* __restrict__ x, int64_t ldx,
                                  float* __restrict__ probs, int64_t ldp) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (int64_t)B * I) return;
-  const int b = (int)(gid / I), i = (int)(gid % I);
-  const float p = sigm(z[(int64_t)b * ldz + i]);
-  if (probs) probs[(int64_t)b * ldp + i] = p;
-  float q = p;
-  if (!last) {
-    const float a0 = tab[qi], a1 = tab[T + qi];
-    const float p0 = p * (1.f - a0) + (1.f - p) * a1;
-    const float p1 = p * a0 + (1.f - p) * (1.f - a1);
-    q = p1 / (p0 + p1);
+  // unit g = (row0 + b) I + i: word g % 4 of Philox(seed, step, g / 4); a thread takes the four units of one call
+  const int64_t n = (int64_t)B * I, base = row0 * I;
+  const int64_t qd = (base >> 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t u0 = (qd << 2) - base;
+  if (u0 >= n) return;
+  uint4 r = make_uint4(0u, 0u, 0u, 0u);
+  if (!draws) r = gmr::Philox::gen(seed, step, (uint64_t)qd);
+  const float a0 = tab[qi], a1 = tab[T + qi];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t u = u0 + k;
+    if (u < 0 || u >= n) continue;
+    const int b = (int)((uint32_t)u / (uint32_t)I), i = (int)(u - (int64_t)b * I);
+    const float p = sigm(z[(int64_t)b * ldz + i]);
+    if (probs) probs[(int64_t)b * ldp + i] = p;
+    float q = p;
+    if (!last) {
+      const float p0 = p * (1.f - a0) + (1.f - p) * a1;
+      const float p1 = p * a0 + (1.f - p) * (1.f - a1);
+      q = p1 / (p0 + p1);
+    }
+    const float v = draws ? (draws[(int64_t)b * ldd + i] ? 1.f : 0.f) : (unit01(ph_pick(r, k)) < q ? 1.f : 0.f);
+    x[(int64_t)b * ldx + i] = v;
   }
-  float v;
-  if (draws) {
-    v = draws[(int64_t)b * ldd + i] ? 1.f : 0.f;
-  } else {
-    const uint4 r = gmr::Philox::gen(seed, step, (uint64_t)((row0 + b) * I + i));
-    v = unit01(r.x) < q ? 1.f : 0.f;
-  }
-  x[(int64_t)b * ldx + i] = v;
 }
 
 // per row: bce_row = sum_i (1-y) z - lw logsigmoid(z), lw = 1 + (pw-1) y (ATen's
@@ -345,7 +373,32 @@ __global__ void dropout_kernel(int64_t rows, int D, int group, const float* __re
                                float p_keep, const uint8_t* __restrict__ mask_in, uint8_t* __restrict__ mask_out,
                                int64_t ldm, uint64_t seed, uint64_t step, int64_t row0, float* __restrict__ y,
                                int64_t ldy) {
+  // draw unit g = (row0 + r) (D / group) + c / group (ph_word); group 1: a thread takes the four units of one call
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (group == 1) {
+    const int64_t n = rows * D, base = row0 * D;
+    const int64_t qd = (base >> 2) + gid;
+    const int64_t u0 = (qd << 2) - base;
+    if (u0 >= n) return;
+    uint4 rr = make_uint4(0u, 0u, 0u, 0u);
+    if (!mask_in) rr = gmr::Philox::gen(seed, step, (uint64_t)qd);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t u = u0 + q;
+      if (u < 0 || u >= n) continue;
+      const int64_t r = (uint32_t)u / (uint32_t)D;  // rows * D < 2^31 (checked at launch)
+      const int c = (int)(u - r * D);
+      bool k;
+      if (mask_in) {
+        k = mask_in[r * ldm + c] != 0;
+      } else {
+        k = unit01(ph_pick(rr, q)) < p_keep;
+        if (mask_out) mask_out[r * ldm + c] = k ? 1 : 0;
+      }
+      y[r * ldy + c] = k ? x[r * ldx + c] / p_keep : 0.f;
+    }
+    return;
+  }
   if (gid >= rows * D) return;
   const int64_t r = gid / D;
   const int c = (int)(gid % D);
@@ -354,8 +407,7 @@ __global__ void dropout_kernel(int64_t rows, int D, int group, const float* __re
   if (mask_in) {
     k = mask_in[r * ldm + mc] != 0;
   } else {
-    const uint4 rr = gmr::Philox::gen(seed, step, (uint64_t)((row0 + r) * (D / group) + mc));
-    k = unit01(rr.x) < p_keep;
+    k = unit01(ph_word(seed, step, (uint64_t)((row0 + r) * (D / group) + mc))) < p_keep;
     if (mask_out && c % group == 0) mask_out[r * ldm + mc] = k ? 1 : 0;
   }
   y[r * ldy + c] = k ? x[r * ldx + c] / p_keep : 0.f;
@@ -384,7 +436,7 @@ __global__ void xattn_table_kernel(int L, int D, int nhead, const float* __restr
 }
 
 // one row per block: the row's nhead keep flags (the head-dropout draw of dropout_kernel, group D / nhead:
-// Philox counter (row0 + r) * nhead + h) or the given mask, then CA[r][j] = sum_h keep P[h][j] + b_o[j]
+// draw unit (row0 + r) * nhead + h, ph_word) or the given mask, then CA[r][j] = sum_h keep P[h][j] + b_o[j]
 __global__ void __launch_bounds__(256) xattn_fwd_kernel(int D, int nhead, const float* __restrict__ P,
                                                         const float* __restrict__ bo, float p_keep,
                                                         const uint8_t* __restrict__ mask_in, uint8_t* __restrict__ mask_out,
@@ -398,8 +450,7 @@ __global__ void __launch_bounds__(256) xattn_fwd_kernel(int D, int nhead, const 
     if (mask_in) {
       k = mask_in[r * ldm + h] != 0;
     } else {
-      const uint4 rr = gmr::Philox::gen(seed, step, (uint64_t)((row0 + r) * nhead + h));
-      k = unit01(rr.x) < p_keep;
+      k = unit01(ph_word(seed, step, (uint64_t)((row0 + r) * nhead + h))) < p_keep;
       if (mask_out) mask_out[r * ldm + h] = k ? 1 : 0;
     }
     kf[h] = k ? 1.f : 0.f;
@@ -536,7 +587,9 @@ extern "C" int gmr_flip_qsample(int32_t B, int32_t I, const float* x0, int64_t l
                                 uint64_t seed, uint64_t step, int64_t row0, float* xt, int64_t ldt, void* stream) {
   GMR_ARG(x0 && tables && xt && B > 0 && I > 0 && row0 >= 0, "bad args");
   GMR_ARG(t || (t_const >= 0 && t_const < T), "bad t");
-  hipLaunchKernelGGL(flip_qsample_kernel, dim3(gmr::grid_for((int64_t)B * I, 256)), dim3(256), 0, (hipStream_t)stream,
+  GMR_ARG((int64_t)B * I < (1ll << 31), "B * I too large");
+  const int64_t npairs = ((row0 * I + (int64_t)B * I + 1) >> 1) - ((row0 * I) >> 1);
+  hipLaunchKernelGGL(flip_qsample_kernel, dim3(gmr::grid_for(npairs, 256)), dim3(256), 0, (hipStream_t)stream,
                      B, I, x0, ld0, t, t_const, tables, T, temp, flip, ld_flip, seed, step, row0, xt, ldt);
   GMR_LAUNCHED();
   return GMR_OK;
@@ -546,7 +599,9 @@ extern "C" int gmr_flip_step(int32_t B, int32_t I, const float* z, int64_t ldz, 
                              int32_t qi, int32_t last, const uint8_t* draws, int64_t ldd, uint64_t seed, uint64_t step,
                              int64_t row0, float* x, int64_t ldx, float* probs, int64_t ldp, void* stream) {
   GMR_ARG(z && tables && x && B > 0 && I > 0 && qi >= 0 && qi < T && row0 >= 0, "bad args");
-  hipLaunchKernelGGL(flip_step_kernel, dim3(gmr::grid_for((int64_t)B * I, 256)), dim3(256), 0, (hipStream_t)stream, B,
+  GMR_ARG((int64_t)B * I < (1ll << 31), "B * I too large");
+  hipLaunchKernelGGL(flip_step_kernel, dim3(gmr::grid_for(ph_quads(row0 * I, (int64_t)B * I), 256)), dim3(256), 0,
+                     (hipStream_t)stream, B,
                      I, z, ldz, tables, T, qi, last, draws, ldd, seed, step, row0, x, ldx, probs, ldp);
   GMR_LAUNCHED();
   return GMR_OK;
@@ -662,7 +717,9 @@ extern "C" int gmr_dropout_f32(int64_t rows, int32_t D, int32_t group, const flo
                                int64_t row0, float* y, int64_t ldy, void* stream) {
   GMR_ARG(x && y && rows > 0 && D > 0 && group >= 1 && D % group == 0 && row0 >= 0, "bad args");
   GMR_ARG(p_keep > 0.f && p_keep <= 1.f, "p_keep in (0, 1]");
-  hipLaunchKernelGGL(dropout_kernel, dim3(gmr::grid_for(rows * D, 256)), dim3(256), 0, (hipStream_t)stream, rows, D,
+  GMR_ARG(rows * D < (1ll << 31), "rows * D too large");
+  const int64_t nthreads = group == 1 ? ph_quads(row0 * D, rows * D) : rows * D;
+  hipLaunchKernelGGL(dropout_kernel, dim3(gmr::grid_for(nthreads, 256)), dim3(256), 0, (hipStream_t)stream, rows, D,
                      group, x, ldx, p_keep, mask_in, mask_out, ldm, seed, step, row0, y, ldy);
   GMR_LAUNCHED();
   return GMR_OK;

@@ -25,10 +25,12 @@ def _x(B, I, seed):
     return x
 
 
-@pytest.mark.parametrize("B,row0,keep", [(300, 0, 0.8), (37, 1000, 0.5), (2048, 5, 0.9)])
-def test_layernorm_drop_fwd_equals_mask_then_layernorm(B, row0, keep):
+@pytest.mark.parametrize("B,row0,keep,skew", [(300, 0, 0.8, 0), (37, 1000, 0.5, 0), (2048, 5, 0.9, 0),
+                                               (300, 3, 0.8, 77), (37, 0, 0.5, 255)])
+def test_layernorm_drop_fwd_equals_mask_then_layernorm(B, row0, keep, skew):
     """gmr_layernorm_drop_fwd (the residual-branch dropout drawn inside the LayerNorm kernel) against
-    gmr_keep_mask_u8 + gmr_layernorm_fwd with the same Philox key: keep bytes, y, s, mean and rstd bit for bit."""
+    gmr_keep_mask_u8 + gmr_layernorm_fwd with the same Philox key: keep bytes, y, s, mean and rstd bit for bit.
+    skew != 0 starts the draw counter off a 256-unit block (the per-column path of the kernel's draws)."""
     from gmr import _lib
     from gmr.kernels import ptr, stream
     D = 512
@@ -43,10 +45,10 @@ def test_layernorm_drop_fwd_equals_mask_then_layernorm(B, row0, keep):
         y, s = torch.empty((B, D), device=DEV), torch.empty((B, D), device=DEV)
         mean, rstd = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
         if fused:
-            _lib.call("gmr_layernorm_drop_fwd", B, D, ptr(a), D, ptr(b), D, keep, 11, 1234, row0 * D, ptr(m), D,
+            _lib.call("gmr_layernorm_drop_fwd", B, D, ptr(a), D, ptr(b), D, keep, 11, 1234, row0 * D + skew, ptr(m), D,
                       1.0 / keep, ptr(w), ptr(bs), 1e-5, 0, ptr(y), D, ptr(s), D, ptr(mean), ptr(rstd), stream())
         else:
-            _lib.call("gmr_keep_mask_u8", B * D, keep, 11, 1234, row0 * D, ptr(m), stream())
+            _lib.call("gmr_keep_mask_u8", B * D, keep, 11, 1234, row0 * D + skew, ptr(m), stream())
             _lib.call("gmr_layernorm_fwd", B, D, ptr(a), D, ptr(b), D, ptr(m), D, 1.0 / keep, ptr(w), ptr(bs), 1e-5, 0,
                       ptr(y), D, ptr(s), D, ptr(mean), ptr(rstd), stream())
         res.append([t.cpu() for t in (m, y, s, mean, rstd)])
@@ -93,3 +95,48 @@ def test_native_layer_issue_bit_identical(train, B, L, row0, monkeypatch):
         runs.append(r)
     for k in runs[0]:
         np.testing.assert_array_equal(runs[1][k].view(np.uint8), runs[0][k].view(np.uint8), err_msg=k)
+
+
+@pytest.mark.parametrize("a", [1, 2, 3, 5, 150])
+def test_draw_kernels_row_split_invariant(a):
+    """Round 6: the per-element Bernoulli kernels take four draws per Philox call (two for flip_qsample), keyed
+    by the GLOBAL unit index; a row split at any row (row0 = a, so the quads / pairs start unaligned) draws what
+    the whole call drew: dropout masks and outputs (group 1 and the head group), flip_step samples, flip_qsample
+    flips, bit for bit; the keep rates stay Bernoulli(p) (binomial bound)."""
+    from gmr import _lib
+    from gmr.kernels import ptr, stream
+    torch.manual_seed(3)
+    R, D, I, T = 301, 136, 1003, 10
+    x = torch.randn(R, D, device="cuda")
+    for group in (1, 17):
+        y = torch.empty_like(x)
+        m = torch.empty((R, D // group), dtype=torch.uint8, device="cuda")
+        _lib.call("gmr_dropout_f32", R, D, group, ptr(x), D, 0.7, None, ptr(m), m.stride(0), 99, 5, 0, ptr(y), D,
+                  stream())
+        y2 = torch.empty_like(x)
+        m2 = torch.empty_like(m)
+        for lo, hi in ((0, a), (a, R)):
+            _lib.call("gmr_dropout_f32", hi - lo, D, group, ptr(x[lo:]), D, 0.7, None, ptr(m2[lo:]), m2.stride(0), 99,
+                      5, lo, ptr(y2[lo:]), D, stream())
+        assert torch.equal(m, m2) and torch.equal(y, y2), group
+        kr = m.float().mean().item()
+        n = m.numel()
+        assert abs(kr - 0.7) < 5 * (0.21 / n) ** 0.5, (group, kr)
+    tab = torch.linspace(0.05, 0.6, 2 * T + 2, device="cuda")
+    z = torch.randn(R, I, device="cuda")
+    xs, xs2 = torch.empty_like(z), torch.empty_like(z)
+    _lib.call("gmr_flip_step", R, I, ptr(z), I, ptr(tab), T, 3, 0, None, 0, 7, 2, 0, ptr(xs), I, None, 0, stream())
+    for lo, hi in ((0, a), (a, R)):
+        _lib.call("gmr_flip_step", hi - lo, I, ptr(z[lo:]), I, ptr(tab), T, 3, 0, None, 0, 7, 2, lo, ptr(xs2[lo:]), I,
+                  None, 0, stream())
+    assert torch.equal(xs, xs2)
+    x0 = (torch.rand(R, I, device="cuda") < 0.1).float()
+    t = torch.randint(0, T, (R,), dtype=torch.int32, device="cuda")
+    xt, xt2 = torch.empty_like(x0), torch.empty_like(x0)
+    _lib.call("gmr_flip_qsample", R, I, ptr(x0), I, ptr(t), 0, ptr(tab), T, 4.0, None, 0, 7, 3, 0, ptr(xt), I,
+              stream())
+    for lo, hi in ((0, a), (a, R)):
+        _lib.call("gmr_flip_qsample", hi - lo, I, ptr(x0[lo:]), I, ptr(t[lo:]), 0, ptr(tab), T, 4.0, None, 0, 7, 3, lo,
+                  ptr(xt2[lo:]), I, stream())
+    assert torch.equal(xt, xt2)
+    assert 0 < (xt != x0).float().mean().item() < 1
