@@ -56,9 +56,11 @@ X6_PEAK_TFS = round(2516.6 / 6, 1)
 KERNEL_NAMES = {"gemm": "gemm_glds_kernel (fp32 MFMA v_mfma_f32_32x32x2_f32, global_load_lds staging, XCD-aware tiles)",
                 "gemm_x6": "gemm_x6_kernel (fp32 operands split exactly into three bf16 terms on the "
                            "way into LDS, six "
-                           "v_mfma_f32_32x32x16_bf16 products accumulated in fp32: fp32-accurate NT products)",
-                "infonce": "cl6_kernel rows + table passes (fused InfoNCE on the split-bf16 pipe: fp32 operands split "
-                           "exactly into three bf16 terms, six v_mfma_f32_32x32x16_bf16 products, fp32 accumulation)",
+                           "v_mfma_f32_32x32x16_bf16 products accumulated in fp32, hi*hi and the five small "
+                           "products in separate accumulators: fp32-accurate, unbiased NT products)",
+                "infonce": "cl6p_kernel rows + table passes (fused InfoNCE on the split-bf16 pipe: fp32 operands split "
+                           "exactly into three bf16 terms; logits on six v_mfma_f32_32x32x16_bf16 products, the "
+                           "gradient-only E T products on three; fp32 accumulation)",
                 "infonce_f32": "cl_rows_kernel + cl_table_kernel (fused InfoNCE, fp32 MFMA)",
                 "spmm": "spmm_side_kernel (bipartite side x 32-column slice per XCD, lane-group entry-stream tasks, "
                         "wave hub blocks combined in-launch) + spmm_lane_kernel for the non-bipartite graphs"}
