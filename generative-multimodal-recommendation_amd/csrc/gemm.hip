@@ -765,7 +765,7 @@ extern "C" int gmr_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t
   GMR_ARG(A && B && C, "null operand");
   GMR_ARG(M > 0 && N > 0 && K > 0, "empty GEMM");
   GMR_ARG(lda >= (trans_a ? M : K) && ldb >= (trans_b ? K : N) && ldc >= N, "leading dimension too small");
-  GMR_ARG(epilogue >= GMR_EPI_NONE && epilogue <= GMR_EPI_LEAKY_NORM, "bad epilogue");
+  GMR_ARG(epilogue >= GMR_EPI_NONE && epilogue <= GMR_EPI_SCALE_BIAS, "bad epilogue");
   GMR_ARG(epilogue != GMR_EPI_LEAKY_NORM ||
               (N == 64 && aux && rowvec1 && ld_aux >= 64 && ld_aux % 4 == 0 && ldc % 4 == 0 &&
                (((uintptr_t)aux | (uintptr_t)C) & 15) == 0),

@@ -59,6 +59,8 @@ __device__ __forceinline__ float epi_fin(const Epi& e, float acc, float b, float
       return fmaxf(v + b, 0.f);
     case GMR_EPI_DRELU:
       return x > 0.f ? v : 0.f;
+    case GMR_EPI_SCALE_BIAS:  // = POSTERIOR with c2 = 0: c1 (v + b) + 0 x rounds once, like c1 (v + b)
+      return e.slope * (v + b);
     default:
       return v;
   }

@@ -164,9 +164,14 @@ class Denoiser(nn.Module):
         return out
 
     def posterior_step(self, h, x, c1, c2):
-        """x <- c1 * (h @ W2^T + b2) + c2 * x (in place; GaussianDiffusion.p_mean_variance mean)."""
-        K.gemm(h, self.slab.view("W2"), x, trans_b=True, epi=K.EPI_POSTERIOR, bias=self.slab.view("b2"), aux=x,
-               slope=c1, beta=c2)
+        """x <- c1 * (h @ W2^T + b2) + c2 * x (in place; GaussianDiffusion.p_mean_variance mean).  c2 == 0 (the
+        last step, t = 0): the same values without reading x (GMR_EPI_SCALE_BIAS), so x need not hold anything."""
+        if c2 == 0.0:
+            K.gemm(h, self.slab.view("W2"), x, trans_b=True, epi=K.EPI_SCALE_BIAS, bias=self.slab.view("b2"),
+                   slope=c1)
+        else:
+            K.gemm(h, self.slab.view("W2"), x, trans_b=True, epi=K.EPI_POSTERIOR, bias=self.slab.view("b2"), aux=x,
+                   slope=c1, beta=c2)
         return x
 
     def slab_head_words(self):

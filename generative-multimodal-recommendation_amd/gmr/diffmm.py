@@ -691,8 +691,11 @@ class DiffMM(GeneralRecommender):
         assert B <= w["B"]
         x, h = w["x"][:B], w["h"][:B]
         users = w["users"][users_lo:users_hi]
-        _lib.call("gmr_diff_densify", B, I, ptr(users), ptr(self.user_ptr), ptr(self.user_items), ptr(x),
-                  x.stride(0), stream())
+        if not dn.PSAMPLE_FOLD:  # the folded chain reads the histories as item lists and its last product
+            # (GMR_EPI_SCALE_BIAS) overwrites x without reading it: no densified copy (rebuild 8.5 -> 7.8 ms per
+            # epoch, profiles/r06n_psample_scale_bias_ab.txt)
+            _lib.call("gmr_diff_densify", B, I, ptr(users), ptr(self.user_ptr), ptr(self.user_items), ptr(x),
+                      x.stride(0), stream())
         EB, _, _ = den.time_bias(T)
         if not w1t_fresh:
             den.refresh_w1t()

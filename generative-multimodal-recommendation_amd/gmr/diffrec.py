@@ -227,8 +227,11 @@ class DiffRec(GeneralRecommender):
         w = self._dwork(B)
         I, T = self.n_items, self.steps
         x, h = w["x"][:B], w["h"][:B]
-        _lib.call("gmr_diff_densify", B, I, ptr(users), ptr(self.user_ptr), ptr(self.user_items), ptr(x),
-                  x.stride(0), stream())
+        if not dn.PSAMPLE_FOLD:  # the folded chain reads the histories as item lists and its last product
+            # (GMR_EPI_SCALE_BIAS) overwrites x without reading it: no densified copy (rebuild 8.5 -> 7.8 ms per
+            # epoch, profiles/r06n_psample_scale_bias_ab.txt)
+            _lib.call("gmr_diff_densify", B, I, ptr(users), ptr(self.user_ptr), ptr(self.user_items), ptr(x),
+                      x.stride(0), stream())
         EB, _, _ = den.time_bias(T)
         den.refresh_w1t()
         xi = x[:, :I]

@@ -13,6 +13,7 @@ from . import _lib
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_TANH, EPI_LEAKY, EPI_POSTERIOR, EPI_DTANH, EPI_ROWSCALE_AUX, EPI_BIAS_RELU, EPI_DRELU = range(9)
 EPI_LEAKY_NORM = 9  # leaky + row normalisation in the split-K reduce: aux = normalised rows, rv1 = norms (written)
+EPI_SCALE_BIAS = 10  # slope * (acc + bias): the posterior with c2 = 0, no aux read
 
 _ws = {}
 

@@ -52,6 +52,8 @@ extern "C" {
                                   reduce: aux (WRITTEN, ld_aux) = C[m] / max(|C[m]|, 1e-12), rowvec1 (WRITTEN) = that
                                   norm; N = 64 plans with split-K only (DiffMM modality projection + F.normalize,
                                   models/diffmm.py:115-127, 138-149) */
+#define GMR_EPI_SCALE_BIAS 10  /* C = slope*(alpha*acc + bias): POSTERIOR with c2 = 0 without reading aux, bit for
+                                  bit (the last p_sample step, t = 0, whose posterior mean is the x0 prediction) */
 
 const char* gmr_last_error_string(void);
 int gmr_version(void);
