@@ -333,6 +333,20 @@ def test_topk_rows_vs_oracle(K, k):
     assert np.array_equal(out.cpu().numpy(), eval_ref.topk_rows(S, k))
 
 
+@pytest.mark.parametrize("col0,n_cols", [(0, 7050), (0, 7051), (1, 7049), (3, 64)])
+def test_argmax_rows_vector_and_tail_paths(K, col0, n_cols):
+    """k = 1 (argmax_rows_kernel): the 16-byte-row path (four columns per load, round 6) and the scalar path
+    (rows not 16-byte aligned), with ragged widths, exact ties (lowest index wins) and -1e10 blocks."""
+    rng = _rng(43)
+    S = rng.standard_normal((97, 7056)).astype(np.float32)
+    S[:, ::3] = np.float32(2.5)
+    S[4, :] = np.float32(-1e10)
+    Sd = _dev(S)[:, col0:col0 + n_cols]
+    out = torch.empty((97, 1), dtype=torch.int32, device=DEV)
+    K.topk_rows(Sd, 1, out)
+    assert np.array_equal(out.cpu().numpy(), eval_ref.topk_rows(S[:, col0:col0 + n_cols], 1))
+
+
 def test_mask_and_topk_golden(K, golden):
     g = golden("diffmm_tiny")
     s = _dev(g["eval_scores_raw"])
@@ -1058,3 +1072,24 @@ def test_spmm_side_multi_outputs_and_jobs(K):
     gl.spmm(rb, [(X[:, :64],), (X[:, 64:128],)])
     assert torch.equal(ya.view(torch.int32), ra.view(torch.int32))
     assert torch.equal(yb.view(torch.int32), rb.view(torch.int32))
+
+
+
+@pytest.mark.parametrize("tile", [0, 1 << 27, 1 << 26])
+@pytest.mark.parametrize("M,N,Kd", [(300, 7050, 1000), (64, 130, 70), (2048, 1000, 1000)])
+def test_gemm_scale_bias_equals_posterior_c2_zero(K, M, N, Kd, tile):
+    """GMR_EPI_SCALE_BIAS (round 6; the last p_sample step) = GMR_EPI_POSTERIOR with c2 = 0 bit for bit, on the
+    default plan, the fp32-input kernel and the split-bf16 kernel (split-K plans included), without reading aux:
+    the SCALE_BIAS output buffer starts as NaN."""
+    torch.manual_seed(7)
+    A = torch.randn(M, Kd, device=DEV)
+    B = torch.randn(N, Kd, device=DEV)
+    bias = torch.randn(N, device=DEV)
+    aux = (torch.rand(M, N, device=DEV) < 0.3).float()
+    C1 = aux.clone()
+    K.gemm(A, B, C1, trans_b=True, epi=K.EPI_POSTERIOR, bias=bias, aux=C1, slope=0.37, beta=0.0, tile=tile)
+    C2 = torch.full((M, N), float("nan"), device=DEV)
+    K.gemm(A, B, C2, trans_b=True, epi=K.EPI_SCALE_BIAS, bias=bias, slope=0.37, tile=tile)
+    torch.cuda.synchronize()
+    assert torch.isfinite(C2).all()
+    assert torch.equal(C1, C2)
