@@ -1252,10 +1252,11 @@ __global__ void cl_table_reduce_nbwd_kernel(int n, int nc, const float* __restri
 
 // ---------------------------------------------------------------------------------------------
 // The same two passes on the bf16 matrix cores (GMR_CL_X6, default): every fp32 operand is split
-// exactly into three bf16 terms (hi + mid + lo, as gemm_x6.hip) and each 32 x 32 x 16 product is
+// exactly into three bf16 terms (hi + mid + lo, as gemm_x6.hip) and each 32 x 32 x 16 logits product is
 // accumulated in fp32 from six v_mfma_f32_32x32x16_bf16 (hi.hi + hi.mid + mid.hi + hi.lo + lo.hi +
-// mid.mid; the dropped terms are below 2^-23 |ab|), so S, E and U keep fp32 accuracy at 6 x 32 cycles
-// per 32 x 32 x 16 block instead of 8 x 64 on v_mfma_f32_32x32x2_f32.
+// mid.mid; the dropped terms are below 2^-23 |ab|), so S and E keep fp32 accuracy at 6 x 32 cycles
+// per 32 x 32 x 16 block instead of 8 x 64 on v_mfma_f32_32x32x2_f32; the gradient-only products U = E T take
+// three (c6_mfma3, round 6).
 // Per staged 32-row block the workgroup converts the fp32 rows once into LDS as three row-major bf16
 // planes [32 rows][64 d] (A operand of S^T = Stg F^T) and three transposed planes [64 d][32 slots]
 // (A operand of Y^T += Stg^T E^T), slots permuted so that the 8 staged rows a lane half feeds to one

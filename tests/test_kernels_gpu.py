@@ -541,6 +541,41 @@ def test_contrast_rows_in_place_bit_exact(K, B, n, monkeypatch):
         monkeypatch.setenv(env, "1")
 
 
+@pytest.mark.parametrize("B,n", [(2048, 19445), (2048, 7050), (300, 1000), (37, 100)])
+def test_contrast_nbwd_pipelined_bit_exact(K, B, n, monkeypatch):
+    """gmr_contrast_fused_nbwd_f32 (DiffMM's form: dT through the table view's normalize backward) on the pipelined
+    passes against the unpipelined ones: loss, dP and dT bit for bit, with P given and P = NULL (rows read in
+    place)."""
+    from gmr import _lib
+    from gmr.kernels import ptr, stream
+    monkeypatch.setenv("GMR_CL_X6", "1")
+    rng = _rng(15)
+    off = 3
+    C = rng.standard_normal((off + n + 2, 128)).astype(np.float32)
+    C /= np.linalg.norm(C, axis=1, keepdims=True)
+    nodes = rng.integers(0, n, B).astype(np.int32)
+    Cd, nd = _dev(C), _dev(nodes)
+    nrm = _dev(rng.uniform(0.5, 2.0, n + 8).astype(np.float32))
+    P = torch.empty((B, 64), device=DEV)
+    K.gather_rows(Cd[:, :64], nd, P, off=off)
+    ws = K.contrast_workspace(B, n, DEV, "test_cl_nbwd")
+    T = Cd[off:off + n, 64:]
+    outs = []
+    for pipe, p in (("0", P), ("1", P), ("1", None)):
+        monkeypatch.setenv("GMR_CL_PIPE", pipe)
+        loss = torch.empty(B, device=DEV)
+        contrib = torch.empty((B, 128), device=DEV)
+        dt = torch.full((n, 128), float("nan"), device=DEV)
+        _lib.call("gmr_contrast_fused_nbwd_f32", B, n, ptr(p), 64 if p is not None else 128, ptr(T), 128, ptr(Cd),
+                  ptr(nd), off, 5.0, 0.01 / B, ptr(loss), ptr(contrib), 128, ptr(dt[:, 64:]), 128, ptr(T), 128,
+                  ptr(nrm), ptr(ws), ws.numel(), stream())
+        outs.append((loss.cpu(), contrib.cpu(), dt[:, 64:].cpu()))
+    assert torch.isfinite(outs[0][2]).all()
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+
+
 def _contrast_env_bit_exact(K, B, n, monkeypatch, env, repeats=1, value="1"):
     monkeypatch.setenv("GMR_CL_X6", "1")
     rng = _rng(13)
